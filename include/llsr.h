@@ -1,0 +1,158 @@
+/* llsr.h — C-ABI of the MI355X-native LeGO-LOAM-SR per-scan hot path.
+ *
+ * Drop-in boundary for the reference's ImageProjection → FeatureAssociation handoff
+ * (LeGO-LOAM/src/imageProjection.cpp:189-222 cloudHandler, featureAssociation.cpp:2742-2778
+ * runFeatureAssociation feature stage; stage types utility.h:63-83, cloud_msgs/msg/CloudInfo.msg).
+ * The reference has no FFI of its own; these entry points replace the arithmetic behind the
+ * node callbacks so a ROS2 shim keeps every topic and the Channel semantics.
+ *
+ * Conventions: plain C types only; int status codes (0 = OK, negative errno-style);
+ * llsr_last_error() gives text; no C++ exception crosses the ABI. A handle is single-threaded
+ * (one per pipeline/stream), matching the reference's one-thread-per-node layout.
+ * Caller owns every host buffer; device buffers live in the handle.
+ */
+#ifndef LLSR_H_
+#define LLSR_H_
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LLSR_ABI_VERSION 1
+
+#define LLSR_OK 0
+#define LLSR_EINVAL (-22)
+#define LLSR_ENOMEM (-12)
+#define LLSR_ENODEV (-19)
+#define LLSR_ERANGE (-34)
+#define LLSR_ENOSYS (-38)
+#define LLSR_EIO (-5)
+
+#define LLSR_LIDAR_VLP16 0
+#define LLSR_LIDAR_HDL64E 2
+
+#define LLSR_MODE_FAITHFUL 0
+#define LLSR_MODE_LM_APPLIED 1
+
+/* Mirrors the ROS2 parameters of the three nodes (loam_config.yaml:1-67 / 137-203;
+ * read at imageProjection.cpp:80-121, featureAssociation.cpp:112-154). Angles in degrees,
+ * exactly as in the YAML; the library applies the reference's conversions. */
+typedef struct llsr_config {
+  int32_t num_vertical_scans;      /* laser.num_vertical_scans   (H)          */
+  int32_t num_horizontal_scans;    /* laser.num_horizontal_scans (W)          */
+  float vertical_angle_bottom;     /* deg */
+  float vertical_angle_top;        /* deg */
+  float sensor_mount_angle;        /* deg (read but unused by groundRemovalOurs) */
+  int32_t ground_scan_index;
+  int32_t use_kitti;               /* ground angle D = 60/25 deg by row (IP:561-566) */
+  int32_t use_vlp32c;              /* must be 0: VLP-32c row-histogram branch is not built */
+  float segment_theta;             /* deg */
+  int32_t segment_valid_point_num;
+  int32_t segment_valid_line_num;
+  float scan_period;               /* s */
+  float edge_threshold;
+  float surf_threshold;
+  float nearest_feature_search_distance;
+  float DBFr;
+  float RatioXY;
+  float RatioZ;
+  int32_t mapping_frequency_divider;
+  int32_t iterCountThres;          /* map_optimization.mapping.iterCountThres */
+  float step_size;
+  float stop_thres;
+  int32_t mode;                    /* LLSR_MODE_* */
+} llsr_config;
+
+/* Fill *cfg with the YAML block for `lidar` (LLSR_LIDAR_VLP16 / LLSR_LIDAR_HDL64E). */
+int32_t llsr_config_default(llsr_config* cfg, int32_t lidar);
+
+/* Per-scan outputs of projection+segmentation (IP) and feature extraction (FA), in the
+ * reference's own order. Host buffers, caller-allocated; capacities from llsr_query_sizes().
+ * Any pointer may be NULL to skip that output. Counts are always written. */
+typedef struct llsr_scan_out {
+  /* ---- ImageProjection (IP) ---- */
+  int32_t n_points;            /* finite input points (after removeNaNFromPointCloud, IP:198) */
+  float orientation[3];        /* start, end, diff (CloudInfo.msg:6-8; IP:430-445) */
+  float* range_image;          /* [H*W] _range_mat, FLT_MAX where empty (IP:337)          */
+  int32_t* cell_point;         /* [H*W] raw-input index of the point kept in the cell, -1  */
+  int8_t* ground_image;        /* [H*W] _ground_mat after groundRemovalOurs (IP:522-774)  */
+  int32_t* label_image;        /* [H*W] _label_mat after cloudSegmentation (IP:776-931)   */
+  int32_t* start_ring_index;   /* [H] CloudInfo.start_ring_index (IP:794)                 */
+  int32_t* end_ring_index;     /* [H] CloudInfo.end_ring_index   (IP:831)                 */
+  int32_t n_segmented;         /* S */
+  float* seg_xyzi;             /* [4*S] _segmented_cloud (intensity = row + col/1e4)      */
+  uint8_t* seg_ground_flag;    /* [S] CloudInfo.segmented_cloud_ground_flag               */
+  uint32_t* seg_col_ind;       /* [S] CloudInfo.segmented_cloud_col_ind                   */
+  float* seg_range;            /* [S] CloudInfo.segmented_cloud_range                     */
+  float* seg_intensity;        /* [S] ProjectionOut.segmentedCloud_Intensity              */
+  int32_t n_outlier;           /* O */
+  float* outlier_xyzi;         /* [4*O] _outlier_cloud                                    */
+  float* outlier_intensity;    /* [O] ProjectionOut.outlierCloud_Intensity                */
+  int32_t n_near;              /* nearground_cloud size K (IP:700-715)                    */
+  int32_t n_ransac_inliers;    /* RANSAC inliers (IP:716-721)                             */
+  int32_t ransac_iterations;   /* PCL iterations_ after computeModel                      */
+  /* ---- FeatureAssociation feature stage (FA:2766-2775) ---- */
+  float* loam_xyzi;            /* [4*S] segmentedCloud after adjustDistortion (FA:565-789) */
+  float* curvature;            /* [S] cloudCurvature, defined on [5, S-5) (FA:817-848)     */
+  uint8_t* picked;             /* [S] cloudNeighborPicked after extractFeaturesOurs         */
+  int8_t* label;               /* [S] cloudLabel after extractFeaturesOurs                  */
+  int32_t n_less_sharp;        /* M */
+  int32_t* less_sharp_ind;     /* [M] cornerPointsLessSharp as segmented indices           */
+  int32_t* dbscan_cluster;     /* [M] DBSCAN_EdgeFeature cluster labels (FA:1318-1387)      */
+  int32_t n_sharp;
+  int32_t* sharp_ind;          /* cornerPointsSharp as segmented indices (FA:1299-1305)     */
+  int32_t n_flat;              /* surfPointsFlat WITHOUT the 160 shadow points               */
+  int32_t* flat_ind;           /* segmented indices; shadow points follow implicitly         */
+  int32_t n_less_flat;
+  float* less_flat_xyzi;       /* [4*L] surfPointsLessFlat (per-ring VoxelGrid 0.2, FA:1268) */
+} llsr_scan_out;
+
+typedef struct llsr_sizes {
+  int32_t cells;               /* H*W: bound for every per-point array */
+  int32_t rings;               /* H */
+  int32_t max_points;          /* input points per scan accepted by the handle */
+  int32_t shadow_points;       /* 160 virtual points (FA:412-450) */
+} llsr_sizes;
+
+typedef struct llsr_handle llsr_handle;
+
+/* Create a handle on HIP device `hip_device` able to process batches of up to `max_batch`
+ * scans of up to `max_points` raw points each. Fails with LLSR_ENODEV when no device or the
+ * HIP kernels are unavailable — there is no CPU fallback behind this ABI. */
+int32_t llsr_create(const llsr_config* cfg, int32_t hip_device, int32_t max_batch,
+                    int32_t max_points, llsr_handle** out);
+void llsr_destroy(llsr_handle* h);
+const char* llsr_last_error(const llsr_handle* h);
+int32_t llsr_query_sizes(const llsr_handle* h, llsr_sizes* out);
+/* Reset the per-slot FeatureAssociation carry-over state (FA:167-198: the H*W arrays that the
+ * reference sizes once and never clears). */
+int32_t llsr_reset_state(llsr_handle* h);
+
+/* One scan, host buffers in/out: the ImageProjection::cloudHandler + FeatureAssociation
+ * feature-stage replacement. `xyzi` holds n raw points (x,y,z,intensity, NaN allowed). */
+int32_t llsr_process_scan(llsr_handle* h, const float* xyzi, int32_t n, llsr_scan_out* out);
+
+/* Batched, device-resident: scans b = 0..B-1 are d_xyzi[d_offsets[b] .. d_offsets[b+1]),
+ * float4 records in HBM (B+1 int64 offsets, also in device memory). Slot b uses FA carry-over
+ * state b. Enqueued on `hip_stream` (hipStream_t, NULL = default stream); returns after
+ * enqueue. Results stay in the handle until the next call. */
+int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const int64_t* d_offsets,
+                           int32_t B, void* hip_stream);
+
+/* Copy slot b's results of the last batch into host buffers (synchronises the stream). */
+int32_t llsr_fetch_scan(llsr_handle* h, int32_t b, llsr_scan_out* out);
+
+/* Device-side counters of the last batch: per slot {n_points, S, O, M, n_sharp, F, L, K}.
+ * `out` must hold 8*B int32 (host). Synchronises. */
+int32_t llsr_batch_counts(llsr_handle* h, int32_t* out);
+
+/* Per-kernel timing of the last batch (HIP events on the handle's launch stream), in the
+ * order of llsr_kernel_name(k). Returns the number of kernels written (<= cap). */
+int32_t llsr_kernel_times_ms(llsr_handle* h, float* out, int32_t cap);
+const char* llsr_kernel_name(int32_t k);
+int32_t llsr_set_profiling(llsr_handle* h, int32_t enable);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LLSR_H_ */

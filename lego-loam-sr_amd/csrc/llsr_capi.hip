@@ -1,0 +1,413 @@
+// llsr_capi.hip — host side of the C-ABI (include/llsr.h): handle lifetime, the HBM buffer
+// pool, the per-batch launch sequence and result fetch. No C++ exception crosses the ABI.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/llsr.h"
+#include "llsr_device.h"
+
+namespace llsr {
+__global__ void k_project(DevCfg, const float4*, const int64_t*, DevBufs);
+__global__ void k_gather_column(DevCfg, const float4*, const int64_t*, DevBufs);
+__global__ void k_ground_add(DevCfg, DevBufs);
+__global__ void k_ground_elev_ransac(DevCfg, DevBufs);
+template <bool kLds> __global__ void k_label(DevCfg, DevBufs);
+__global__ void k_segment(DevCfg, const float4*, const int64_t*, DevBufs);
+__global__ void k_fa_points(DevCfg, DevBufs);
+__global__ void k_select_ring(DevCfg, DevBufs);
+__global__ void k_fa_finish(DevCfg, DevBufs);
+
+__global__ void k_init_counts(int* counts, int B) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  int* c = counts + b * kCnt;
+  for (int k = 0; k < kCnt; ++k) c[k] = 0;
+  c[C_FIRST] = INT_MAX;
+  c[C_LAST] = -1;
+}
+}  // namespace llsr
+
+using namespace llsr;
+
+namespace {
+const char* kKernelNames[] = {"init",          "k_project",    "k_gather_column", "k_ground_add",
+                              "k_ground_elev_ransac", "k_label", "k_segment",      "k_fa_points",
+                              "k_select_ring", "k_fa_finish"};
+constexpr int kNumKernels = 10;
+}  // namespace
+
+struct llsr_handle {
+  llsr_config cfg;
+  DevCfg dc;
+  int device = 0;
+  int max_batch = 0, max_points = 0;
+  DevBufs d{};
+  void* pool = nullptr;
+  size_t pool_bytes = 0;
+  float4* d_in = nullptr;      // single-scan staging
+  int64_t* d_off = nullptr;
+  hipStream_t stream = nullptr;
+  hipStream_t last_stream = nullptr;
+  int last_B = 0;
+  bool profiling = false;
+  hipEvent_t ev[kNumKernels + 1] = {};
+  float ktimes[kNumKernels] = {};
+  bool have_times = false;
+  std::string err;
+};
+
+static int32_t fail(llsr_handle* h, int32_t code, const std::string& msg) {
+  if (h) h->err = msg;
+  return code;
+}
+
+#define HIP_OK(h, expr)                                                                  \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return fail(h, LLSR_EIO, std::string(#expr ": ") + hipGetErrorString(e_));         \
+  } while (0)
+
+extern "C" int32_t llsr_config_default(llsr_config* c, int32_t lidar) {
+  if (!c) return LLSR_EINVAL;
+  std::memset(c, 0, sizeof *c);
+  if (lidar == LLSR_LIDAR_VLP16) {  // loam_config.yaml:1-67
+    c->num_vertical_scans = 16; c->num_horizontal_scans = 1800;
+    c->vertical_angle_bottom = -15.0f; c->vertical_angle_top = 15.0f;
+    c->ground_scan_index = 7; c->use_kitti = 0;
+    c->DBFr = 5.0f; c->RatioXY = 0.5f; c->RatioZ = 2.5f;
+    c->edge_threshold = 0.03f; c->surf_threshold = 0.03f; c->nearest_feature_search_distance = 5.0f;
+  } else if (lidar == LLSR_LIDAR_HDL64E) {  // loam_config.yaml:137-203
+    c->num_vertical_scans = 64; c->num_horizontal_scans = 1800;
+    c->vertical_angle_bottom = -24.8f; c->vertical_angle_top = 2.0f;
+    c->ground_scan_index = 50; c->use_kitti = 1;
+    c->DBFr = 7.5f; c->RatioXY = 0.3f; c->RatioZ = 5.0f;
+    c->edge_threshold = 0.005f; c->surf_threshold = 0.005f; c->nearest_feature_search_distance = 25.0f;
+  } else {
+    return LLSR_EINVAL;
+  }
+  c->sensor_mount_angle = 0.0f;
+  c->use_vlp32c = 0;
+  c->segment_theta = 60.0f; c->segment_valid_point_num = 5; c->segment_valid_line_num = 3;
+  c->scan_period = 0.1f;
+  c->mapping_frequency_divider = 1;
+  c->iterCountThres = 200; c->step_size = 1.0f; c->stop_thres = 0.05f;
+  c->mode = LLSR_MODE_FAITHFUL;
+  return LLSR_OK;
+}
+
+// Host-side constants with the reference's exact conversions (IP:117-121, 849; FA:152-154).
+static void make_devcfg(const llsr_config& c, DevCfg& d) {
+  const double kDegToRad = M_PI / 180.0;
+  d.H = c.num_vertical_scans;
+  d.W = c.num_horizontal_scans;
+  d.HW = d.H * d.W;
+  d.ip_resX = (float)((M_PI * 2) / d.W);
+  d.ip_resY = (float)(kDegToRad * (c.vertical_angle_top - c.vertical_angle_bottom) / float(d.H - 1));
+  d.ip_angBottom = (float)(-(c.vertical_angle_bottom - 0.1) * kDegToRad);
+  const float segTheta = (float)(c.segment_theta * kDegToRad);
+  d.segThr = std::tan(segTheta);
+  d.sinX = std::sin(d.ip_resX); d.cosX = std::cos(d.ip_resX);
+  d.sinY = std::sin(d.ip_resY); d.cosY = std::cos(d.ip_resY);
+  d.use_kitti = c.use_kitti;
+  d.gsi = c.ground_scan_index;
+  d.pointNum = c.segment_valid_point_num;
+  d.lineNum = c.segment_valid_line_num;
+  d.scan_period = c.scan_period;
+  d.edge_thr = c.edge_threshold;
+  d.surf_thr = c.surf_threshold;
+  const float fa_resX = (float)((M_PI * 2) / d.W);
+  d.fa_resY = (float)(kDegToRad * (c.vertical_angle_top - c.vertical_angle_bottom) / float(d.H - 1));
+  d.sinResX = std::sin(fa_resX);
+  d.RatioXY = c.RatioXY;
+  d.RatioZ = c.RatioZ;
+  d.DBFr = c.DBFr;
+  d.ccl_lds = (d.H <= 16 && d.HW <= 32768) ? 1 : 0;
+}
+
+template <class T>
+static T* carve(char*& p, size_t n) {
+  T* r = reinterpret_cast<T*>(p);
+  p += (n * sizeof(T) + 255) & ~size_t(255);
+  return r;
+}
+
+static size_t layout(DevBufs& d, char* p0, int B, int H, int HW) {
+  char* p = p0;
+  const size_t n = (size_t)B * HW;
+  d.counts = carve<int>(p, (size_t)B * kCnt);
+  d.orient = carve<float>(p, (size_t)B * 4);
+  d.cell_pt = carve<int>(p, n);
+  d.range = carve<float>(p, n);
+  d.full = carve<float4>(p, n);
+  d.vis = carve<float>(p, n);
+  d.ground = carve<int8_t>(p, n);
+  d.label = carve<int>(p, n);
+  d.near_pts = carve<float4>(p, n);
+  d.shuf = carve<int>(p, n);
+  d.ccl_a = carve<int>(p, n);
+  d.ccl_b = carve<unsigned long long>(p, n);
+  d.start_ring = carve<int>(p, (size_t)B * H);
+  d.end_ring = carve<int>(p, (size_t)B * H);
+  d.seg = carve<float4>(p, n);
+  d.seg_ground = carve<uint8_t>(p, n);
+  d.seg_col = carve<uint32_t>(p, n);
+  d.seg_range = carve<float>(p, n);
+  d.seg_int = carve<float>(p, n);
+  d.outl = carve<float4>(p, n);
+  d.outl_int = carve<float>(p, n);
+  d.loam = carve<float4>(p, n);
+  d.curv = carve<float>(p, n);
+  d.picked = carve<uint8_t>(p, n);
+  d.clabel = carve<int8_t>(p, n);
+  d.ring_cnt = carve<int>(p, (size_t)B * 3 * H);
+  d.edge_tmp = carve<int>(p, n);
+  d.flat_tmp = carve<int>(p, n);
+  d.lflat_tmp = carve<float4>(p, n);
+  d.less_sharp = carve<int>(p, n);
+  d.cluster = carve<int>(p, n);
+  d.sharp = carve<int>(p, n);
+  d.flat = carve<int>(p, n);
+  d.lflat = carve<float4>(p, n);
+  d.db_pts = carve<float4>(p, n);
+  d.db_kz = carve<float>(p, n);
+  return (size_t)(p - p0);
+}
+
+extern "C" int32_t llsr_create(const llsr_config* cfg, int32_t hip_device, int32_t max_batch,
+                               int32_t max_points, llsr_handle** out) {
+  if (!cfg || !out || max_batch < 1 || max_points < 1) return LLSR_EINVAL;
+  *out = nullptr;
+  if (cfg->use_vlp32c) return LLSR_ENOSYS;
+  if (cfg->num_vertical_scans < 2 || cfg->num_vertical_scans > 64 || cfg->num_horizontal_scans < 16 ||
+      cfg->num_horizontal_scans > 2048)
+    return LLSR_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= hip_device || hip_device < 0) return LLSR_ENODEV;
+  llsr_handle* h = new (std::nothrow) llsr_handle();
+  if (!h) return LLSR_ENOMEM;
+  h->cfg = *cfg;
+  h->device = hip_device;
+  h->max_batch = max_batch;
+  h->max_points = max_points;
+  make_devcfg(*cfg, h->dc);
+  if (hipSetDevice(hip_device) != hipSuccess) { delete h; return LLSR_ENODEV; }
+  DevBufs probe{};
+  const size_t bytes = layout(probe, nullptr, max_batch, h->dc.H, h->dc.HW) + 4096;
+  if (hipMalloc(&h->pool, bytes) != hipSuccess) { delete h; return LLSR_ENOMEM; }
+  h->pool_bytes = bytes;
+  layout(h->d, (char*)h->pool, max_batch, h->dc.H, h->dc.HW);
+  if (hipMalloc(&h->d_in, sizeof(float4) * (size_t)max_points) != hipSuccess ||
+      hipMalloc(&h->d_off, sizeof(int64_t) * 2) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    llsr_destroy(h);
+    return LLSR_ENOMEM;
+  }
+  for (auto& e : h->ev) hipEventCreate(&e);
+  if (h->dc.ccl_lds) {
+    if (hipFuncSetAttribute((const void*)k_label<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            h->dc.HW * (int)sizeof(int)) != hipSuccess) {
+      llsr_destroy(h);
+      return LLSR_ENODEV;
+    }
+  }
+  int32_t rc = llsr_reset_state(h);
+  if (rc != LLSR_OK) { llsr_destroy(h); return rc; }
+  *out = h;
+  return LLSR_OK;
+}
+
+extern "C" void llsr_destroy(llsr_handle* h) {
+  if (!h) return;
+  hipSetDevice(h->device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  for (auto& e : h->ev)
+    if (e) hipEventDestroy(e);
+  if (h->pool) hipFree(h->pool);
+  if (h->d_in) hipFree(h->d_in);
+  if (h->d_off) hipFree(h->d_off);
+  if (h->stream) hipStreamDestroy(h->stream);
+  delete h;
+}
+
+extern "C" const char* llsr_last_error(const llsr_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+extern "C" int32_t llsr_query_sizes(const llsr_handle* h, llsr_sizes* s) {
+  if (!h || !s) return LLSR_EINVAL;
+  s->cells = h->dc.HW;
+  s->rings = h->dc.H;
+  s->max_points = h->max_points;
+  s->shadow_points = 160;
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_reset_state(llsr_handle* h) {
+  if (!h) return LLSR_EINVAL;
+  HIP_OK(h, hipSetDevice(h->device));
+  const size_t n = (size_t)h->max_batch * h->dc.HW;
+  HIP_OK(h, hipMemsetAsync(h->d.picked, 0, n, h->stream));
+  HIP_OK(h, hipMemsetAsync(h->d.clabel, 0, n, h->stream));
+  HIP_OK(h, hipStreamSynchronize(h->stream));
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_set_profiling(llsr_handle* h, int32_t enable) {
+  if (!h) return LLSR_EINVAL;
+  h->profiling = enable != 0;
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const int64_t* d_offsets,
+                                      int32_t B, void* hip_stream) {
+  if (!h || !d_xyzi || !d_offsets) return fail(h, LLSR_EINVAL, "null argument");
+  if (B < 1 || B > h->max_batch) return fail(h, LLSR_ERANGE, "batch size outside [1, max_batch]");
+  HIP_OK(h, hipSetDevice(h->device));
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+  const DevCfg& c = h->dc;
+  const float4* pts = reinterpret_cast<const float4*>(d_xyzi);
+  int k = 0;
+  auto mark = [&]() {
+    if (h->profiling) hipEventRecord(h->ev[k], s);
+    ++k;
+  };
+  mark();
+  HIP_OK(h, hipMemsetAsync(h->d.cell_pt, 0xFF, sizeof(int) * (size_t)B * c.HW, s));
+  k_init_counts<<<(B + 255) / 256, 256, 0, s>>>(h->d.counts, B);
+  mark();
+  k_project<<<dim3((h->max_points + 255) / 256, B), 256, 0, s>>>(c, pts, d_offsets, h->d);
+  mark();
+  k_gather_column<<<dim3((c.W + 255) / 256, B), 256, 0, s>>>(c, pts, d_offsets, h->d);
+  mark();
+  k_ground_add<<<dim3((c.H + 3) / 4, B), 256, 0, s>>>(c, h->d);
+  mark();
+  k_ground_elev_ransac<<<B, 1024, 0, s>>>(c, h->d);
+  mark();
+  if (c.ccl_lds)
+    k_label<true><<<B, 1024, c.HW * sizeof(int), s>>>(c, h->d);
+  else
+    k_label<false><<<B, 1024, 0, s>>>(c, h->d);
+  mark();
+  k_segment<<<B, 1024, 0, s>>>(c, pts, d_offsets, h->d);
+  mark();
+  k_fa_points<<<B, 1024, 0, s>>>(c, h->d);
+  mark();
+  k_select_ring<<<dim3(c.H, B), 256, 0, s>>>(c, h->d);
+  mark();
+  k_fa_finish<<<B, 1024, 0, s>>>(c, h->d);
+  mark();
+  HIP_OK(h, hipGetLastError());
+  h->last_stream = s;
+  h->last_B = B;
+  h->have_times = h->profiling;
+  return LLSR_OK;
+}
+
+static int32_t sync_last(llsr_handle* h) {
+  HIP_OK(h, hipSetDevice(h->device));
+  HIP_OK(h, hipStreamSynchronize(h->last_stream ? h->last_stream : h->stream));
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_kernel_times_ms(llsr_handle* h, float* out, int32_t cap) {
+  if (!h || !out) return LLSR_EINVAL;
+  if (!h->have_times) return 0;
+  int32_t rc = sync_last(h);
+  if (rc) return rc;
+  int n = 0;
+  for (int k = 0; k < kNumKernels && n < cap; ++k, ++n) {
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, h->ev[k], h->ev[k + 1]);
+    out[n] = ms;
+  }
+  return n;
+}
+
+extern "C" const char* llsr_kernel_name(int32_t k) {
+  return (k >= 0 && k < kNumKernels) ? kKernelNames[k] : "";
+}
+
+extern "C" int32_t llsr_batch_counts(llsr_handle* h, int32_t* out) {
+  if (!h || !out) return LLSR_EINVAL;
+  int32_t rc = sync_last(h);
+  if (rc) return rc;
+  std::vector<int> cnt((size_t)h->last_B * kCnt);
+  HIP_OK(h, hipMemcpy(cnt.data(), h->d.counts, cnt.size() * sizeof(int), hipMemcpyDeviceToHost));
+  const int idx[8] = {C_NPTS, C_S, C_O, C_M, C_SHARP, C_F, C_L, C_K};
+  for (int b = 0; b < h->last_B; ++b)
+    for (int q = 0; q < 8; ++q) out[b * 8 + q] = cnt[(size_t)b * kCnt + idx[q]];
+  return LLSR_OK;
+}
+
+template <class T>
+static hipError_t d2h(void* dst, const T* src, size_t n) {
+  if (!dst || n == 0) return hipSuccess;
+  return hipMemcpy(dst, src, n * sizeof(T), hipMemcpyDeviceToHost);
+}
+
+extern "C" int32_t llsr_fetch_scan(llsr_handle* h, int32_t b, llsr_scan_out* o) {
+  if (!h || !o) return LLSR_EINVAL;
+  if (b < 0 || b >= h->last_B) return fail(h, LLSR_ERANGE, "slot outside last batch");
+  int32_t rc = sync_last(h);
+  if (rc) return rc;
+  const DevCfg& c = h->dc;
+  const size_t base = (size_t)b * c.HW;
+  int cnt[kCnt];
+  HIP_OK(h, d2h(cnt, h->d.counts + b * kCnt, kCnt));
+  float ori[4];
+  HIP_OK(h, d2h(ori, h->d.orient + b * 4, 4));
+  o->n_points = cnt[C_NPTS];
+  std::memcpy(o->orientation, ori, sizeof(float) * 3);
+  const int S = cnt[C_S], O = cnt[C_O], M = cnt[C_M];
+  o->n_segmented = S;
+  o->n_outlier = O;
+  o->n_near = cnt[C_K];
+  o->n_ransac_inliers = cnt[C_INL];
+  o->ransac_iterations = cnt[C_RIT];
+  o->n_less_sharp = M;
+  o->n_sharp = cnt[C_SHARP];
+  o->n_flat = cnt[C_F];
+  o->n_less_flat = cnt[C_L];
+  HIP_OK(h, d2h(o->range_image, h->d.range + base, c.HW));
+  HIP_OK(h, d2h(o->cell_point, h->d.cell_pt + base, c.HW));
+  HIP_OK(h, d2h(o->ground_image, h->d.ground + base, c.HW));
+  HIP_OK(h, d2h(o->label_image, h->d.label + base, c.HW));
+  HIP_OK(h, d2h(o->start_ring_index, h->d.start_ring + (size_t)b * c.H, c.H));
+  HIP_OK(h, d2h(o->end_ring_index, h->d.end_ring + (size_t)b * c.H, c.H));
+  HIP_OK(h, d2h(o->seg_xyzi, (const float*)(h->d.seg + base), 4 * (size_t)S));
+  HIP_OK(h, d2h(o->seg_ground_flag, h->d.seg_ground + base, S));
+  HIP_OK(h, d2h(o->seg_col_ind, h->d.seg_col + base, S));
+  HIP_OK(h, d2h(o->seg_range, h->d.seg_range + base, S));
+  HIP_OK(h, d2h(o->seg_intensity, h->d.seg_int + base, S));
+  HIP_OK(h, d2h(o->outlier_xyzi, (const float*)(h->d.outl + base), 4 * (size_t)O));
+  HIP_OK(h, d2h(o->outlier_intensity, h->d.outl_int + base, O));
+  HIP_OK(h, d2h(o->loam_xyzi, (const float*)(h->d.loam + base), 4 * (size_t)S));
+  HIP_OK(h, d2h(o->curvature, h->d.curv + base, S));
+  HIP_OK(h, d2h(o->picked, h->d.picked + base, S));
+  HIP_OK(h, d2h(o->label, h->d.clabel + base, S));
+  HIP_OK(h, d2h(o->less_sharp_ind, h->d.less_sharp + base, M));
+  HIP_OK(h, d2h(o->dbscan_cluster, h->d.cluster + base, M));
+  HIP_OK(h, d2h(o->sharp_ind, h->d.sharp + base, o->n_sharp));
+  HIP_OK(h, d2h(o->flat_ind, h->d.flat + base, o->n_flat));
+  HIP_OK(h, d2h(o->less_flat_xyzi, (const float*)(h->d.lflat + base), 4 * (size_t)o->n_less_flat));
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_process_scan(llsr_handle* h, const float* xyzi, int32_t n, llsr_scan_out* out) {
+  if (!h || !out || n < 0 || (n > 0 && !xyzi)) return fail(h, LLSR_EINVAL, "bad argument");
+  if (n > h->max_points) return fail(h, LLSR_ERANGE, "scan larger than max_points");
+  HIP_OK(h, hipSetDevice(h->device));
+  const int64_t off[2] = {0, n};
+  HIP_OK(h, hipStreamSynchronize(h->stream));
+  if (n > 0) HIP_OK(h, hipMemcpy(h->d_in, xyzi, sizeof(float4) * (size_t)n, hipMemcpyHostToDevice));
+  HIP_OK(h, hipMemcpy(h->d_off, off, sizeof off, hipMemcpyHostToDevice));
+  int32_t rc = llsr_process_batch(h, (const float*)h->d_in, h->d_off, 1, h->stream);
+  if (rc) return rc;
+  return llsr_fetch_scan(h, 0, out);
+}

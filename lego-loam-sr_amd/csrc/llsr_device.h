@@ -1,0 +1,162 @@
+// llsr_device.h — shared device-side declarations: the per-batch configuration block, the
+// handle's device buffers, and small wave/block primitives for CDNA4 (64-lane waves).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace llsr {
+
+// Per-slot counter words (counts[b * kCnt + ...]).
+enum : int {
+  C_NPTS = 0,      // finite input points
+  C_FIRST = 1,     // first finite raw index (atomicMin)
+  C_LAST = 2,      // last finite raw index (atomicMax)
+  C_S = 3,         // segmented points
+  C_O = 4,         // outliers
+  C_K = 5,         // near-ground cloud size
+  C_INL = 6,       // RANSAC inliers
+  C_RIT = 7,       // RANSAC iterations
+  C_M = 8,         // cornerPointsLessSharp
+  C_SHARP = 9,     // cornerPointsSharp
+  C_F = 10,        // surfPointsFlat (without shadow points)
+  C_L = 11,        // surfPointsLessFlat
+  C_HALF = 12,     // adjustDistortion halfPassed split index
+  kCnt = 16
+};
+
+// Everything a kernel needs to know about the sensor, precomputed on the host with the same
+// float/double conversions as the reference constructors (IP:117-121, FA:152-154).
+struct DevCfg {
+  int H, W, HW;
+  float ip_resX, ip_resY, ip_angBottom;
+  float segThr, sinX, cosX, sinY, cosY;
+  int use_kitti, gsi, pointNum, lineNum;
+  float scan_period, edge_thr, surf_thr;
+  float fa_resY, sinResX, RatioXY, RatioZ, DBFr;
+  int ccl_lds;  // union-find parent array fits LDS (H <= 16 && HW <= 32768)
+};
+
+// Device buffers owned by the handle; every per-slot array has stride HW (or H for rings).
+struct DevBufs {
+  int* counts;          // [B][kCnt]
+  float* orient;        // [B][4]
+  int* cell_pt;         // [B][HW] raw point index or -1
+  float* range;         // [B][HW]
+  float4* full;         // [B][HW] x,y,z, row + col/1e4
+  float* vis;           // [B][HW] raw intensity of the kept point
+  int8_t* ground;       // [B][HW]
+  int* label;           // [B][HW]
+  float4* near_pts;     // [B][HW] near-ground cloud (w = cell index)
+  int* shuf;            // [B][HW] RANSAC shuffled_indices_
+  int* ccl_a;           // [B][HW] scratch (global-mode union-find parent / stats)
+  unsigned long long* ccl_b;  // [B][HW] scratch (global-mode row masks)
+  int* start_ring;      // [B][H]
+  int* end_ring;        // [B][H]
+  float4* seg;          // [B][HW] segmented cloud (IP frame)
+  uint8_t* seg_ground;  // [B][HW] (zero beyond S: CloudInfo arrays have length H*W)
+  uint32_t* seg_col;    // [B][HW]
+  float* seg_range;     // [B][HW]
+  float* seg_int;       // [B][HW]
+  float4* outl;         // [B][HW]
+  float* outl_int;      // [B][HW]
+  float4* loam;         // [B][HW] segmented cloud after adjustDistortion
+  float* curv;          // [B][HW]
+  uint8_t* picked;      // [B][HW] FA carry-over state cloudNeighborPicked
+  int8_t* clabel;       // [B][HW] FA carry-over state cloudLabel
+  int* ring_cnt;        // [B][3][H] edges, flats, less-flat per ring
+  int* edge_tmp;        // [B][HW] per-ring edge lists at their ring's start position
+  int* flat_tmp;        // [B][HW]
+  float4* lflat_tmp;    // [B][HW]
+  int* less_sharp;      // [B][HW]
+  int* cluster;         // [B][HW]
+  int* sharp;           // [B][HW]
+  int* flat;            // [B][HW]
+  float4* lflat;        // [B][HW]
+  float4* db_pts;       // [B][HW] DBSCAN scratch: (x0, y0, z0, kxy)
+  float* db_kz;         // [B][HW]
+};
+
+// ---- wave / block primitives (wave64) ------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+template <class T>
+__device__ __forceinline__ T wave_incl_scan_add(T x) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    T y = __shfl_up(x, d, 64);
+    if (l >= d) x += y;
+  }
+  return x;
+}
+
+template <class T>
+__device__ __forceinline__ T wave_reduce_add(T x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  return x;
+}
+
+template <class T>
+__device__ __forceinline__ T wave_reduce_min(T x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    T y = __shfl_xor(x, d, 64);
+    x = y < x ? y : x;
+  }
+  return x;
+}
+
+template <class T>
+__device__ __forceinline__ T wave_reduce_max(T x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    T y = __shfl_xor(x, d, 64);
+    x = y > x ? y : x;
+  }
+  return x;
+}
+
+// Exclusive prefix sum over the block; `tmp` holds >= blockDim/64 ints of LDS.
+// Returns the exclusive prefix of v; *total receives the block sum. Contains barriers.
+__device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* total) {
+  const int l = lane_id(), w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  int x = wave_incl_scan_add(v);
+  if (l == 63) tmp[w] = x;
+  __syncthreads();
+  if (w == 0) {
+    int t = l < nw ? tmp[l] : 0;
+    t = wave_incl_scan_add(t);
+    if (l < nw) tmp[l] = t;
+  }
+  __syncthreads();
+  int pre = w ? tmp[w - 1] : 0;
+  *total = tmp[nw - 1];
+  __syncthreads();
+  return pre + x - v;
+}
+
+__device__ __forceinline__ int block_reduce_add(int v, int* tmp) {
+  int t;
+  block_excl_scan(v, tmp, &t);
+  return t;
+}
+
+__device__ __forceinline__ int block_reduce_min(int v, int* tmp) {
+  const int l = lane_id(), w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_reduce_min(v);
+  if (l == 0) tmp[w] = v;
+  __syncthreads();
+  int r = tmp[0];
+  for (int k = 1; k < nw; ++k) r = tmp[k] < r ? tmp[k] : r;
+  __syncthreads();
+  return r;
+}
+
+// x86-64 truncating conversions (cvttss2si / cvttsd2si): NaN / out of range -> INT_MIN.
+__device__ __forceinline__ int trunc_i32(double v) {
+  if (!(v > -2147483649.0 && v < 2147483648.0)) return (int)0x80000000;
+  return (int)v;
+}
+
+}  // namespace llsr

@@ -1,0 +1,704 @@
+// llsr_ip.hip — ImageProjection on gfx950: projection, ground segmentation, connected-component
+// labelling and segmented-cloud extraction for a batch of scans (one slot per scan).
+//
+// Reference: LeGO-LOAM/src/imageProjection.cpp (IP). Each kernel names the lines it restates.
+// Built with -ffp-contract=off: every float/double expression below evaluates in the same order
+// and precision as the reference's x86-64 -O3 build, so outputs are bit-identical.
+#include <cfloat>
+#include <climits>
+
+#include "llsr_device.h"
+#include "llsr_libm.h"
+
+namespace llsr {
+
+using namespace llsr_libm;
+
+constexpr double kDegToRad = 3.14159265358979323846 / 180.0;  // utility.h:49
+constexpr double kPi = 3.14159265358979323846;
+
+__device__ __forceinline__ bool finite3(float4 p) {
+  return __builtin_isfinite(p.x) && __builtin_isfinite(p.y) && __builtin_isfinite(p.z);
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1 project: removeNaNFromPointCloud (IP:198) + projectPointCloud row/col (IP:305-336).
+// One thread per raw point; the serial "last writer wins" of IP:337-347 becomes atomicMax of
+// the raw index per cell (the compacted order preserves raw order). Also counts finite points
+// and the first/last finite index for findStartEndAngle (IP:430-436).
+// grid (ceil(maxN/256), B), block 256.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_project(DevCfg c, const float4* __restrict__ pts,
+                                                 const int64_t* __restrict__ off, DevBufs d) {
+  const int b = blockIdx.y;
+  const int64_t o0 = off[b], n = off[b + 1] - o0;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if ((int64_t)blockIdx.x * blockDim.x >= n) return;
+  bool fin = false;
+  if (i < n) {
+    const float4 p = pts[o0 + i];
+    fin = finite3(p);
+    if (fin) {
+      const float range = sqrt_(p.x * p.x + p.y * p.y + p.z * p.z);
+      const float va = asinf_(p.z / range);
+      const int row = trunc_i32((double)((va + c.ip_angBottom) / c.ip_resY));
+      if (row >= 0 && row < c.H) {
+        const float ha = atan2f_(p.x, p.y);
+        int col = trunc_i32(-round(((double)ha - kPi / 2) / (double)c.ip_resX) + c.W * 0.5);
+        if (col >= c.W) col -= c.W;
+        if (col >= 0 && col < c.W && !((double)range < 0.1))
+          atomicMax(&d.cell_pt[(size_t)b * c.HW + col + row * c.W], i);
+      }
+    }
+  }
+  const unsigned long long m = __ballot(fin);
+  if (lane_id() == 0 && m) {
+    int* cnt = d.counts + b * kCnt;
+    atomicAdd(&cnt[C_NPTS], (int)__popcll(m));
+    const int base = blockIdx.x * blockDim.x + (threadIdx.x & ~63);
+    atomicMin(&cnt[C_FIRST], base + (int)__ffsll((long long)m) - 1);
+    atomicMax(&cnt[C_LAST], base + 63 - (int)__clzll((long long)m));
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K2 gather + ground column pass: builds range_mat/full_cloud for each cell (IP:337-347,
+// resetParameters IP:170-179) and runs groundRemovalOurs' per-column vector test and Filter
+// (IP:524-629) in the same sweep. One thread per (scan, column), rows bottom-up.
+// grid (ceil(W/256), B), block 256.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_gather_column(DevCfg c, const float4* __restrict__ pts,
+                                                       const int64_t* __restrict__ off, DevBufs d) {
+  const int b = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= c.W) return;
+  const int64_t o0 = off[b];
+  const size_t base = (size_t)b * c.HW;
+  const float qnan = __builtin_nanf("");
+  bool haveRV = false, obs = false;
+  float RVx = 0.f, RVy = 0.f, RVz = 0.f;
+  float lx = 0.f, ly = 0.f, lz = 0.f;
+  for (int i = 0; i < c.H; ++i) {
+    const int cell = j + i * c.W;
+    const int pi = d.cell_pt[base + cell];
+    float4 f;
+    float rng, vis;
+    if (pi >= 0) {
+      const float4 p = pts[o0 + pi];
+      rng = sqrt_(p.x * p.x + p.y * p.y + p.z * p.z);
+      f = make_float4(p.x, p.y, p.z, (float)((double)(float)i + (double)(float)j / 10000.0));
+      vis = p.w;
+    } else {
+      rng = FLT_MAX;
+      f = make_float4(qnan, qnan, qnan, 0.0f);
+      vis = 0.0f;
+    }
+    d.range[base + cell] = rng;
+    d.full[base + cell] = f;
+    d.vis[base + cell] = vis;
+    int8_t g;
+    if (f.w == 0.0f) {
+      g = -1;  // IP:535: NaN cells (and a real point at row 0, col 0) have intensity 0
+    } else if (!haveRV) {
+      const float d0 = sqrt_(f.x * f.x + f.y * f.y);
+      RVx = f.x / d0; RVy = f.y / d0; RVz = 0.0f;
+      haveRV = true;
+      lx = f.x; ly = f.y; lz = f.z;
+      g = 1;
+    } else {
+      const float TVx = f.x - lx, TVy = f.y - ly, TVz = f.z - lz;
+      const float ang = (float)((double)acosf_((TVx * RVx + TVy * RVy + TVz * RVz) /
+                                               (sqrt_(TVx * TVx + TVy * TVy + TVz * TVz) *
+                                                sqrt_(RVx * RVx + RVy * RVy + RVz * RVz))) /
+                                kDegToRad);
+      const float D = c.use_kitti ? (i < 16 ? 60.0f : 25.0f) : 12.5f;
+      if (ang <= D) { RVx += TVx; RVy += TVy; RVz += TVz; g = 1; }
+      else g = 0;
+      lx = f.x; ly = f.y; lz = f.z;
+    }
+    // Filter (IP:620-628): after the first 0 of the column every 1 becomes 2.
+    if (g == 0) obs = true;
+    else if (g == 1 && obs) g = 2;
+    d.ground[base + cell] = g;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K3 ADD (IP:631-671): per row, a forward then a backward recurrence "2 -> 1 if a ground cell
+// sits one or two columns behind and the step is short". The state before column j is the pair
+// (g'[j-2]==1, g'[j-1]==1), so each column is a map on 4 states; a wave composes the maps of
+// its 64 lane-chunks with a shuffle scan and replays each chunk from its exact incoming state.
+// Bit-identical to the serial loop. One wave per row. grid (ceil(H/4), B), block 256.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t st_apply(uint32_t f, uint32_t s) { return (f >> (2 * s)) & 3u; }
+__device__ __forceinline__ uint32_t st_compose(uint32_t g, uint32_t f) {  // g after f
+  uint32_t h = 0;
+#pragma unroll
+  for (uint32_t s = 0; s < 4; ++s) h |= st_apply(g, st_apply(f, s)) << (2 * s);
+  return h;
+}
+// map of one column: s=(a|b<<1) -> (b | c<<1), c = one || (cand && (a||b))
+__device__ __forceinline__ uint32_t st_column(bool one, bool cand) {
+  uint32_t f = 0;
+#pragma unroll
+  for (uint32_t s = 0; s < 4; ++s) {
+    const uint32_t a = s & 1u, bb = s >> 1;
+    const uint32_t cc = one ? 1u : (cand && (a | bb)) ? 1u : 0u;
+    f |= (bb | (cc << 1)) << (2 * s);
+  }
+  return f;
+}
+
+__device__ __forceinline__ bool add_test(const float4* __restrict__ full, int cell, int nb) {
+  const float4 p = full[cell], q = full[nb];
+  const float r = sqrt_(p.x * p.x + p.y * p.y + p.z * p.z);
+  const float dx = p.x - q.x, dy = p.y - q.y, dz = p.z - q.z;
+  const float dr = sqrt_(dx * dx + dy * dy + dz * dz);
+  return (double)dr <= 0.061 * (double)r && (double)dz <= 0.1;
+}
+
+__global__ __launch_bounds__(256) void k_ground_add(DevCfg c, DevBufs d) {
+  __shared__ int8_t grow[4][2048];
+  const int b = blockIdx.y;
+  const int wv = threadIdx.x >> 6, l = lane_id();
+  const int i = blockIdx.x * 4 + wv;
+  if (i >= c.H) return;
+  const int W = c.W;
+  const size_t rbase = (size_t)b * c.HW + (size_t)i * W;
+  int8_t* g = grow[wv];
+  for (int j = l; j < W; j += 64) g[j] = d.ground[rbase + j];
+  __builtin_amdgcn_wave_barrier();
+  const float4* full = d.full + rbase;
+  const int CH = (W + 63) / 64;
+  const uint32_t kId = 0xE4u;  // identity map on 4 states
+
+  // ---- forward pass, j = 2 .. W-1 ----
+  {
+    const int j0 = l * CH, j1 = min(j0 + CH, W);
+    uint32_t F = kId;
+    uint64_t candBits = 0;  // CH <= 64
+    for (int j = j0; j < j1; ++j) {
+      if (j < 2) continue;
+      const bool two = g[j] == 2;
+      const bool cand = two && add_test(full, j, j - 2);
+      if (cand) candBits |= 1ull << (j - j0);
+      F = st_compose(st_column(g[j] == 1, cand), F);
+    }
+    // exclusive scan of maps over lanes (lane order = column order)
+    uint32_t incl = F;
+#pragma unroll
+    for (int dlt = 1; dlt < 64; dlt <<= 1) {
+      const uint32_t y = __shfl_up(incl, dlt, 64);
+      if (l >= dlt) incl = st_compose(incl, y);
+    }
+    uint32_t excl = __shfl_up(incl, 1, 64);
+    if (l == 0) excl = kId;
+    const uint32_t s0 = (g[0] == 1 ? 1u : 0u) | (g[1] == 1 ? 2u : 0u);
+    uint32_t s = st_apply(excl, s0);
+    __builtin_amdgcn_wave_barrier();
+    for (int j = j0; j < j1; ++j) {
+      if (j < 2) continue;
+      const bool cand = (candBits >> (j - j0)) & 1ull;
+      const uint32_t a = s & 1u, bb = s >> 1;
+      bool one = g[j] == 1;
+      if (cand && (a | bb)) { g[j] = 1; one = true; }
+      s = bb | ((one ? 1u : 0u) << 1);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  // ---- backward pass, j = W-3 .. 0, neighbours j+1, j+2 ----
+  {
+    // lane l owns the l-th chunk counted from the right end.
+    const int hi = W - 3;  // first column visited
+    const int j1 = hi - l * CH, j0 = max(j1 - CH + 1, 0);  // chunk [j0, j1], visited descending
+    uint32_t F = kId;
+    uint64_t candBits = 0;
+    for (int j = j1; j >= j0; --j) {
+      const bool two = g[j] == 2;
+      const bool cand = two && add_test(full, j, j + 2);
+      if (cand) candBits |= 1ull << (j1 - j);
+      F = st_compose(st_column(g[j] == 1, cand), F);
+    }
+    uint32_t incl = F;
+#pragma unroll
+    for (int dlt = 1; dlt < 64; dlt <<= 1) {
+      const uint32_t y = __shfl_up(incl, dlt, 64);
+      if (l >= dlt) incl = st_compose(incl, y);
+    }
+    uint32_t excl = __shfl_up(incl, 1, 64);
+    if (l == 0) excl = kId;
+    const uint32_t s0 = (g[W - 1] == 1 ? 1u : 0u) | (g[W - 2] == 1 ? 2u : 0u);
+    uint32_t s = st_apply(excl, s0);
+    __builtin_amdgcn_wave_barrier();
+    for (int j = j1; j >= j0; --j) {
+      const bool cand = (candBits >> (j1 - j)) & 1ull;
+      const uint32_t a = s & 1u, bb = s >> 1;
+      bool one = g[j] == 1;
+      if (cand && (a | bb)) { g[j] = 1; one = true; }
+      s = bb | ((one ? 1u : 0u) << 1);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  for (int j = l; j < W; j += 64) d.ground[rbase + j] = g[j];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Device mt19937 (== boost::mt19937 / std::mt19937) for PCL's SampleConsensusModel RNG.
+// ---------------------------------------------------------------------------------------------
+struct MT {
+  uint32_t mt[624];
+  int idx;
+};
+__device__ void mt_seed(MT& m, uint32_t s) {
+  m.mt[0] = s;
+  for (int k = 1; k < 624; ++k) m.mt[k] = 1812433253u * (m.mt[k - 1] ^ (m.mt[k - 1] >> 30)) + (uint32_t)k;
+  m.idx = 624;
+}
+__device__ uint32_t mt_next(MT& m) {
+  if (m.idx >= 624) {
+    for (int k = 0; k < 624; ++k) {
+      const uint32_t y = (m.mt[k] & 0x80000000u) | (m.mt[(k + 1) % 624] & 0x7fffffffu);
+      m.mt[k] = m.mt[(k + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    m.idx = 0;
+  }
+  uint32_t y = m.mt[m.idx++];
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+
+__device__ __forceinline__ float ransac_dist(const float cf[4], float4 q) {
+  // Eigen SSE dot of 4 floats: (c0 p0 + c2 p2) + (c1 p1 + c3 * 1)
+  return fabs_((cf[0] * q.x + cf[2] * q.z) + (cf[1] * q.y + cf[3] * 1.0f));
+}
+
+// ---------------------------------------------------------------------------------------------
+// K4 ELEVATION + NEAR + RANSAC + final ground (IP:673-735). One workgroup (1024 threads) per
+// scan: a last-valid carry scan over columns, a row-major compaction of near-ground cells, and
+// PCL 1.10's RandomSampleConsensus driven by lane 0 with inlier counting spread over the block.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_ground_elev_ransac(DevCfg c, DevBufs d) {
+  __shared__ float colz[2048];
+  __shared__ int colok[2048];
+  __shared__ int tmp[32];
+  __shared__ MT rng;
+  __shared__ int sh_int[8];
+  __shared__ float sh_cf[4], best_cf[4];
+  __shared__ int sample[3];
+  const int b = blockIdx.x;
+  const int W = c.W, H = c.H, HW = c.HW;
+  const size_t base = (size_t)b * HW;
+  int8_t* g = d.ground + base;
+  const float4* full = d.full + base;
+  const int tid = threadIdx.x, nt = blockDim.x;
+
+  // ---- ELEVATION: per-column ground count and top ground z (IP:676-687) ----
+  for (int j = tid; j < W; j += nt) {
+    int cnt = 0;
+    float zt = 0.0f;
+    for (int i = 0; i < H; ++i)
+      if (g[j + i * W] == 1) { ++cnt; zt = full[j + i * W].z; }
+    colz[j] = zt;
+    colok[j] = cnt >= 5 ? j : -1;
+  }
+  __syncthreads();
+  // last-valid carry across columns: max-scan of colok (block-sequential chunks of 2)
+  {
+    const int per = (W + nt - 1) / nt;
+    const int j0 = tid * per, j1 = min(j0 + per, W);
+    int last = -1;
+    for (int j = j0; j < j1; ++j) last = colok[j] > last ? colok[j] : last;
+    // inclusive max-scan over threads
+    const int l = lane_id(), w = tid >> 6, nw = nt >> 6;
+    int x = last;
+    for (int dl = 1; dl < 64; dl <<= 1) {
+      int y = __shfl_up(x, dl, 64);
+      if (l >= dl) x = y > x ? y : x;
+    }
+    if (l == 63) tmp[w] = x;
+    __syncthreads();
+    int pre = -1;
+    for (int k = 0; k < w; ++k) pre = tmp[k] > pre ? tmp[k] : pre;
+    int ex = __shfl_up(x, 1, 64);
+    if (l == 0) ex = -1;
+    int run = ex > pre ? ex : pre;
+    __syncthreads();
+    for (int j = j0; j < j1; ++j) {
+      run = colok[j] > run ? colok[j] : run;
+      colok[j] = run;  // index of the carried column, -1 = initial -1.3
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < W; j += nt) {
+    const float EH = colok[j] >= 0 ? colz[colok[j]] : -1.3f;
+    for (int i = 0; i < H; ++i) {
+      const int cell = j + i * W;
+      if (g[cell] == 2) g[cell] = ((double)full[cell].z < (double)EH + 0.3) ? 1 : 0;
+    }
+  }
+  __syncthreads();
+
+  // ---- NEAR (IP:701-715): row-major compaction, intensity = linear index ----
+  const int per = (HW + nt - 1) / nt;
+  const int c0 = min(tid * per, HW), c1 = min(c0 + per, HW);
+  int myc = 0;
+  for (int cell = c0; cell < c1; ++cell) {
+    if (g[cell] != 1) continue;
+    const float4 p = full[cell];
+    const float depth = sqrt_(p.x * p.x + p.y * p.y);
+    if ((double)depth <= 10) ++myc;
+  }
+  int K;
+  int pos = block_excl_scan(myc, tmp, &K);
+  float4* nearp = d.near_pts + base;
+  for (int cell = c0; cell < c1; ++cell) {
+    if (g[cell] != 1) continue;
+    const float4 p = full[cell];
+    const float depth = sqrt_(p.x * p.x + p.y * p.y);
+    if ((double)depth <= 10) {
+      nearp[pos++] = make_float4(p.x, p.y, p.z, (float)cell);
+      if ((double)depth <= 5) g[cell] = 0;
+    }
+  }
+  int* shuf = d.shuf + base;
+  for (int k = tid; k < K; k += nt) shuf[k] = k;
+  __syncthreads();
+
+  // ---- RANSAC (PCL 1.10 RandomSampleConsensus::computeModel, threshold 0.5) ----
+  // sh_int: 0 stop, 1 valid-model, 2 iterations, 3 best count, 4 skipped, 5 have-best
+  __shared__ double kk;
+  if (tid == 0) {
+    mt_seed(rng, 12345u);
+    sh_int[0] = K < 3 ? 1 : 0;
+    sh_int[2] = K < 3 ? INT_MAX - 1 : 0;
+    sh_int[3] = -INT_MAX;
+    sh_int[4] = 0;
+    sh_int[5] = 0;
+    kk = 1.0;
+  }
+  __syncthreads();
+  const double log_probability = log(1.0 - 0.99);
+  const double one_over = K > 0 ? 1.0 / (double)K : 0.0;
+  while (true) {
+    if (tid == 0) {
+      sh_int[1] = 0;
+      if (!(sh_int[0] == 0 && sh_int[2] < kk && sh_int[4] < 100000)) {
+        sh_int[0] = 1;
+      } else {
+        bool ok = false;
+        for (int tries = 0; tries < 1000 && !ok; ++tries) {
+          for (int q = 0; q < 3; ++q) {
+            const int r = (int)(mt_next(rng) >> 1);
+            const int sw = q + (int)((unsigned)r % (unsigned)(K - q));
+            const int t = shuf[q]; shuf[q] = shuf[sw]; shuf[sw] = t;
+          }
+          const float4 p0 = nearp[shuf[0]], p1 = nearp[shuf[1]], p2 = nearp[shuf[2]];
+          const float r0 = (p1.x - p0.x) / (p2.x - p0.x), r1 = (p1.y - p0.y) / (p2.y - p0.y),
+                      r2 = (p1.z - p0.z) / (p2.z - p0.z);
+          ok = (r0 != r1) || (r2 != r1);
+        }
+        if (!ok) {
+          sh_int[0] = 1;
+        } else {
+          const float4 p0 = nearp[shuf[0]], p1 = nearp[shuf[1]], p2 = nearp[shuf[2]];
+          const float a0 = p1.x - p0.x, a1 = p1.y - p0.y, a2 = p1.z - p0.z;
+          const float b0 = p2.x - p0.x, b1 = p2.y - p0.y, b2 = p2.z - p0.z;
+          const float r0 = a0 / b0, r1 = a1 / b1, r2 = a2 / b2;
+          if (r0 == r1 && r2 == r1) {
+            sh_int[4] += 1;
+          } else {
+            float cf[4];
+            cf[0] = a1 * b2 - a2 * b1;
+            cf[1] = a2 * b0 - a0 * b2;
+            cf[2] = a0 * b1 - a1 * b0;
+            cf[3] = 0.0f;
+            const float sq = (cf[0] * cf[0] + cf[2] * cf[2]) + (cf[1] * cf[1] + cf[3] * cf[3]);
+            if (sq > 0.0f) {
+              const float nrm = sqrt_(sq);
+              for (int q = 0; q < 4; ++q) cf[q] = cf[q] / nrm;
+            }
+            cf[3] = -1.0f * ((cf[0] * p0.x + cf[2] * p0.z) + (cf[1] * p0.y + cf[3] * 1.0f));
+            for (int q = 0; q < 4; ++q) sh_cf[q] = cf[q];
+            sh_int[1] = 1;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (sh_int[0]) break;
+    if (!sh_int[1]) continue;
+    float cf[4] = {sh_cf[0], sh_cf[1], sh_cf[2], sh_cf[3]};
+    int cnt = 0;
+    for (int k = tid; k < K; k += nt)
+      if ((double)ransac_dist(cf, nearp[k]) < 0.5) ++cnt;
+    cnt = block_reduce_add(cnt, tmp);
+    if (tid == 0) {
+      if (cnt > sh_int[3]) {
+        sh_int[3] = cnt;
+        for (int q = 0; q < 4; ++q) best_cf[q] = cf[q];
+        sh_int[5] = 1;
+        const double w = (double)cnt * one_over;
+        double p_no = 1.0 - pow(w, 3.0);
+        p_no = fmax(2.220446049250313e-16, p_no);
+        p_no = fmin(1.0 - 2.220446049250313e-16, p_no);
+        kk = log_probability / log(p_no);
+      }
+      sh_int[2] += 1;
+      if (sh_int[2] > 10000) sh_int[0] = 1;
+    }
+    __syncthreads();
+  }
+  // ---- inliers with depth <= 5 become ground again (IP:727-735) ----
+  int ninl = 0;
+  if (sh_int[5]) {
+    const float cf[4] = {best_cf[0], best_cf[1], best_cf[2], best_cf[3]};
+    for (int k = tid; k < K; k += nt) {
+      const float4 q = nearp[k];
+      if ((double)ransac_dist(cf, q) < 0.5) {
+        ++ninl;
+        const int cell = (int)q.w;
+        const float4 p = full[cell];
+        const float depth = sqrt_(p.x * p.x + p.y * p.y);
+        if ((double)depth <= 5) g[cell] = 1;
+      }
+    }
+  }
+  ninl = block_reduce_add(ninl, tmp);
+  if (tid == 0) {
+    int* cnt = d.counts + b * kCnt;
+    cnt[C_K] = K;
+    cnt[C_INL] = ninl;
+    cnt[C_RIT] = sh_int[2];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K5 cloudSegmentation labelling (IP:783-789 driving labelComponents IP:847-931).
+// The BFS edge test is symmetric, so each BFS visits exactly one connected component of the
+// label-0 cells (4-neighbourhood, columns wrap, rows do not), seeded at its smallest linear
+// index. We compute components with a lock-free union-find (link to the smaller root, so the
+// root is that seed), then size and the row set of the non-seed members (lineCountFlag is set
+// only for pushed cells, IP:904), feasibility (IP:912-922), and label = 1 + rank of the seed
+// among feasible components in row-major order; infeasible -> 999999. One workgroup per scan.
+// LDS mode (VLP-16 size): parent array in LDS; else global scratch with workgroup-scope atomics.
+// ---------------------------------------------------------------------------------------------
+template <class Acc>
+__device__ __forceinline__ int uf_find(Acc& P, int x) {
+  while (true) {
+    const int p = P.ld(x);
+    if (p == x) return x;
+    const int gp = P.ld(p);
+    if (gp == p) return p;
+    P.st(x, gp);  // path halving; benign race (values only move toward the root)
+    x = gp;
+  }
+}
+template <class Acc>
+__device__ __forceinline__ void uf_unite(Acc& P, int a, int b) {
+  while (true) {
+    a = uf_find(P, a);
+    b = uf_find(P, b);
+    if (a == b) return;
+    if (a > b) { const int t = a; a = b; b = t; }
+    const int old = P.cas(b, b, a);  // hook larger root under smaller
+    if (old == b) return;
+    b = old;
+  }
+}
+struct LdsAcc {
+  int* p;
+  __device__ int ld(int i) { return __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+  __device__ void st(int i, int v) { __hip_atomic_store(p + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+  __device__ int cas(int i, int e, int v) {
+    __hip_atomic_compare_exchange_strong(p + i, &e, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return e;
+  }
+};
+
+__device__ __forceinline__ bool seg_edge(const DevCfg& c, float ra, float rb, bool horiz) {
+  const float d1 = ra < rb ? rb : ra;  // std::max(a, b) = (a < b) ? b : a
+  const float d2 = rb < ra ? rb : ra;  // std::min(a, b) = (b < a) ? b : a
+  const float sA = horiz ? c.sinX : c.sinY, cA = horiz ? c.cosX : c.cosY;
+  const float tang = d2 * sA / (d1 - d2 * cA);
+  return tang > c.segThr;
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
+  extern __shared__ int lds_parent[];
+  __shared__ int tmp[32];
+  const int b = blockIdx.x;
+  const int W = c.W, H = c.H, HW = c.HW;
+  const size_t base = (size_t)b * HW;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int8_t* g = d.ground + base;
+  const float* rng = d.range + base;
+  int* lab = d.label + base;
+  LdsAcc P{kLds ? lds_parent : d.ccl_a + base};
+
+  // label_mat init (IP:752-759): -1 for ground or empty, else 0 -> union-find singleton
+  for (int cell = tid; cell < HW; cell += nt) {
+    const bool l0 = !(g[cell] == 1 || rng[cell] == FLT_MAX);
+    P.st(cell, l0 ? cell : -1);
+  }
+  __syncthreads();
+  for (int cell = tid; cell < HW; cell += nt) {
+    if (P.ld(cell) < 0) continue;
+    const int i = cell / W, j = cell - i * W;
+    const float r = rng[cell];
+    const int right = (j + 1 < W) ? cell + 1 : cell + 1 - W;  // wrap (IP:884-886)
+    if (P.ld(right) >= 0 && seg_edge(c, r, rng[right], true)) uf_unite(P, cell, right);
+    if (i + 1 < H) {
+      const int down = cell + W;
+      if (P.ld(down) >= 0 && seg_edge(c, r, rng[down], false)) uf_unite(P, cell, down);
+    }
+  }
+  __syncthreads();
+  // flatten: root per cell -> lab (temporarily), -1 for non-label-0 cells
+  for (int cell = tid; cell < HW; cell += nt) {
+    const int p = P.ld(cell);
+    lab[cell] = p < 0 ? -1 : uf_find(P, cell);
+  }
+  __syncthreads();
+  // component stats. LDS mode packs (size << 16) | rowmask16 into one word per root;
+  // global mode keeps size in ccl_a and the 64-bit row mask in ccl_b.
+  int* stat = kLds ? lds_parent : d.ccl_a + base;
+  unsigned long long* rowm = d.ccl_b + base;
+  for (int cell = tid; cell < HW; cell += nt) {
+    stat[cell] = 0;
+    if (!kLds) rowm[cell] = 0ull;
+  }
+  __syncthreads();
+  for (int cell = tid; cell < HW; cell += nt) {
+    const int root = lab[cell];
+    if (root < 0) continue;
+    const int row = cell / W;
+    if (kLds) {
+      atomicAdd(&stat[root], 1 << 16);
+      if (cell != root) atomicOr(&stat[root], 1 << row);
+    } else {
+      atomicAdd(&stat[root], 1);
+      if (cell != root) atomicOr(&rowm[root], 1ull << row);
+    }
+  }
+  __syncthreads();
+  // feasibility and rank of feasible seeds in row-major order
+  const int per = (HW + nt - 1) / nt;
+  const int c0 = min(tid * per, HW), c1 = min(c0 + per, HW);
+  int mine = 0;
+  for (int cell = c0; cell < c1; ++cell) {
+    if (lab[cell] != cell) continue;
+    int size, lines;
+    if (kLds) { size = (unsigned)stat[cell] >> 16; lines = __popc(stat[cell] & 0xffff); }
+    else { size = stat[cell]; lines = __popcll(rowm[cell]); }
+    const bool feas = size >= 30 || (size >= c.pointNum && lines >= c.lineNum);
+    if (feas) ++mine;
+  }
+  int tot;
+  int rank = block_excl_scan(mine, tmp, &tot);
+  // second pass: overwrite the stat word of each root with its final label
+  for (int cell = c0; cell < c1; ++cell) {
+    if (lab[cell] != cell) continue;
+    int size, lines;
+    if (kLds) { size = (unsigned)stat[cell] >> 16; lines = __popc(stat[cell] & 0xffff); }
+    else { size = stat[cell]; lines = __popcll(rowm[cell]); }
+    const bool feas = size >= 30 || (size >= c.pointNum && lines >= c.lineNum);
+    stat[cell] = feas ? ++rank : 999999;
+  }
+  __syncthreads();
+  for (int cell = tid; cell < HW; cell += nt) {
+    const int root = lab[cell];
+    if (root >= 0) lab[cell] = stat[root];
+  }
+}
+
+template __global__ void k_label<true>(DevCfg, DevBufs);
+template __global__ void k_label<false>(DevCfg, DevBufs);
+
+// ---------------------------------------------------------------------------------------------
+// K6 segmented / outlier extraction (IP:791-832) + findStartEndAngle (IP:430-445).
+// Row-major block compaction; ring start/end indices fall out of the running count at each
+// row boundary. One workgroup per scan.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_segment(DevCfg c, const float4* __restrict__ pts,
+                                                  const int64_t* __restrict__ off, DevBufs d) {
+  __shared__ int tmp[32];
+  const int b = blockIdx.x;
+  const int W = c.W, H = c.H, HW = c.HW;
+  const size_t base = (size_t)b * HW;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int8_t* g = d.ground + base;
+  const int* lab = d.label + base;
+  int* cnt = d.counts + b * kCnt;
+  if (tid == 0) {
+    float o0 = 0.f, o1 = 0.f, o2 = 0.f;
+    if (cnt[C_NPTS] > 0) {
+      const float4 a = pts[off[b] + cnt[C_FIRST]], e = pts[off[b] + cnt[C_LAST]];
+      o0 = -atan2f_(a.y, a.x);
+      o1 = (float)(-atan2f_(e.y, e.x) + 2 * kPi);
+      if (o1 - o0 > 3 * kPi) o1 = (float)(o1 - 2 * kPi);
+      else if (o1 - o0 < kPi) o1 = (float)(o1 + 2 * kPi);
+      o2 = o1 - o0;
+    }
+    d.orient[b * 4 + 0] = o0;
+    d.orient[b * 4 + 1] = o1;
+    d.orient[b * 4 + 2] = o2;
+  }
+  const int per = (HW + nt - 1) / nt;
+  const int c0 = min(tid * per, HW), c1 = min(c0 + per, HW);
+  // 0 = skip, 1 = segmented, 2 = outlier
+  auto kind = [&](int cell) -> int {
+    const int i = cell / W, j = cell - i * W;
+    const int L = lab[cell];
+    const int8_t gv = g[cell];
+    if (!(L > 0 || gv == 1)) return 0;
+    if (L == 999999) return (i > c.gsi && j % 5 == 0) ? 2 : 0;
+    if (gv == 1 && (j % 5 != 0 && j > 5 && j < W - 5)) return 0;
+    return 1;
+  };
+  int ns = 0, no = 0;
+  for (int cell = c0; cell < c1; ++cell) {
+    const int k = kind(cell);
+    ns += k == 1;
+    no += k == 2;
+  }
+  int S, O;
+  int ps = block_excl_scan(ns, tmp, &S);
+  int po = block_excl_scan(no, tmp, &O);
+  for (int cell = c0; cell < c1; ++cell) {
+    const int i = cell / W, j = cell - i * W;
+    if (j == 0) {
+      d.start_ring[b * H + i] = ps - 1 + 5;
+      if (i > 0) d.end_ring[b * H + i - 1] = ps - 1 - 5;
+    }
+    const int k = kind(cell);
+    if (k == 1) {
+      d.seg[base + ps] = d.full[base + cell];
+      d.seg_ground[base + ps] = g[cell] == 1;
+      d.seg_col[base + ps] = (uint32_t)j;
+      d.seg_range[base + ps] = d.range[base + cell];
+      d.seg_int[base + ps] = d.vis[base + cell];
+      ++ps;
+    } else if (k == 2) {
+      d.outl[base + po] = d.full[base + cell];
+      d.outl_int[base + po] = d.vis[base + cell];
+      ++po;
+    }
+  }
+  if (tid == 0) {
+    d.end_ring[b * H + H - 1] = S - 1 - 5;
+    cnt[C_S] = S;
+    cnt[C_O] = O;
+  }
+  // CloudInfo arrays are H*W long and zero past S (IP:184-186); FA reads a few past S.
+  for (int k = S + tid; k < HW; k += nt) {
+    d.seg_ground[base + k] = 0;
+    d.seg_col[base + k] = 0u;
+    d.seg_range[base + k] = 0.0f;
+  }
+}
+
+}  // namespace llsr

@@ -1,0 +1,297 @@
+// llsr_libm.h — bit-exact restatements of the glibc (2.31–2.35, sysdeps/ieee754/flt-32)
+// single-precision elementary functions that the LeGO-LOAM-SR hot path calls on floats.
+//
+// Why: the reference computes row/column indices, ground angles and DBSCAN scales with glibc
+// float libm (imageProjection.cpp:313 asinf, :321 atan2f, :559 acosf; featureAssociation.cpp:577
+// atan2f, :1330 atan2f, :1332 tanf). The device's own ocml functions round differently in a few
+// ULPs, which flips row/column truncation and threshold tests. These ports follow the fdlibm
+// algorithms glibc ships for these functions, written with explicit IEEE-754 single ops so they
+// produce identical bits on the host (g++ -ffp-contract=off) and on gfx950 (hipcc
+// -ffp-contract=off, correctly-rounded f32 divide/sqrt — hipcc's default).
+//
+// Validation: oracle/libm_check.cpp compares every function against the host glibc over all
+// 2^32 float inputs (asinf, acosf, atanf, tanf on |x| < 3pi/4) and over dense random/structured
+// pairs for atan2f. See DESIGN.md §libm.
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+#if defined(__HIPCC__)
+#define LLSR_HD __host__ __device__ __forceinline__
+#else
+#define LLSR_HD static inline
+#endif
+
+namespace llsr_libm {
+
+LLSR_HD uint32_t fbits(float f) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __float_as_uint(f);
+#else
+  uint32_t u; memcpy(&u, &f, 4); return u;
+#endif
+}
+LLSR_HD float bitsf(uint32_t u) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __uint_as_float(u);
+#else
+  float f; memcpy(&f, &u, 4); return f;
+#endif
+}
+LLSR_HD float fabs_(float x) { return bitsf(fbits(x) & 0x7fffffffu); }
+// IEEE correctly-rounded single sqrt on both sides.
+LLSR_HD float sqrt_(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_sqrtf(x);
+#else
+  return __builtin_sqrtf(x);
+#endif
+}
+
+// ---- asinf: glibc e_asinf.c (x + x^3 p(x^2) form, pio2_hi rounded up) ----------------------
+LLSR_HD float asinf_(float x) {
+  const float one = 1.0f, huge = 1.0e30f;
+  const float pio2_hi = 1.57079637050628662109375f;
+  const float pio2_lo = -4.37113900018624283e-8f;
+  const float pio4_hi = 0.785398185253143310546875f;
+  const float p0 = 1.666675248e-1f, p1 = 7.495297643e-2f, p2 = 4.547037598e-2f,
+              p3 = 2.417951451e-2f, p4 = 4.216630880e-2f;
+  int32_t hx = (int32_t)fbits(x);
+  int32_t ix = hx & 0x7fffffff;
+  float t, w, p, q, c, r, s;
+  if (ix == 0x3f800000) return x * pio2_hi + x * pio2_lo;
+  if (ix > 0x3f800000) return (x - x) / (x - x);
+  if (ix < 0x3f000000) {
+    if (ix < 0x32000000) {
+      if (huge + x > one) return x;
+    } else {
+      t = x * x;
+      w = t * (p0 + t * (p1 + t * (p2 + t * (p3 + t * p4))));
+      return x + x * w;
+    }
+  }
+  w = one - fabs_(x);
+  t = w * 0.5f;
+  p = t * (p0 + t * (p1 + t * (p2 + t * (p3 + t * p4))));
+  s = sqrt_(t);
+  if (ix >= 0x3F79999A) {
+    t = pio2_hi - (2.0f * (s + s * p) - pio2_lo);
+  } else {
+    w = bitsf(fbits(s) & 0xfffff000u);
+    c = (t - w * w) / (s + w);
+    r = p;
+    p = 2.0f * s * r - (pio2_lo - 2.0f * c);
+    q = pio4_hi - 2.0f * w;
+    t = pio4_hi - (p - q);
+  }
+  return hx > 0 ? t : -t;
+}
+
+// ---- acosf: glibc e_acosf.c (fdlibm rational R(z)=p/q) --------------------------------------
+LLSR_HD float acosf_(float x) {
+  const float one = 1.0f, pi = 3.1415925026e+00f, pio2_hi = 1.5707962513e+00f,
+              pio2_lo = 7.5497894159e-08f;
+  const float pS0 = 1.6666667163e-01f, pS1 = -3.2556581497e-01f, pS2 = 2.0121252537e-01f,
+              pS3 = -4.0055535734e-02f, pS4 = 7.9153501429e-04f, pS5 = 3.4793309169e-05f,
+              qS1 = -2.4033949375e+00f, qS2 = 2.0209457874e+00f, qS3 = -6.8828397989e-01f,
+              qS4 = 7.7038154006e-02f;
+  int32_t hx = (int32_t)fbits(x);
+  int32_t ix = hx & 0x7fffffff;
+  float z, p, q, r, w, s, c, df;
+  if (ix == 0x3f800000) {
+    if (hx > 0) return 0.0f;
+    return pi + 2.0f * pio2_lo;
+  } else if (ix > 0x3f800000) {
+    return (x - x) / (x - x);
+  }
+  if (ix < 0x3f000000) {
+    if (ix <= 0x32800000) return pio2_hi + pio2_lo;
+    z = x * x;
+    p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    r = p / q;
+    return pio2_hi - (x - (pio2_lo - x * r));
+  } else if (hx < 0) {
+    z = (one + x) * 0.5f;
+    p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    s = sqrt_(z);
+    r = p / q;
+    w = r * s - pio2_lo;
+    return pi - 2.0f * (s + w);
+  } else {
+    z = (one - x) * 0.5f;
+    s = sqrt_(z);
+    df = bitsf(fbits(s) & 0xfffff000u);
+    c = (z - df * df) / (s + df);
+    p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    r = p / q;
+    w = r * s + c;
+    return 2.0f * (df + w);
+  }
+}
+
+// ---- atanf: glibc s_atanf.c (fdlibm, 11-term odd/even split) --------------------------------
+LLSR_HD float atanf_(float x) {
+  const float atanhi0 = 4.6364760399e-01f, atanhi1 = 7.8539812565e-01f,
+              atanhi2 = 9.8279368877e-01f, atanhi3 = 1.5707962513e+00f;
+  const float atanlo0 = 5.0121582440e-09f, atanlo1 = 3.7748947079e-08f,
+              atanlo2 = 3.4473217170e-08f, atanlo3 = 7.5497894159e-08f;
+  const float aT0 = 3.3333334327e-01f, aT1 = -2.0000000298e-01f, aT2 = 1.4285714924e-01f,
+              aT3 = -1.1111110449e-01f, aT4 = 9.0908870101e-02f, aT5 = -7.6918758452e-02f,
+              aT6 = 6.6610731184e-02f, aT7 = -5.8335702866e-02f, aT8 = 4.9768779427e-02f,
+              aT9 = -3.6531571299e-02f, aT10 = 1.6285819933e-02f;
+  const float one = 1.0f, huge = 1.0e30f;
+  int32_t hx = (int32_t)fbits(x);
+  int32_t ix = hx & 0x7fffffff;
+  int id;
+  if (ix >= 0x4c000000) {
+    if (ix > 0x7f800000) return x + x;
+    return hx > 0 ? atanhi3 + atanlo3 : -atanhi3 - atanlo3;
+  }
+  if (ix < 0x3ee00000) {
+    if (ix < 0x31000000) {
+      if (huge + x > one) return x;
+    }
+    id = -1;
+  } else {
+    x = fabs_(x);
+    if (ix < 0x3f980000) {
+      if (ix < 0x3f300000) { id = 0; x = (2.0f * x - one) / (2.0f + x); }
+      else { id = 1; x = (x - one) / (x + one); }
+    } else {
+      if (ix < 0x401c0000) { id = 2; x = (x - 1.5f) / (one + 1.5f * x); }
+      else { id = 3; x = -1.0f / x; }
+    }
+  }
+  float z = x * x;
+  float w = z * z;
+  float s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+  float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+  if (id < 0) return x - x * (s1 + s2);
+  float hi = id == 0 ? atanhi0 : id == 1 ? atanhi1 : id == 2 ? atanhi2 : atanhi3;
+  float lo = id == 0 ? atanlo0 : id == 1 ? atanlo1 : id == 2 ? atanlo2 : atanlo3;
+  z = hi - ((x * (s1 + s2) - lo) - x);
+  return hx < 0 ? -z : z;
+}
+
+// ---- atan2f: glibc e_atan2f.c -----------------------------------------------------------------
+LLSR_HD float atan2f_(float y, float x) {
+  const float tiny = 1.0e-30f, zero = 0.0f, pi_o_4 = 7.8539818525e-01f,
+              pi_o_2 = 1.5707963705e+00f, pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
+  int32_t hx = (int32_t)fbits(x), ix = hx & 0x7fffffff;
+  int32_t hy = (int32_t)fbits(y), iy = hy & 0x7fffffff;
+  if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
+  if (hx == 0x3f800000) return atanf_(y);
+  int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+  if (iy == 0) {
+    switch (m) {
+      case 0: case 1: return y;
+      case 2: return pi + tiny;
+      default: return -pi - tiny;
+    }
+  }
+  if (ix == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+  if (ix == 0x7f800000) {
+    if (iy == 0x7f800000) {
+      switch (m) {
+        case 0: return pi_o_4 + tiny;
+        case 1: return -pi_o_4 - tiny;
+        case 2: return 3.0f * pi_o_4 + tiny;
+        default: return -3.0f * pi_o_4 - tiny;
+      }
+    } else {
+      switch (m) {
+        case 0: return zero;
+        case 1: return -zero;
+        case 2: return pi + tiny;
+        default: return -pi - tiny;
+      }
+    }
+  }
+  if (iy == 0x7f800000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+  int32_t k = (iy - ix) >> 23;
+  float z;
+  if (k > 60) z = pi_o_2 + 0.5f * pi_lo;
+  else if (hx < 0 && k < -60) z = 0.0f;
+  else z = atanf_(fabs_(y / x));
+  switch (m) {
+    case 0: return z;
+    case 1: return bitsf(fbits(z) ^ 0x80000000u);
+    case 2: return pi - (z - pi_lo);
+    default: return (z - pi_lo) - pi;
+  }
+}
+
+// ---- tanf: glibc s_tanf.c + k_tanf.c; argument reduction only for |x| < 3pi/4 ---------------
+// (the hot path only evaluates tanf(atan2f(z, r_xy) +- res_Y) with |arg| <= pi/2 + res_Y).
+LLSR_HD float kernel_tanf_(float x, float y, int iy) {
+  const float one = 1.0f, pio4 = 7.8539812565e-01f, pio4lo = 3.7748947079e-08f;
+  const float T0 = 3.3333334327e-01f, T1 = 1.3333334029e-01f, T2 = 5.3968254477e-02f,
+              T3 = 2.1869488060e-02f, T4 = 8.8632395491e-03f, T5 = 3.5920790397e-03f,
+              T6 = 1.4562094584e-03f, T7 = 5.8804126456e-04f, T8 = 2.4646313977e-04f,
+              T9 = 7.8179444245e-05f, T10 = 7.1407252108e-05f, T11 = -1.8558637748e-05f,
+              T12 = 2.5907305826e-05f;
+  int32_t hx = (int32_t)fbits(x);
+  int32_t ix = hx & 0x7fffffff;
+  float z, r, v, w, s;
+  if (ix < 0x39000000) {
+    if ((int)x == 0) {
+      if ((ix | (iy + 1)) == 0) return one / fabs_(x);
+      else if (iy == 1) return x;
+      else return -one / x;
+    }
+  }
+  if (ix >= 0x3f2ca140) {
+    if (hx < 0) { x = -x; y = -y; }
+    z = pio4 - x;
+    w = pio4lo - y;
+    x = z + w; y = 0.0f;
+    if (fabs_(x) < 0x1p-13f)
+      return (float)((1 - ((hx >> 30) & 2)) * iy) * (1.0f - 2.0f * (float)iy * x);
+  }
+  z = x * x;
+  w = z * z;
+  r = T1 + w * (T3 + w * (T5 + w * (T7 + w * (T9 + w * T11))));
+  v = z * (T2 + w * (T4 + w * (T6 + w * (T8 + w * (T10 + w * T12)))));
+  s = z * x;
+  r = y + z * (s * (r + v) + y);
+  r += T0 * s;
+  w = x + r;
+  if (ix >= 0x3f2ca140) {
+    v = (float)iy;
+    return (float)(1 - ((hx >> 30) & 2)) * (v - 2.0f * (x - (w * w / (w + v) - r)));
+  }
+  if (iy == 1) return w;
+  float a, t;
+  z = bitsf(fbits(w) & 0xfffff000u);
+  v = r - (z - x);
+  t = a = -1.0f / w;
+  t = bitsf(fbits(t) & 0xfffff000u);
+  s = 1.0f + t * z;
+  return t + a * (s + t * v);
+}
+
+LLSR_HD float tanf_(float x) {
+  int32_t hx = (int32_t)fbits(x);
+  int32_t ix = hx & 0x7fffffff;
+  if (ix <= 0x3f490fda) return kernel_tanf_(x, 0.0f, 1);
+  if (ix >= 0x7f800000) return x - x;
+  // glibc's __ieee754_rem_pio2f reuses the sincosf "reduce_fast" step (double precision,
+  // 2/pi prescaled by 2^24 so the quadrant lands in bits 24..31). It is exact for |x| <= 120;
+  // beyond that (never reached: the hot path's arguments are bounded by pi/2 + res_Y) return
+  // NaN so a misuse is loud, never silently inexact.
+  if (ix < 0x42f00000) {
+    double dx = (double)x;
+    double r = dx * 0x1.45F306DC9C883p+23;
+    int32_t n = ((int32_t)r + 0x800000) >> 24;
+    dx = dx - (double)n * 0x1.921FB54442D18p0;
+    float y0 = (float)dx;
+    float y1 = (float)(dx - (double)y0);
+    return kernel_tanf_(y0, y1, 1 - ((n & 1) << 1));
+  }
+  return bitsf(0x7fc00000u);
+}
+
+}  // namespace llsr_libm

@@ -1,0 +1,163 @@
+"""Python host binding of the MI355X LeGO-LOAM-SR hot path (ctypes over include/llsr.h).
+
+Mirrors the reference's node-level interface for this path:
+
+* `ImageProjection.cloud_handler(points)` ~ ImageProjection::cloudHandler (imageProjection.cpp:189)
+  -> a ProjectionOut-like dict (segmented / outlier clouds + CloudInfo fields).
+* `FeatureAssociation.extract(...)` ~ the feature stage of runFeatureAssociation
+  (featureAssociation.cpp:2766-2775).
+* `Pipeline.process_scan` runs both for one scan; `Pipeline.process_batch` runs B scans that are
+  already resident in HBM (device pointers, e.g. from torch tensors).
+
+There is no CPU fallback: if libllsr.so (the HIP build) is missing or no HIP device is present,
+construction raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _abi
+from ._abi import Config, config_for  # noqa: F401
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PKG = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(_PKG, "libllsr.so")
+_LIB = None
+
+EXPORTS = [
+    "llsr_config_default", "llsr_create", "llsr_destroy", "llsr_last_error", "llsr_query_sizes",
+    "llsr_reset_state", "llsr_process_scan", "llsr_process_batch", "llsr_fetch_scan",
+    "llsr_batch_counts", "llsr_kernel_times_ms", "llsr_kernel_name", "llsr_set_profiling",
+]
+
+
+class LlsrError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libllsr.so (raises if it has not been built)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise LlsrError(f"{LIB_PATH} missing: build it with `make -C lego-loam-sr_amd` "
+                            "(there is no CPU fallback for the HIP path)")
+        L = C.CDLL(LIB_PATH)
+        L.llsr_config_default.argtypes = [C.POINTER(Config), C.c_int32]
+        L.llsr_create.argtypes = [C.POINTER(Config), C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]
+        L.llsr_destroy.argtypes = [C.c_void_p]
+        L.llsr_last_error.restype = C.c_char_p
+        L.llsr_last_error.argtypes = [C.c_void_p]
+        L.llsr_query_sizes.argtypes = [C.c_void_p, C.POINTER(_abi.Sizes)]
+        L.llsr_reset_state.argtypes = [C.c_void_p]
+        L.llsr_process_scan.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(_abi.ScanOut)]
+        L.llsr_process_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
+        L.llsr_fetch_scan.argtypes = [C.c_void_p, C.c_int32, C.POINTER(_abi.ScanOut)]
+        L.llsr_batch_counts.argtypes = [C.c_void_p, C.c_void_p]
+        L.llsr_kernel_times_ms.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+        L.llsr_kernel_name.restype = C.c_char_p
+        L.llsr_kernel_name.argtypes = [C.c_int32]
+        L.llsr_set_profiling.argtypes = [C.c_void_p, C.c_int32]
+        for fn in EXPORTS:
+            if fn not in ("llsr_last_error", "llsr_kernel_name", "llsr_destroy"):
+                getattr(L, fn).restype = C.c_int32
+        L.llsr_destroy.restype = None
+        _LIB = L
+    return _LIB
+
+
+def default_config(lidar: str, horizontal: int | None = None) -> Config:
+    c = Config()
+    code = {"vlp16": _abi.LLSR_LIDAR_VLP16, "hdl64e": _abi.LLSR_LIDAR_HDL64E}[lidar]
+    rc = lib().llsr_config_default(C.byref(c), code)
+    if rc != 0:
+        raise LlsrError(f"llsr_config_default: {rc}")
+    if horizontal is not None:
+        c.num_horizontal_scans = horizontal
+    return c
+
+
+class Pipeline:
+    """One llsr handle: ImageProjection + FeatureAssociation feature stage on a HIP device."""
+
+    def __init__(self, cfg: Config, device: int = 0, max_batch: int = 1, max_points: int | None = None):
+        self.cfg = cfg
+        H, W = cfg.num_vertical_scans, cfg.num_horizontal_scans
+        self.max_points = max_points or 2 * H * W
+        self.max_batch = max_batch
+        h = C.c_void_p()
+        rc = lib().llsr_create(C.byref(cfg), device, max_batch, self.max_points, C.byref(h))
+        if rc != 0:
+            raise LlsrError(f"llsr_create failed ({rc}): no HIP device or invalid config")
+        self._h = h
+        self.out = _abi.OutBuffers(H, W)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().llsr_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise LlsrError(f"{what} failed ({rc}): {lib().llsr_last_error(self._h).decode()}")
+
+    def reset(self):
+        self._check(lib().llsr_reset_state(self._h), "llsr_reset_state")
+
+    def process_scan(self, xyzi: np.ndarray) -> dict:
+        xyzi = np.ascontiguousarray(xyzi, dtype=np.float32).reshape(-1, 4)
+        self._check(lib().llsr_process_scan(self._h, xyzi.ctypes.data, xyzi.shape[0], C.byref(self.out.struct)),
+                    "llsr_process_scan")
+        return self.out.result()
+
+    def process_batch(self, d_xyzi: int, d_offsets: int, B: int, stream: int = 0):
+        """Enqueue B device-resident scans (raw device pointers) on a hipStream_t (0 = own)."""
+        self._check(lib().llsr_process_batch(self._h, C.c_void_p(d_xyzi), C.c_void_p(d_offsets), B,
+                                             C.c_void_p(stream)), "llsr_process_batch")
+
+    def fetch(self, b: int) -> dict:
+        self._check(lib().llsr_fetch_scan(self._h, b, C.byref(self.out.struct)), "llsr_fetch_scan")
+        return self.out.result()
+
+    def batch_counts(self, B: int) -> np.ndarray:
+        buf = np.zeros((B, 8), dtype=np.int32)
+        self._check(lib().llsr_batch_counts(self._h, buf.ctypes.data), "llsr_batch_counts")
+        return buf
+
+    def set_profiling(self, on: bool):
+        self._check(lib().llsr_set_profiling(self._h, 1 if on else 0), "llsr_set_profiling")
+
+    def kernel_times(self) -> dict:
+        buf = np.zeros(32, dtype=np.float32)
+        n = lib().llsr_kernel_times_ms(self._h, buf.ctypes.data, 32)
+        if n < 0:
+            self._check(n, "llsr_kernel_times_ms")
+        return {lib().llsr_kernel_name(k).decode(): float(buf[k]) for k in range(n)}
+
+
+class ImageProjection:
+    """Drop-in for ImageProjection::cloudHandler's arithmetic (IP:189-222)."""
+
+    def __init__(self, pipeline: Pipeline):
+        self.p = pipeline
+
+    def cloud_handler(self, xyzi: np.ndarray) -> dict:
+        r = self.p.process_scan(xyzi)
+        return {
+            "segmented_cloud": r["seg_xyzi"], "outlier_cloud": r["outlier_xyzi"],
+            "seg_msg": {
+                "start_ring_index": r["start_ring_index"], "end_ring_index": r["end_ring_index"],
+                "start_orientation": float(r["orientation"][0]), "end_orientation": float(r["orientation"][1]),
+                "orientation_diff": float(r["orientation"][2]),
+                "segmented_cloud_ground_flag": r["seg_ground_flag"].astype(bool),
+                "segmented_cloud_col_ind": r["seg_col_ind"], "segmented_cloud_range": r["seg_range"],
+            },
+            "outlierCloud_Intensity": r["outlier_intensity"].astype(np.float64),
+            "segmentedCloud_Intensity": r["seg_intensity"].astype(np.float64),
+            "_full": r,
+        }

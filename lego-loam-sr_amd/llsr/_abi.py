@@ -1,0 +1,177 @@
+"""ctypes mirror of include/llsr.h (the C-ABI boundary). Plain data types only."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+LLSR_OK = 0
+LLSR_LIDAR_VLP16 = 0
+LLSR_LIDAR_HDL64E = 2
+LLSR_MODE_FAITHFUL = 0
+LLSR_MODE_LM_APPLIED = 1
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("num_vertical_scans", C.c_int32),
+        ("num_horizontal_scans", C.c_int32),
+        ("vertical_angle_bottom", C.c_float),
+        ("vertical_angle_top", C.c_float),
+        ("sensor_mount_angle", C.c_float),
+        ("ground_scan_index", C.c_int32),
+        ("use_kitti", C.c_int32),
+        ("use_vlp32c", C.c_int32),
+        ("segment_theta", C.c_float),
+        ("segment_valid_point_num", C.c_int32),
+        ("segment_valid_line_num", C.c_int32),
+        ("scan_period", C.c_float),
+        ("edge_threshold", C.c_float),
+        ("surf_threshold", C.c_float),
+        ("nearest_feature_search_distance", C.c_float),
+        ("DBFr", C.c_float),
+        ("RatioXY", C.c_float),
+        ("RatioZ", C.c_float),
+        ("mapping_frequency_divider", C.c_int32),
+        ("iterCountThres", C.c_int32),
+        ("step_size", C.c_float),
+        ("stop_thres", C.c_float),
+        ("mode", C.c_int32),
+    ]
+
+
+def config_for(lidar: str, horizontal: int | None = None) -> Config:
+    """The loam_config.yaml block (VLP-16: lines 1-67, HDL-64E: 137-203) as a Config.
+
+    Pure-Python copy of llsr_config_default so the oracle can be configured without the
+    product library; tests check both agree.
+    """
+    c = Config()
+    if lidar == "vlp16":
+        c.num_vertical_scans, c.num_horizontal_scans = 16, 1800
+        c.vertical_angle_bottom, c.vertical_angle_top = -15.0, 15.0
+        c.ground_scan_index, c.use_kitti = 7, 0
+        c.DBFr, c.RatioXY, c.RatioZ = 5.0, 0.5, 2.5
+        c.edge_threshold, c.surf_threshold, c.nearest_feature_search_distance = 0.03, 0.03, 5.0
+    elif lidar == "hdl64e":
+        c.num_vertical_scans, c.num_horizontal_scans = 64, 1800
+        c.vertical_angle_bottom, c.vertical_angle_top = -24.8, 2.0
+        c.ground_scan_index, c.use_kitti = 50, 1
+        c.DBFr, c.RatioXY, c.RatioZ = 7.5, 0.3, 5.0
+        c.edge_threshold, c.surf_threshold, c.nearest_feature_search_distance = 0.005, 0.005, 25.0
+    else:
+        raise ValueError(lidar)
+    if horizontal is not None:
+        c.num_horizontal_scans = horizontal
+    c.sensor_mount_angle = 0.0
+    c.use_vlp32c = 0
+    c.segment_theta, c.segment_valid_point_num, c.segment_valid_line_num = 60.0, 5, 3
+    c.scan_period = 0.1
+    c.mapping_frequency_divider = 1
+    c.iterCountThres, c.step_size, c.stop_thres = 200, 1.0, 0.05
+    c.mode = LLSR_MODE_FAITHFUL
+    return c
+
+
+_P = C.c_void_p
+
+
+class ScanOut(C.Structure):
+    _fields_ = [
+        ("n_points", C.c_int32),
+        ("orientation", C.c_float * 3),
+        ("range_image", _P),
+        ("cell_point", _P),
+        ("ground_image", _P),
+        ("label_image", _P),
+        ("start_ring_index", _P),
+        ("end_ring_index", _P),
+        ("n_segmented", C.c_int32),
+        ("seg_xyzi", _P),
+        ("seg_ground_flag", _P),
+        ("seg_col_ind", _P),
+        ("seg_range", _P),
+        ("seg_intensity", _P),
+        ("n_outlier", C.c_int32),
+        ("outlier_xyzi", _P),
+        ("outlier_intensity", _P),
+        ("n_near", C.c_int32),
+        ("n_ransac_inliers", C.c_int32),
+        ("ransac_iterations", C.c_int32),
+        ("loam_xyzi", _P),
+        ("curvature", _P),
+        ("picked", _P),
+        ("label", _P),
+        ("n_less_sharp", C.c_int32),
+        ("less_sharp_ind", _P),
+        ("dbscan_cluster", _P),
+        ("n_sharp", C.c_int32),
+        ("sharp_ind", _P),
+        ("n_flat", C.c_int32),
+        ("flat_ind", _P),
+        ("n_less_flat", C.c_int32),
+        ("less_flat_xyzi", _P),
+    ]
+
+
+class Sizes(C.Structure):
+    _fields_ = [("cells", C.c_int32), ("rings", C.c_int32), ("max_points", C.c_int32),
+                ("shadow_points", C.c_int32)]
+
+
+# (field, dtype, elements per cell/point) for the array outputs; "HW" arrays sized H*W, "H"
+# arrays sized H, the rest sized to the H*W bound and trimmed by their count field.
+ARRAYS = [
+    ("range_image", np.float32, "HW", 1, None),
+    ("cell_point", np.int32, "HW", 1, None),
+    ("ground_image", np.int8, "HW", 1, None),
+    ("label_image", np.int32, "HW", 1, None),
+    ("start_ring_index", np.int32, "H", 1, None),
+    ("end_ring_index", np.int32, "H", 1, None),
+    ("seg_xyzi", np.float32, "HW", 4, "n_segmented"),
+    ("seg_ground_flag", np.uint8, "HW", 1, "n_segmented"),
+    ("seg_col_ind", np.uint32, "HW", 1, "n_segmented"),
+    ("seg_range", np.float32, "HW", 1, "n_segmented"),
+    ("seg_intensity", np.float32, "HW", 1, "n_segmented"),
+    ("outlier_xyzi", np.float32, "HW", 4, "n_outlier"),
+    ("outlier_intensity", np.float32, "HW", 1, "n_outlier"),
+    ("loam_xyzi", np.float32, "HW", 4, "n_segmented"),
+    ("curvature", np.float32, "HW", 1, "n_segmented"),
+    ("picked", np.uint8, "HW", 1, "n_segmented"),
+    ("label", np.int8, "HW", 1, "n_segmented"),
+    ("less_sharp_ind", np.int32, "HW", 1, "n_less_sharp"),
+    ("dbscan_cluster", np.int32, "HW", 1, "n_less_sharp"),
+    ("sharp_ind", np.int32, "HW", 1, "n_sharp"),
+    ("flat_ind", np.int32, "HW", 1, "n_flat"),
+    ("less_flat_xyzi", np.float32, "HW", 4, "n_less_flat"),
+]
+
+COUNTS = ["n_points", "n_segmented", "n_outlier", "n_near", "n_ransac_inliers",
+          "ransac_iterations", "n_less_sharp", "n_sharp", "n_flat", "n_less_flat"]
+
+
+class OutBuffers:
+    """Host numpy buffers bound to a ScanOut; `result()` returns trimmed copies."""
+
+    def __init__(self, H: int, W: int):
+        self.H, self.W = H, W
+        self.struct = ScanOut()
+        self.bufs = {}
+        for name, dt, kind, per, _ in ARRAYS:
+            n = (H * W if kind == "HW" else H) * per
+            a = np.zeros(n, dtype=dt)
+            self.bufs[name] = a
+            setattr(self.struct, name, a.ctypes.data)
+
+    def result(self) -> dict:
+        s = self.struct
+        r = {k: int(getattr(s, k)) for k in COUNTS}
+        r["orientation"] = np.array(s.orientation[:], dtype=np.float32)
+        for name, dt, kind, per, cnt in ARRAYS:
+            a = self.bufs[name]
+            if cnt is not None:
+                a = a[: r[cnt] * per]
+            if per == 4:
+                a = a.reshape(-1, 4)
+            r[name] = a.copy()
+        return r

@@ -1,0 +1,36 @@
+/* oracle.h — TEST INFRASTRUCTURE ONLY. CPU restatement of the LeGO-LOAM-SR hot path used as
+ * the parity checker (tests/, __graft_entry__.smoke) and as bench.py's cpu_baseline leg.
+ * Never linked into the product library (lego-loam-sr_amd/).
+ *
+ * Parity status: the reference cannot be built here (ROS2/PCL/Eigen/GTSAM absent, SURVEY.md
+ * §8c) and holds no golden vectors for this path, so this restatement is "parity unpinned"
+ * against the reference binary. What IS pinned: its libm calls are host glibc, and the device
+ * libm ports are checked bit-exactly against that glibc (libm_check.cpp); its kNN is checked
+ * against the reference's vendored nanoflann.hpp compiled by path (oracle/Makefile, _ref/).
+ */
+#ifndef LLSR_ORACLE_H_
+#define LLSR_ORACLE_H_
+#include "../include/llsr.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct oracle_state oracle_state;
+
+oracle_state* oracle_create(const llsr_config* cfg);
+void oracle_destroy(oracle_state* s);
+/* Reset the FA carry-over arrays (FA:167-198) to their value-initialised state. */
+void oracle_reset(oracle_state* s);
+/* One scan through ImageProjection::cloudHandler (IP:189-222) and the FeatureAssociation
+ * feature stage (FA:2766-2775). Same output layout/semantics as llsr_process_scan. */
+int32_t oracle_process_scan(oracle_state* s, const float* xyzi, int32_t n, llsr_scan_out* out);
+/* Per-stage wall time of the last oracle_process_scan (ms): IP, FA-features. */
+void oracle_stage_ms(const oracle_state* s, double* ip_ms, double* fa_ms);
+/* RANSAC with a caller seed (seed 12345 = PCL default) over the last scan's near-ground cloud;
+ * used to show the synthetic scenes' inlier sets do not depend on the RNG. */
+int32_t oracle_ransac_inliers(oracle_state* s, uint32_t seed, int32_t* inliers, int32_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

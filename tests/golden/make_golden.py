@@ -1,0 +1,39 @@
+"""Regenerate the golden fixtures (run from the repo root: python tests/golden/make_golden.py).
+
+The reference cannot be built or imported here (ROS2/PCL/Eigen absent) and ships
+no golden vectors for this path, so these fixtures pin the CPU restatement (oracle/) on seeded
+synthetic scans: two consecutive VLP-16 frames through one oracle instance (the second frame
+exercises FeatureAssociation's carry-over state). Inputs are stored too, so the fixtures do not
+depend on numpy's RNG stream. Parity against the reference binary itself is unpinned.
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "lego-loam-sr_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+from llsr import _abi, synth  # noqa: E402
+import oracle_py  # noqa: E402
+
+SEEDS = (1, 2)
+
+
+def main():
+    cfg = _abi.config_for("vlp16")
+    ora = oracle_py.Oracle(cfg)
+    for k, seed in enumerate(SEEDS):
+        pts = synth.make_scan(seed, "vlp16")
+        r = ora.process(pts)
+        arrays = {f"out_{name}": r[name] for name, *_ in _abi.ARRAYS}
+        counts = np.array([r[c] for c in _abi.COUNTS], dtype=np.int64)
+        np.savez_compressed(os.path.join(HERE, f"vlp16_frame{k}.npz"), input=pts, seed=seed,
+                            counts=counts, orientation=r["orientation"], **arrays)
+        print(f"frame {k} seed {seed}: " + ", ".join(f"{c}={r[c]}" for c in _abi.COUNTS))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,66 @@
+"""CPU tests of the C-ABI boundary: the HIP library builds for gfx950, loads, exports every entry
+point include/llsr.h declares, and its host-only helpers agree with the Python mirror. No compute
+call is made here (no GPU in this container): creating a handle must fail loudly with ENODEV."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+import llsr
+from llsr import _abi
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "llsr.h")
+
+
+def _declared():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(llsr_[a-z_]+)\s*\(", text)))
+
+
+def test_header_declares_expected_surface():
+    assert set(llsr.EXPORTS) == set(_declared())
+
+
+def test_library_exports_every_declared_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", llsr.LIB_PATH], check=True,
+                         capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (llsr_\w+)", out))
+    missing = set(_declared()) - exported
+    assert not missing, missing
+
+
+def test_library_has_gfx950_code_object():
+    blob = open(llsr.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+@pytest.mark.parametrize("lidar,horizontal", [("vlp16", None), ("hdl64e", None)])
+def test_config_default_matches_yaml_mirror(lidar, horizontal):
+    a = llsr.default_config(lidar, horizontal)
+    b = _abi.config_for(lidar, horizontal)
+    for name, _ in _abi.Config._fields_:
+        assert getattr(a, name) == getattr(b, name), name
+
+
+def test_struct_sizes_match_header():
+    # llsr_config: 23 4-byte fields; llsr_scan_out: pointer/int layout as declared
+    assert C.sizeof(_abi.Config) == 23 * 4
+    assert C.sizeof(_abi.Sizes) == 16
+
+
+def test_create_without_device_fails_loudly():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("a HIP device is visible")
+    except Exception:
+        pass
+    h = C.c_void_p()
+    cfg = llsr.default_config("vlp16")
+    rc = llsr.lib().llsr_create(C.byref(cfg), 0, 1, 1000, C.byref(h))
+    assert rc == -19 and not h.value  # LLSR_ENODEV: no silent CPU fallback
+    with pytest.raises(llsr.LlsrError):
+        llsr.Pipeline(cfg)

@@ -1,0 +1,198 @@
+"""CPU tests of the oracle (test infrastructure) — golden fixtures, invariants, RANSAC
+seed-independence of the synthetic scenes, and CPU re-derivations of the parallel algorithms the
+HIP kernels use (union-find labelling, ADD automaton scan) checked against the oracle's serial
+restatement."""
+import os
+
+import numpy as np
+import pytest
+
+from llsr import _abi, synth
+import oracle_py
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def vlp_cfg():
+    return _abi.config_for("vlp16")
+
+
+def test_golden_fixtures_reproduce(vlp_cfg):
+    ora = oracle_py.Oracle(vlp_cfg)
+    for k in range(2):
+        z = np.load(os.path.join(GOLDEN, f"vlp16_frame{k}.npz"))
+        regen = synth.make_scan(int(z["seed"]), "vlp16")
+        assert np.array_equal(regen.view(np.uint32), z["input"].view(np.uint32)), "synth is not deterministic"
+        r = ora.process(z["input"])
+        assert [r[c] for c in _abi.COUNTS] == z["counts"].tolist()
+        assert np.array_equal(r["orientation"], z["orientation"])
+        for name, *_ in _abi.ARRAYS:
+            a, b = np.asarray(r[name]), z[f"out_{name}"]
+            if a.dtype == np.float32:
+                a, b = a.view(np.uint32), b.view(np.uint32)
+            assert np.array_equal(a, b), name
+
+
+def test_ransac_inliers_seed_independent(vlp_cfg):
+    ora = oracle_py.Oracle(vlp_cfg)
+    for seed in (1, 40, 77):
+        ora.process(synth.make_scan(seed, "vlp16"))
+        ref = ora.ransac_inliers(12345)
+        assert ref.size > 100
+        for s in (1, 2, 99, 2024):
+            assert np.array_equal(ora.ransac_inliers(s), ref)
+
+
+def test_invariants(vlp_cfg):
+    ora = oracle_py.Oracle(vlp_cfg)
+    H, W = 16, 1800
+    r = ora.process(synth.make_scan(3, "vlp16"))
+    S = r["n_segmented"]
+    # ring indices follow IP:794/831
+    counts = np.diff(np.concatenate([[0], r["end_ring_index"] + 6]))
+    assert np.array_equal(r["start_ring_index"][0], 4)
+    assert counts.sum() == S
+    # segmented column indices are row-major ordered within each ring
+    lab, g = r["label_image"].reshape(H, W), r["ground_image"].reshape(H, W)
+    assert set(np.unique(g)).issubset({-1, 0, 1})
+    assert (lab[g == 1] == -1).all()
+    assert ((lab == -1) | (lab == 999999) | (lab >= 1)).all()
+    # features are disjoint and indices in range
+    e, f = r["less_sharp_ind"], r["flat_ind"]
+    assert len(set(e.tolist()) & set(f.tolist())) == 0
+    assert e.max() < S and f.max() < S
+    assert set(r["sharp_ind"].tolist()).issubset(set(e.tolist()))
+    assert (r["label"][e] == 1).all()
+
+
+def _uf_labels(rng_img, lab_img, H, W, cfg):
+    """CPU restatement of k_label's algorithm (union-find, min-index root, stats, rank)."""
+    HW = H * W
+    parent = np.arange(HW)
+    l0 = (lab_img.reshape(-1) == 0)
+    r = rng_img.reshape(-1)
+    resX = np.float32((np.pi * 2) / W)
+    resY = np.float32(np.deg2rad(1.0) * (cfg.vertical_angle_top - cfg.vertical_angle_bottom) / np.float32(H - 1))
+    thr = np.tan(np.float32(cfg.segment_theta * np.deg2rad(1.0)))
+
+    def edge(a, b, alpha):
+        d1, d2 = np.maximum(r[a], r[b]), np.minimum(r[a], r[b])
+        s, c = np.sin(alpha, dtype=np.float32), np.cos(alpha, dtype=np.float32)
+        return (d2 * s / (d1 - d2 * c)) > thr
+
+    def find(x):
+        while parent[x] != x:
+            parent[x] = parent[parent[x]]
+            x = parent[x]
+        return x
+
+    cells = np.nonzero(l0)[0]
+    for c in cells:
+        i, j = divmod(int(c), W)
+        nbrs = [(i * W + (j + 1) % W, resX)]
+        if i + 1 < H:
+            nbrs.append(((i + 1) * W + j, resY))
+        for n, alpha in nbrs:
+            if l0[n] and edge(c, n, alpha):
+                a, b = find(c), find(n)
+                if a != b:
+                    parent[max(a, b)] = min(a, b)
+    root = np.array([find(c) if l0[c] else -1 for c in range(HW)])
+    out = np.where(l0, 0, lab_img.reshape(-1)).astype(np.int64)
+    rank = 0
+    for c in range(HW):
+        if not l0[c] or root[c] != c:
+            continue
+        members = np.nonzero(root == c)[0]
+        rows = set((members[members != c] // W).tolist())
+        feas = members.size >= 30 or (members.size >= cfg.segment_valid_point_num and len(rows) >= cfg.segment_valid_line_num)
+        if feas:
+            rank += 1
+        out[members] = rank if feas else 999999
+    return out.reshape(H, W)
+
+
+def test_union_find_labelling_matches_bfs():
+    """The HIP labeller's algorithm (union-find) equals the reference BFS on a small image."""
+    cfg = _abi.config_for("vlp16", horizontal=120)
+    ora = oracle_py.Oracle(cfg)
+    # a coarse 16 x 120 scan: subsample a full scan's azimuths so the BFS has real structure
+    full = synth.make_scan(4, "vlp16").reshape(1800, 16, 4)[::15].reshape(-1, 4)
+    r = ora.process(full)
+    H, W = 16, 120
+    lab = r["label_image"].reshape(H, W)
+    pre = np.where((r["ground_image"].reshape(H, W) == 1) | (r["range_image"].reshape(H, W) == np.float32(3.4028235e38)), -1, 0)
+    uf = _uf_labels(r["range_image"].reshape(H, W), pre, H, W, cfg)
+    assert np.array_equal(uf, lab)
+
+
+def _add_serial(g, cF, cB):
+    g = g.copy()
+    W = g.size
+    for j in range(2, W):
+        if g[j] == 2 and (g[j - 2] == 1 or g[j - 1] == 1) and cF[j]:
+            g[j] = 1
+    for j in range(W - 3, -1, -1):
+        if g[j] == 2 and (g[j + 2] == 1 or g[j + 1] == 1) and cB[j]:
+            g[j] = 1
+    return g
+
+
+def _add_scan(g, cF, cB, lanes=8):
+    """k_ground_add's chunked 4-state map scan, restated in Python."""
+    def col_map(one, cand):
+        f = 0
+        for s in range(4):
+            a, b = s & 1, s >> 1
+            c = 1 if one else (1 if (cand and (a or b)) else 0)
+            f |= (b | (c << 1)) << (2 * s)
+        return f
+
+    ap = lambda f, s: (f >> (2 * s)) & 3  # noqa: E731
+    comp = lambda g2, f: sum(ap(g2, ap(f, s)) << (2 * s) for s in range(4))  # noqa: E731
+    g = g.copy()
+    W = g.size
+    CH = -(-W // lanes)
+    for direction in ("fwd", "bwd"):
+        chunks = []
+        for l in range(lanes):
+            if direction == "fwd":
+                js = [j for j in range(l * CH, min(l * CH + CH, W)) if j >= 2]
+            else:
+                hi = W - 3 - l * CH
+                js = list(range(hi, max(hi - CH + 1, 0) - 1, -1)) if hi >= 0 else []
+            chunks.append(js)
+        maps = []
+        for js in chunks:
+            F = 0xE4
+            for j in js:
+                cand = g[j] == 2 and (cF[j] if direction == "fwd" else cB[j])
+                F = comp(col_map(g[j] == 1, cand), F)
+            maps.append(F)
+        s0 = (1 if g[0] == 1 else 0) | (2 if g[1] == 1 else 0) if direction == "fwd" else \
+             (1 if g[W - 1] == 1 else 0) | (2 if g[W - 2] == 1 else 0)
+        pref = 0xE4
+        newg = g.copy()
+        for js, F in zip(chunks, maps):
+            s = ap(pref, s0)
+            for j in js:
+                cand = g[j] == 2 and (cF[j] if direction == "fwd" else cB[j])
+                a, b = s & 1, s >> 1
+                one = g[j] == 1
+                if cand and (a or b):
+                    newg[j] = 1
+                    one = True
+                s = b | ((1 if one else 0) << 1)
+            pref = comp(F, pref)
+        g = newg
+    return g
+
+
+def test_add_automaton_scan_matches_serial():
+    rng = np.random.default_rng(0)
+    for W in (37, 64, 113, 200):
+        for _ in range(30):
+            g = rng.choice(np.array([-1, 0, 1, 2]), size=W, p=[0.1, 0.2, 0.3, 0.4])
+            cF, cB = rng.random(W) < 0.7, rng.random(W) < 0.7
+            assert np.array_equal(_add_scan(g, cF, cB), _add_serial(g, cF, cB))
