@@ -146,10 +146,12 @@ int32_t llsr_fetch_scan(llsr_handle* h, int32_t b, llsr_scan_out* out);
  * `out` must hold 8*B int32 (host). Synchronises. */
 int32_t llsr_batch_counts(llsr_handle* h, int32_t* out);
 
-/* Per-kernel timing of the last batch (HIP events on the handle's launch stream), in the
- * order of llsr_kernel_name(k). Returns the number of kernels written (<= cap). */
+/* Per-kernel device time (ms per batch, averaged over every batch enqueued since profiling was
+ * enabled) from HIP events recorded on each batch's launch stream between its kernels, in the
+ * order of llsr_kernel_name(k). Synchronises. Returns the number of kernels written (<= cap). */
 int32_t llsr_kernel_times_ms(llsr_handle* h, float* out, int32_t cap);
 const char* llsr_kernel_name(int32_t k);
+/* Enable/disable per-kernel event timing; (re)enabling clears the accumulated averages. */
 int32_t llsr_set_profiling(llsr_handle* h, int32_t enable);
 
 #ifdef __cplusplus

@@ -57,9 +57,12 @@ struct llsr_handle {
   hipStream_t last_stream = nullptr;
   int last_B = 0;
   bool profiling = false;
-  hipEvent_t ev[kNumKernels + 1] = {};
-  float ktimes[kNumKernels] = {};
-  bool have_times = false;
+  // Event sets for up to kRing in-flight profiled batches; retired sets are summed into ksum.
+  static constexpr int kRing = 64;
+  hipEvent_t ev[kRing][kNumKernels + 1] = {};
+  int ring_head = 0, ring_used = 0;
+  double ksum[kNumKernels] = {};
+  long long kbatches = 0;
   std::string err;
 };
 
@@ -210,7 +213,9 @@ extern "C" int32_t llsr_create(const llsr_config* cfg, int32_t hip_device, int32
     llsr_destroy(h);
     return LLSR_ENOMEM;
   }
-  for (auto& e : h->ev) hipEventCreate(&e);
+  for (auto& set : h->ev)
+    for (auto& e : set)
+      if (hipEventCreate(&e) != hipSuccess) { llsr_destroy(h); return LLSR_ENODEV; }
   if (h->dc.ccl_lds) {
     if (hipFuncSetAttribute((const void*)k_label<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             h->dc.HW * (int)sizeof(int)) != hipSuccess) {
@@ -228,8 +233,9 @@ extern "C" void llsr_destroy(llsr_handle* h) {
   if (!h) return;
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
-  for (auto& e : h->ev)
-    if (e) hipEventDestroy(e);
+  for (auto& set : h->ev)
+    for (auto& e : set)
+      if (e) (void)hipEventDestroy(e);
   if (h->pool) hipFree(h->pool);
   if (h->d_in) hipFree(h->d_in);
   if (h->d_off) hipFree(h->d_off);
@@ -258,8 +264,23 @@ extern "C" int32_t llsr_reset_state(llsr_handle* h) {
   return LLSR_OK;
 }
 
+// Retire the oldest profiled batch: wait for its last event and add its kernel intervals.
+static void retire_oldest(llsr_handle* h) {
+  const int slot = (h->ring_head - h->ring_used + llsr_handle::kRing) % llsr_handle::kRing;
+  (void)hipEventSynchronize(h->ev[slot][kNumKernels]);
+  for (int k = 0; k < kNumKernels; ++k) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, h->ev[slot][k], h->ev[slot][k + 1]) == hipSuccess) h->ksum[k] += ms;
+  }
+  h->kbatches += 1;
+  h->ring_used -= 1;
+}
+
 extern "C" int32_t llsr_set_profiling(llsr_handle* h, int32_t enable) {
   if (!h) return LLSR_EINVAL;
+  while (h->ring_used > 0) retire_oldest(h);
+  for (double& v : h->ksum) v = 0.0;
+  h->kbatches = 0;
   h->profiling = enable != 0;
   return LLSR_OK;
 }
@@ -273,8 +294,10 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   const DevCfg& c = h->dc;
   const float4* pts = reinterpret_cast<const float4*>(d_xyzi);
   int k = 0;
+  if (h->profiling && h->ring_used == llsr_handle::kRing) retire_oldest(h);
+  hipEvent_t* evs = h->ev[h->ring_head];
   auto mark = [&]() {
-    if (h->profiling) hipEventRecord(h->ev[k], s);
+    if (h->profiling) (void)hipEventRecord(evs[k], s);
     ++k;
   };
   mark();
@@ -303,9 +326,12 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   k_fa_finish<<<B, 1024, 0, s>>>(c, h->d);
   mark();
   HIP_OK(h, hipGetLastError());
+  if (h->profiling) {
+    h->ring_head = (h->ring_head + 1) % llsr_handle::kRing;
+    h->ring_used += 1;
+  }
   h->last_stream = s;
   h->last_B = B;
-  h->have_times = h->profiling;
   return LLSR_OK;
 }
 
@@ -317,15 +343,11 @@ static int32_t sync_last(llsr_handle* h) {
 
 extern "C" int32_t llsr_kernel_times_ms(llsr_handle* h, float* out, int32_t cap) {
   if (!h || !out) return LLSR_EINVAL;
-  if (!h->have_times) return 0;
-  int32_t rc = sync_last(h);
-  if (rc) return rc;
+  HIP_OK(h, hipSetDevice(h->device));
+  while (h->ring_used > 0) retire_oldest(h);
+  if (h->kbatches == 0) return 0;
   int n = 0;
-  for (int k = 0; k < kNumKernels && n < cap; ++k, ++n) {
-    float ms = 0.f;
-    hipEventElapsedTime(&ms, h->ev[k], h->ev[k + 1]);
-    out[n] = ms;
-  }
+  for (int k = 0; k < kNumKernels && n < cap; ++k, ++n) out[n] = (float)(h->ksum[k] / (double)h->kbatches);
   return n;
 }
 

@@ -24,8 +24,14 @@ def diff_report(name, g, o, limit=5):
     g, o = np.asarray(g), np.asarray(o)
     if g.shape != o.shape:
         return f"{name}: shape {g.shape} vs oracle {o.shape}"
-    gb, ob = _bits(g).reshape(g.shape[0], -1) if g.ndim else _bits(g), _bits(o).reshape(o.shape[0], -1) if o.ndim else _bits(o)
-    bad = np.nonzero(np.any(gb != ob, axis=-1) if gb.ndim > 1 else gb != ob)[0]
+    if g.size == 0:
+        return None
+    gb, ob = _bits(g), _bits(o)
+    if gb.ndim > 1:
+        gb, ob = gb.reshape(gb.shape[0], -1), ob.reshape(ob.shape[0], -1)
+        bad = np.nonzero(np.any(gb != ob, axis=1))[0]
+    else:
+        bad = np.nonzero(gb != ob)[0]
     if bad.size == 0:
         return None
     rows = ", ".join(f"[{k}] gpu={g[k].tolist()} oracle={o[k].tolist()}" for k in bad[:limit])
