@@ -323,7 +323,7 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   mark();
   k_select_ring<<<dim3(c.H, B), 256, 0, s>>>(c, h->d);
   mark();
-  k_fa_finish<<<B, 1024, 0, s>>>(c, h->d);
+  k_fa_finish<<<B, 64, 0, s>>>(c, h->d);
   mark();
   HIP_OK(h, hipGetLastError());
   if (h->profiling) {

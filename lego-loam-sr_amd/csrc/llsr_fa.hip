@@ -131,12 +131,15 @@ __global__ __launch_bounds__(1024) void k_fa_points(DevCfg c, DevBufs d) {
 
 // ---------------------------------------------------------------------------------------------
 // K8 per-ring selection (FA:1165-1271). One workgroup (256 threads) per (scan, ring).
-// cloudSmoothness[sp, ep) is sorted by value (ties by index; the reference's introsort leaves
-// tie order unspecified), position 4 carries the never-overwritten phantom {0, ind 0}
-// (FA:169, 819), position ep stays unsorted. Lane 0 then runs the serial edge (ep..sp) and flat
-// (sp..ep) loops against an LDS window [sp-5, ep+5] of picked/col/ground/curvature; ring windows
-// are disjoint (11 positions separate ep_r from sp_{r+1}), so rings run concurrently.
-// Less-flat points are compacted and voxel-downsampled (PCL VoxelGrid leaf 0.2) in-block.
+// Reference order: cloudSmoothness[sp, ep) sorted by value (ties by index here; the reference's
+// introsort leaves tie order unspecified), position 4 = the never-overwritten phantom {0, ind 0}
+// (FA:169, 819), position ep unsorted. The edge loop visits ep, then ep-1..sp; the flat loop
+// sp..ep. An entry can only be selected if it passes the static tests (threshold, ground flag,
+// not already picked before the loop), and skipping entries that fail them does not change what
+// the loop does to the others. So the block compacts the statically eligible entries, sorts only
+// those, and lane 0 replays the serial loop over them against an LDS window [sp-5, ep+5] of
+// picked/col/ground/label. Ring windows are disjoint (11 positions separate ep_r and sp_{r+1}).
+// Less-flat points are then compacted and voxel-downsampled (PCL VoxelGrid, leaf 0.2).
 // ---------------------------------------------------------------------------------------------
 constexpr int kRingMax = 2048;  // >= max W
 constexpr int kWin = kRingMax + 16;
@@ -157,17 +160,22 @@ __device__ __forceinline__ void bitonic_sort_u64(uint64_t* key, int n2) {
   }
 }
 
+__device__ __forceinline__ int pow2_ceil(int n) {
+  int n2 = 1;
+  while (n2 < n) n2 <<= 1;
+  return n2;
+}
+
 __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   __shared__ uint64_t key[kRingMax];
   __shared__ uint8_t wpick[kWin];
   __shared__ uint8_t wgnd[kWin];
   __shared__ int8_t wlab[kWin];
-  __shared__ uint32_t wcol[kWin];
-  __shared__ float wcurv[kWin];
-  __shared__ float4 cand[kRingMax];
+  __shared__ uint16_t wcol[kWin];
+  __shared__ uint16_t cpos[kRingMax];
   __shared__ int tmp[8];
   __shared__ float red[6][4];
-  __shared__ int nvox;
+  __shared__ int s_cnt;
   const int i = blockIdx.x, b = blockIdx.y;
   const int H = c.H, HW = c.HW;
   const size_t base = (size_t)b * HW;
@@ -180,17 +188,6 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
     return;
   }
   const float* curv = d.curv + base;
-  const int nsort = ep - sp;
-  int n2 = 1;
-  while (n2 < nsort) n2 <<= 1;
-  for (int t = tid; t < n2; t += nt) {
-    uint64_t k = ~0ull;
-    if (t < nsort) {
-      const int pos = sp + t;
-      k = pos == 4 ? 0ull : ((uint64_t)__float_as_uint(curv[pos]) << 32) | (uint32_t)pos;
-    }
-    key[t] = k;
-  }
   const int ws = sp - 5 > 0 ? sp - 5 : 0;
   const int we = ep + 5 < HW - 1 ? ep + 5 : HW - 1;
   const int wn = we - ws + 1;
@@ -199,49 +196,86 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
     wpick[t] = d.picked[base + pos];
     wgnd[t] = d.seg_ground[base + pos];
     wlab[t] = d.clabel[base + pos];
-    wcol[t] = d.seg_col[base + pos];
-    wcurv[t] = curv[pos];
+    wcol[t] = (uint16_t)d.seg_col[base + pos];
+  }
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
+  auto suppress = [&](int ind) {
+    wpick[ind - ws] = 1;
+    for (int l = 1; l <= 5; ++l) {
+      if (ind + l >= HW) continue;
+      const int cd = abs((int)wcol[ind + l - ws] - (int)wcol[ind + l - 1 - ws]);
+      if (cd > 10) break;
+      wpick[ind + l - ws] = 1;
+    }
+    for (int l = -1; l >= -5; --l) {
+      if (ind + l < 0) continue;
+      const int cd = abs((int)wcol[ind + l - ws] - (int)wcol[ind + l + 1 - ws]);
+      if (cd > 10) break;
+      wpick[ind + l - ws] = 1;
+    }
+  };
+  // ---- edges: statically eligible sorted-part entries, visited in descending key order ----
+  for (int p = sp + tid; p < ep; p += nt) {
+    const int ind = p == 4 ? 0 : p;
+    const float v = p == 4 ? 0.0f : curv[p];
+    const int w = ind - ws;
+    if (wpick[w] == 0 && v > c.edge_thr && wgnd[w] == 0)
+      key[atomicAdd(&s_cnt, 1)] = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)ind;
   }
   __syncthreads();
+  int nE = s_cnt;
+  int n2 = pow2_ceil(nE);
+  for (int t = nE + tid; t < n2; t += nt) key[t] = 0ull;
+  __syncthreads();
   bitonic_sort_u64(key, n2);
-
   if (tid == 0) {
-    auto suppress = [&](int ind) {
-      wpick[ind - ws] = 1;
-      for (int l = 1; l <= 5; ++l) {
-        if (ind + l >= HW) continue;
-        const int cd = abs((int)(wcol[ind + l - ws] - wcol[ind + l - 1 - ws]));
-        if (cd > 10) break;
-        wpick[ind + l - ws] = 1;
-      }
-      for (int l = -1; l >= -5; --l) {
-        if (ind + l < 0) continue;
-        const int cd = abs((int)(wcol[ind + l - ws] - wcol[ind + l + 1 - ws]));
-        if (cd > 10) break;
-        wpick[ind + l - ws] = 1;
-      }
-    };
-    int nE = 0, nF = 0;
-    for (int k = ep; k >= sp; --k) {
-      const int ind = k == ep ? ep : (int)(uint32_t)key[k - sp];
+    int cnt = 0;
+    for (int t = -1; t < nE; ++t) {
+      int ind;
+      float v;
+      if (t < 0) { ind = ep; v = curv[ep]; }  // the unsorted entry at ep is visited first
+      else { const uint64_t k = key[n2 - 1 - t]; ind = (int)(uint32_t)k; v = __uint_as_float((uint32_t)(k >> 32)); }
       const int w = ind - ws;
-      if (wpick[w] == 0 && wcurv[w] > c.edge_thr && wgnd[w] == 0) {
+      if (wpick[w] == 0 && v > c.edge_thr && wgnd[w] == 0) {
         wlab[w] = 1;
-        d.edge_tmp[base + sp + nE++] = ind;
+        d.edge_tmp[base + sp + cnt++] = ind;
         suppress(ind);
       }
     }
-    for (int k = sp; k <= ep; ++k) {
-      const int ind = k == ep ? ep : (int)(uint32_t)key[k - sp];
+    rc[i] = cnt;
+    s_cnt = 0;
+  }
+  __syncthreads();
+  // ---- flats: ascending key order, entry ep last ----
+  for (int p = sp + tid; p < ep; p += nt) {
+    const int ind = p == 4 ? 0 : p;
+    const float v = p == 4 ? 0.0f : curv[p];
+    const int w = ind - ws;
+    if (wpick[w] == 0 && v < c.surf_thr && wgnd[w] == 1)
+      key[atomicAdd(&s_cnt, 1)] = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)ind;
+  }
+  __syncthreads();
+  const int nF = s_cnt;
+  n2 = pow2_ceil(nF);
+  for (int t = nF + tid; t < n2; t += nt) key[t] = ~0ull;
+  __syncthreads();
+  bitonic_sort_u64(key, n2);
+  if (tid == 0) {
+    int cnt = 0;
+    for (int t = 0; t <= nF; ++t) {
+      int ind;
+      float v;
+      if (t == nF) { ind = ep; v = curv[ep]; }
+      else { const uint64_t k = key[t]; ind = (int)(uint32_t)k; v = __uint_as_float((uint32_t)(k >> 32)); }
       const int w = ind - ws;
-      if (wpick[w] == 0 && wcurv[w] < c.surf_thr && wgnd[w] == 1) {
+      if (wpick[w] == 0 && v < c.surf_thr && wgnd[w] == 1) {
         wlab[w] = -1;
-        d.flat_tmp[base + sp + nF++] = ind;
+        d.flat_tmp[base + sp + cnt++] = ind;
         suppress(ind);
       }
     }
-    rc[i] = nE;
-    rc[H + i] = nF;
+    rc[H + i] = cnt;
   }
   __syncthreads();
   for (int t = tid; t < wn; t += nt) {
@@ -256,14 +290,14 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   for (int k = k0; k < k1; ++k) mine += wlab[sp + k - ws] <= 0;
   int L;
   int pos = block_excl_scan(mine, tmp, &L);
-  const float4* loam = d.loam + base;
   for (int k = k0; k < k1; ++k)
-    if (wlab[sp + k - ws] <= 0) cand[pos++] = loam[sp + k];
+    if (wlab[sp + k - ws] <= 0) cpos[pos++] = (uint16_t)k;
   __syncthreads();
+  const float4* lp = d.loam + base + sp;
   // ---- VoxelGrid(0.2) applyFilter (PCL 1.10), centroids summed in (voxel, input) order ----
   float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
   for (int t = tid; t < L; t += nt) {
-    const float4 p = cand[t];
+    const float4 p = lp[cpos[t]];
     mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
     mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
   }
@@ -277,14 +311,14 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   }
   const float inv = 1.0f / 0.2f;
   float4* out = d.lflat_tmp + base + sp;
-  const long long dx = (long long)((mx[0] - mn[0]) * inv) + 1, dy = (long long)((mx[1] - mn[1]) * inv) + 1,
-                  dz = (long long)((mx[2] - mn[2]) * inv) + 1;
   if (L == 0) {
     if (tid == 0) rc[2 * H + i] = 0;
     return;
   }
+  const long long dx = (long long)((mx[0] - mn[0]) * inv) + 1, dy = (long long)((mx[1] - mn[1]) * inv) + 1,
+                  dz = (long long)((mx[2] - mn[2]) * inv) + 1;
   if (dx * dy * dz > (long long)INT_MAX) {  // PCL: leaf too small -> output = input
-    for (int t = tid; t < L; t += nt) out[t] = cand[t];
+    for (int t = tid; t < L; t += nt) out[t] = lp[cpos[t]];
     if (tid == 0) rc[2 * H + i] = L;
     return;
   }
@@ -294,12 +328,11 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
     div[a] = (int)floorf(mx[a] * inv) - minb[a] + 1;
   }
   const int mul1 = div[0], mul2 = div[0] * div[1];
-  int L2 = 1;
-  while (L2 < L) L2 <<= 1;
+  const int L2 = pow2_ceil(L);
   for (int t = tid; t < L2; t += nt) {
     uint64_t k = ~0ull;
     if (t < L) {
-      const float4 p = cand[t];
+      const float4 p = lp[cpos[t]];
       const int i0 = (int)(floorf(p.x * inv) - (float)minb[0]);
       const int i1 = (int)(floorf(p.y * inv) - (float)minb[1]);
       const int i2 = (int)(floorf(p.z * inv) - (float)minb[2]);
@@ -309,7 +342,6 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   }
   __syncthreads();
   bitonic_sort_u64(key, L2);
-  // voxel heads -> ordinal via block scan over contiguous chunks
   const int perv = (L + nt - 1) / nt;
   const int v0 = min(tid * perv, L), v1 = min(v0 + perv, L);
   int heads = 0;
@@ -322,7 +354,7 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
     float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
     int e = t;
     while (e < L && (uint32_t)(key[e] >> 32) == vid) {
-      const float4 p = cand[(uint32_t)key[e]];
+      const float4 p = lp[cpos[(uint32_t)key[e]]];
       sx += p.x; sy += p.y; sz += p.z; si += p.w;
       ++e;
     }
@@ -334,81 +366,79 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
 
 // ---------------------------------------------------------------------------------------------
 // K9 concatenate per-ring lists (ring order, FA:1165) and DBSCAN_EdgeFeature (FA:1318-1387)
-// + cluster run-length filter (FA:1281-1305). One workgroup (1024 threads) per scan.
-// The O(M^2) neighbourhood tests run in parallel across the block for each i; the serial
-// label-merge semantics (collapse through label 0, relabel of every member label) are applied
-// exactly with LDS bitmaps. Points/labels live in LDS when M <= kDbLds, else in global scratch.
+// + cluster run-length filter (FA:1281-1305). ONE WAVE per scan: the serial merge loop over i
+// needs a neighbourhood pass, a min-label reduction and a relabel pass per point; inside one wave
+// these are ordered by the wave's own LDS ordering (no workgroup barriers). The O(M^2) tests run
+// 64-wide. Points / labels live in LDS when M <= kDb, else in per-slot global scratch.
+// Semantics reproduced exactly: in_label_list always holds the labels of the eps-neighbours as
+// read before any update (with cluster[i] = 0), so the relabel also collapses every point whose
+// label is 0 — including not-yet-visited ones — into min_label (FA:1369-1375).
 // ---------------------------------------------------------------------------------------------
-constexpr int kDbLds = 4096;
+constexpr int kDb = 2048;
 
-__global__ __launch_bounds__(1024) void k_fa_finish(DevCfg c, DevBufs d) {
+__device__ __forceinline__ void wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__global__ __launch_bounds__(64) void k_fa_finish(DevCfg c, DevBufs d) {
   __shared__ int roff[3][65];
-  __shared__ float4 sP[kDbLds];
-  __shared__ float sKz[kDbLds];
-  __shared__ int sCl[kDbLds + 1];
-  __shared__ uint32_t sIn[2][kDbLds / 32];
-  __shared__ uint32_t sLb[2][kDbLds / 32 + 1];
-  __shared__ int sMin[2];
-  __shared__ int tmp[32];
+  __shared__ float4 sP[kDb];
+  __shared__ int sAux[kDb + 1];   // kz (as float bits) during the merge, label histogram after
+  __shared__ int sCl[kDb];
+  __shared__ uint32_t sIn[kDb / 32];
+  __shared__ uint32_t sLb[kDb / 32 + 1];
   const int b = blockIdx.x;
   const int H = c.H;
   const size_t base = (size_t)b * c.HW;
-  const int tid = threadIdx.x, nt = blockDim.x;
+  const int l = threadIdx.x;
   const int* rc = d.ring_cnt + (size_t)b * 3 * H;
-  if (tid < 3) {
-    int acc = 0;
-    for (int r = 0; r < H; ++r) { roff[tid][r] = acc; acc += rc[tid * H + r]; }
-    roff[tid][H] = acc;
+  // ring offsets (exclusive scan over <= 64 rings, three lists)
+  for (int q = 0; q < 3; ++q) {
+    const int v = l < H ? rc[q * H + l] : 0;
+    const int incl = wave_incl_scan_add(v);
+    if (l < H) roff[q][l] = incl - v;
+    if (l == 63) roff[q][H] = incl;
   }
-  __syncthreads();
+  wave_fence();
   const int M = roff[0][H], F = roff[1][H], Lf = roff[2][H];
   for (int r = 0; r < H; ++r) {
     const int sp = d.start_ring[b * H + r];
-    for (int t = tid; t < rc[r]; t += nt) d.less_sharp[base + roff[0][r] + t] = d.edge_tmp[base + sp + t];
-    for (int t = tid; t < rc[H + r]; t += nt) d.flat[base + roff[1][r] + t] = d.flat_tmp[base + sp + t];
-    for (int t = tid; t < rc[2 * H + r]; t += nt) d.lflat[base + roff[2][r] + t] = d.lflat_tmp[base + sp + t];
+    for (int t = l; t < rc[r]; t += 64) d.less_sharp[base + roff[0][r] + t] = d.edge_tmp[base + sp + t];
+    for (int t = l; t < rc[H + r]; t += 64) d.flat[base + roff[1][r] + t] = d.flat_tmp[base + sp + t];
+    for (int t = l; t < rc[2 * H + r]; t += 64) d.lflat[base + roff[2][r] + t] = d.lflat_tmp[base + sp + t];
   }
-  __syncthreads();
+  __threadfence_block();
 
-  // ---- DBSCAN_EdgeFeature ----
-  const bool lds = M <= kDbLds;
+  const bool lds = M <= kDb;
   float4* P = lds ? sP : d.db_pts + base;
-  float* KZ = lds ? sKz : d.db_kz + base;
+  int* AUX = lds ? sAux : (int*)(d.db_kz + base);
   int* CL = lds ? sCl : d.cluster + base;
-  uint32_t* IN0 = lds ? sIn[0] : (uint32_t*)(d.ccl_b + base);
-  const int nwIn = (M + 31) / 32;
-  uint32_t* IN1 = IN0 + (lds ? kDbLds / 32 : nwIn);
-  uint32_t* LB0 = lds ? sLb[0] : IN1 + nwIn;
-  const int nwLb = (M + 1 + 31) / 32;
-  uint32_t* LB1 = LB0 + (lds ? kDbLds / 32 + 1 : nwLb);
+  uint32_t* IN = lds ? sIn : (uint32_t*)(d.ccl_b + base);
+  const int nwIn = (M + 31) / 32, nwLb = (M + 1 + 31) / 32;
+  uint32_t* LB = lds ? sLb : IN + nwIn;
   const float4* loam = d.loam + base;
-  for (int a = tid; a < M; a += nt) {
+  for (int a = l; a < M; a += 64) {
     const float4 p = loam[d.less_sharp[base + a]];
-    const float x0 = p.z, y0 = p.x, z0 = p.y;
-    const float rxy = sqrt_(x0 * x0 + y0 * y0);
-    const float AB = atan2f_(z0, rxy);
+    const float x0 = p.z, y0 = p.x, z0 = p.y;  // LOAM -> lidar axes (FA:1327-1329)
+    const float AB = atan2f_(z0, sqrt_(x0 * x0 + y0 * y0));
     const float kxy = sqrt_(x0 * x0 + y0 * y0) * c.sinResX * c.RatioXY;
     const float kz = (sqrt_(x0 * x0 + y0 * y0) * tanf_(AB + c.fa_resY) -
                       sqrt_(x0 * x0 + y0 * y0) * tanf_(AB - c.fa_resY)) / 2 * c.RatioZ;
     P[a] = make_float4(x0, y0, z0, kxy);
-    KZ[a] = kz;
+    AUX[a] = __float_as_int(kz);
     CL[a] = 0;
   }
-  for (int w = tid; w < nwIn; w += nt) { IN0[w] = 0u; IN1[w] = 0u; }
-  for (int w = tid; w < nwLb; w += nt) { LB0[w] = 0u; LB1[w] = 0u; }
-  if (tid == 0) { sMin[0] = 999999999; sMin[1] = 999999999; }
-  __syncthreads();
+  for (int w = l; w < nwIn; w += 64) IN[w] = 0u;
+  for (int w = l; w < nwLb; w += 64) LB[w] = 0u;
+  __threadfence_block();
   int label = 0;
   for (int i = 0; i < M; ++i) {
-    uint32_t* IN = (i & 1) ? IN1 : IN0;
-    uint32_t* LB = (i & 1) ? LB1 : LB0;
-    uint32_t* INo = (i & 1) ? IN0 : IN1;
-    uint32_t* LBo = (i & 1) ? LB0 : LB1;
     const float4 pi = P[i];
     int lmin = 999999999;
-    for (int j = tid; j < M; j += nt) {
+    for (int j = l; j < M; j += 64) {
       const float4 pj = P[j];
-      const float kzj = KZ[j];
+      const float kzj = __int_as_float(AUX[j]);
       const float eps = sqrt_((pi.x - pj.x) * (pi.x - pj.x) / (pj.w * pj.w) +
                               (pi.y - pj.y) * (pi.y - pj.y) / (pj.w * pj.w) +
                               (pi.z - pj.z) * (pi.z - pj.z) / (kzj * kzj));
@@ -420,80 +450,63 @@ __global__ __launch_bounds__(1024) void k_fa_finish(DevCfg c, DevBufs d) {
       }
     }
     lmin = wave_reduce_min(lmin);
-    if (lane_id() == 0 && lmin < 999999999) atomicMin(&sMin[i & 1], lmin);
-    // clear the other buffers (used by iteration i-1, consumed before the last barrier)
-    for (int w = tid; w < nwIn; w += nt) INo[w] = 0u;
-    for (int w = tid; w < nwLb; w += nt) LBo[w] = 0u;
-    if (tid == 0) sMin[(i + 1) & 1] = 999999999;
-    __syncthreads();
-    const int minLabel = sMin[i & 1];
-    if (minLabel <= label) {
-      for (int j = tid; j < M; j += nt) {
+    if (lds) wave_fence(); else __threadfence_block();
+    if (lmin <= label) {
+      for (int j = l; j < M; j += 64) {
         const int cur = j == i ? 0 : CL[j];
-        const bool inj = (IN[j >> 5] >> (j & 31)) & 1u;
-        if (inj || ((LB[cur >> 5] >> (cur & 31)) & 1u)) CL[j] = minLabel;
+        if (((IN[j >> 5] >> (j & 31)) & 1u) || ((LB[cur >> 5] >> (cur & 31)) & 1u)) CL[j] = lmin;
         else if (j == i) CL[j] = 0;
       }
     } else {
       label += 1;
-      for (int j = tid; j < M; j += nt) {
-        const bool inj = (IN[j >> 5] >> (j & 31)) & 1u;
-        if (inj) CL[j] = label;
+      for (int j = l; j < M; j += 64) {
+        if ((IN[j >> 5] >> (j & 31)) & 1u) CL[j] = label;
         else if (j == i) CL[j] = 0;
       }
     }
-    __syncthreads();
+    if (lds) wave_fence(); else __threadfence_block();
+    for (int w = l; w < nwIn; w += 64) IN[w] = 0u;
+    for (int w = l; w <= (label >> 5) && w < nwLb; w += 64) LB[w] = 0u;
+    if (lds) wave_fence(); else __threadfence_block();
   }
-  // ---- run lengths of sorted labels, last run dropped; label r+1 kept if run r >= 4 ----
-  // labels are in [0, label]; histogram into KZ's storage (no longer needed)
-  int* hist = lds ? (int*)sKz : (int*)(d.db_kz + base);
+  // ---- run lengths of the sorted labels, last run dropped; keep label r+1 if run r >= 4 ----
+  int* hist = AUX;
   const int NL = label + 1;
-  for (int l = tid; l < NL; l += nt) hist[l] = 0;
-  __syncthreads();
-  for (int a = tid; a < M; a += nt) atomicAdd(&hist[CL[a]], 1);
-  __syncthreads();
+  for (int q = l; q < NL; q += 64) hist[q] = 0;
+  __threadfence_block();
+  for (int a = l; a < M; a += 64) atomicAdd(&hist[CL[a]], 1);
+  __threadfence_block();
   int lmax = -1;
-  for (int l = tid; l < NL; l += nt)
-    if (hist[l] > 0) lmax = l;
+  for (int q = l; q < NL; q += 64)
+    if (hist[q] > 0) lmax = q;
   lmax = wave_reduce_max(lmax);
-  if (lane_id() == 0) tmp[tid >> 6] = lmax;
-  __syncthreads();
-  lmax = -1;
-  for (int w = 0; w < (nt >> 6); ++w) lmax = tmp[w] > lmax ? tmp[w] : lmax;
-  __syncthreads();
-  // rank of each present label among present labels (ascending)
-  const int perl = (NL + nt - 1) / nt;
-  const int l0 = min(tid * perl, NL), l1 = min(l0 + perl, NL);
-  int pres = 0;
-  for (int l = l0; l < l1; ++l) pres += hist[l] > 0;
-  int tot;
-  int r = block_excl_scan(pres, tmp, &tot);
-  // inlier marks go into LB0 (label-indexed bitmap); clear it first
-  for (int w = tid; w < nwLb; w += nt) LB0[w] = 0u;
-  __syncthreads();
-  for (int l = l0; l < l1; ++l) {
-    if (hist[l] <= 0) continue;
-    if (l != lmax && hist[l] >= 4) {
-      const int lab = r + 1;
-      if (lab < NL) atomicOr(&LB0[lab >> 5], 1u << (lab & 31));
-    }
-    ++r;
+  for (int w = l; w < nwLb; w += 64) LB[w] = 0u;
+  __threadfence_block();
+  const unsigned long long lt = (1ull << l) - 1ull;
+  int run = 0;
+  for (int q0 = 0; q0 < NL; q0 += 64) {
+    const int q = q0 + l;
+    const bool pres = q < NL && hist[q] > 0;
+    const unsigned long long m = __ballot(pres);
+    const int r = run + __popcll(m & lt);
+    if (pres && q != lmax && hist[q] >= 4 && r + 1 < NL) atomicOr(&LB[(r + 1) >> 5], 1u << ((r + 1) & 31));
+    run += __popcll(m);
   }
-  __syncthreads();
-  const int perm = (M + nt - 1) / nt;
-  const int a0 = min(tid * perm, M), a1 = min(a0 + perm, M);
+  __threadfence_block();
   int ns = 0;
-  for (int a = a0; a < a1; ++a) ns += (LB0[CL[a] >> 5] >> (CL[a] & 31)) & 1u;
-  int NS;
-  int ps = block_excl_scan(ns, tmp, &NS);
-  for (int a = a0; a < a1; ++a)
-    if ((LB0[CL[a] >> 5] >> (CL[a] & 31)) & 1u) d.sharp[base + ps++] = d.less_sharp[base + a];
+  for (int a0 = 0; a0 < M; a0 += 64) {
+    const int a = a0 + l;
+    const bool keep = a < M && ((LB[CL[a] >> 5] >> (CL[a] & 31)) & 1u);
+    const unsigned long long m = __ballot(keep);
+    if (keep) d.sharp[base + ns + __popcll(m & lt)] = d.less_sharp[base + a];
+    ns += __popcll(m);
+  }
   if (lds)
-    for (int a = tid; a < M; a += nt) d.cluster[base + a] = CL[a];
-  if (tid == 0) {
+    for (int a = l; a < M; a += 64) d.cluster[base + a] = CL[a];
+  if (l == 0) {
     int* cnt = d.counts + b * kCnt;
     cnt[C_M] = M;
-    cnt[C_SHARP] = NS;
+    cnt[C_SHARP] = ns;
     cnt[C_F] = F;
     cnt[C_L] = Lf;
   }

@@ -342,26 +342,25 @@ __global__ __launch_bounds__(1024) void k_ground_elev_ransac(DevCfg c, DevBufs d
   __syncthreads();
 
   // ---- NEAR (IP:701-715): row-major compaction, intensity = linear index ----
-  const int per = (HW + nt - 1) / nt;
-  const int c0 = min(tid * per, HW), c1 = min(c0 + per, HW);
-  int myc = 0;
-  for (int cell = c0; cell < c1; ++cell) {
-    if (g[cell] != 1) continue;
-    const float4 p = full[cell];
-    const float depth = sqrt_(p.x * p.x + p.y * p.y);
-    if ((double)depth <= 10) ++myc;
-  }
-  int K;
-  int pos = block_excl_scan(myc, tmp, &K);
   float4* nearp = d.near_pts + base;
-  for (int cell = c0; cell < c1; ++cell) {
-    if (g[cell] != 1) continue;
-    const float4 p = full[cell];
-    const float depth = sqrt_(p.x * p.x + p.y * p.y);
-    if ((double)depth <= 10) {
-      nearp[pos++] = make_float4(p.x, p.y, p.z, (float)cell);
+  int K = 0;
+  for (int t0 = 0; t0 < HW; t0 += nt) {
+    const int cell = t0 + tid;
+    bool nearc = false;
+    float depth = 0.f;
+    if (cell < HW && g[cell] == 1) {
+      const float4 p = full[cell];
+      depth = sqrt_(p.x * p.x + p.y * p.y);
+      nearc = (double)depth <= 10;
+    }
+    int tot;
+    const int ex = block_excl_scan(nearc ? 1 : 0, tmp, &tot);
+    if (nearc) {
+      const float4 p = full[cell];
+      nearp[K + ex] = make_float4(p.x, p.y, p.z, (float)cell);
       if ((double)depth <= 5) g[cell] = 0;
     }
+    K += tot;
   }
   int* shuf = d.shuf + base;
   for (int k = tid; k < K; k += nt) shuf[k] = k;
@@ -585,28 +584,22 @@ __global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
     }
   }
   __syncthreads();
-  // feasibility and rank of feasible seeds in row-major order
-  const int per = (HW + nt - 1) / nt;
-  const int c0 = min(tid * per, HW), c1 = min(c0 + per, HW);
-  int mine = 0;
-  for (int cell = c0; cell < c1; ++cell) {
-    if (lab[cell] != cell) continue;
-    int size, lines;
-    if (kLds) { size = (unsigned)stat[cell] >> 16; lines = __popc(stat[cell] & 0xffff); }
-    else { size = stat[cell]; lines = __popcll(rowm[cell]); }
-    const bool feas = size >= 30 || (size >= c.pointNum && lines >= c.lineNum);
-    if (feas) ++mine;
-  }
-  int tot;
-  int rank = block_excl_scan(mine, tmp, &tot);
-  // second pass: overwrite the stat word of each root with its final label
-  for (int cell = c0; cell < c1; ++cell) {
-    if (lab[cell] != cell) continue;
-    int size, lines;
-    if (kLds) { size = (unsigned)stat[cell] >> 16; lines = __popc(stat[cell] & 0xffff); }
-    else { size = stat[cell]; lines = __popcll(rowm[cell]); }
-    const bool feas = size >= 30 || (size >= c.pointNum && lines >= c.lineNum);
-    stat[cell] = feas ? ++rank : 999999;
+  // feasibility and rank of feasible seeds in row-major order (coalesced tiles)
+  int rank = 0;
+  for (int t0 = 0; t0 < HW; t0 += nt) {
+    const int cell = t0 + tid;
+    bool root = false, feas = false;
+    if (cell < HW && lab[cell] == cell) {
+      root = true;
+      int size, lines;
+      if (kLds) { size = (unsigned)stat[cell] >> 16; lines = __popc(stat[cell] & 0xffff); }
+      else { size = stat[cell]; lines = __popcll(rowm[cell]); }
+      feas = size >= 30 || (size >= c.pointNum && lines >= c.lineNum);
+    }
+    int tot;
+    const int ex = block_excl_scan(feas ? 1 : 0, tmp, &tot);  // barriers: all stat reads done
+    if (root) stat[cell] = feas ? rank + ex + 1 : 999999;
+    rank += tot;
   }
   __syncthreads();
   for (int cell = tid; cell < HW; cell += nt) {
@@ -647,8 +640,6 @@ __global__ __launch_bounds__(1024) void k_segment(DevCfg c, const float4* __rest
     d.orient[b * 4 + 1] = o1;
     d.orient[b * 4 + 2] = o2;
   }
-  const int per = (HW + nt - 1) / nt;
-  const int c0 = min(tid * per, HW), c1 = min(c0 + per, HW);
   // 0 = skip, 1 = segmented, 2 = outlier
   auto kind = [&](int cell) -> int {
     const int i = cell / W, j = cell - i * W;
@@ -659,35 +650,35 @@ __global__ __launch_bounds__(1024) void k_segment(DevCfg c, const float4* __rest
     if (gv == 1 && (j % 5 != 0 && j > 5 && j < W - 5)) return 0;
     return 1;
   };
-  int ns = 0, no = 0;
-  for (int cell = c0; cell < c1; ++cell) {
-    const int k = kind(cell);
-    ns += k == 1;
-    no += k == 2;
-  }
-  int S, O;
-  int ps = block_excl_scan(ns, tmp, &S);
-  int po = block_excl_scan(no, tmp, &O);
-  for (int cell = c0; cell < c1; ++cell) {
-    const int i = cell / W, j = cell - i * W;
-    if (j == 0) {
-      d.start_ring[b * H + i] = ps - 1 + 5;
-      if (i > 0) d.end_ring[b * H + i - 1] = ps - 1 - 5;
+  // row-major compaction in coalesced tiles of blockDim cells; one packed scan per tile
+  int baseS = 0, baseO = 0;
+  for (int t0 = 0; t0 < HW; t0 += nt) {
+    const int cell = t0 + tid;
+    const int k = cell < HW ? kind(cell) : 0;
+    int tot;
+    const int ex = block_excl_scan((k == 1 ? 1 : 0) | (k == 2 ? 1 << 16 : 0), tmp, &tot);
+    const int ps = baseS + (ex & 0xffff), po = baseO + (ex >> 16);
+    if (cell < HW) {
+      const int i = cell / W, j = cell - i * W;
+      if (j == 0) {
+        d.start_ring[b * H + i] = ps - 1 + 5;
+        if (i > 0) d.end_ring[b * H + i - 1] = ps - 1 - 5;
+      }
+      if (k == 1) {
+        d.seg[base + ps] = d.full[base + cell];
+        d.seg_ground[base + ps] = g[cell] == 1;
+        d.seg_col[base + ps] = (uint32_t)j;
+        d.seg_range[base + ps] = d.range[base + cell];
+        d.seg_int[base + ps] = d.vis[base + cell];
+      } else if (k == 2) {
+        d.outl[base + po] = d.full[base + cell];
+        d.outl_int[base + po] = d.vis[base + cell];
+      }
     }
-    const int k = kind(cell);
-    if (k == 1) {
-      d.seg[base + ps] = d.full[base + cell];
-      d.seg_ground[base + ps] = g[cell] == 1;
-      d.seg_col[base + ps] = (uint32_t)j;
-      d.seg_range[base + ps] = d.range[base + cell];
-      d.seg_int[base + ps] = d.vis[base + cell];
-      ++ps;
-    } else if (k == 2) {
-      d.outl[base + po] = d.full[base + cell];
-      d.outl_int[base + po] = d.vis[base + cell];
-      ++po;
-    }
+    baseS += tot & 0xffff;
+    baseO += tot >> 16;
   }
+  const int S = baseS, O = baseO;
   if (tid == 0) {
     d.end_ring[b * H + H - 1] = S - 1 - 5;
     cnt[C_S] = S;
