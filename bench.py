@@ -44,7 +44,9 @@ def kernel_bytes(name: str, c: dict, HW: int) -> float:
         "k_segment": 5 * HW + 53 * S + 9 * (HW - S),
         "k_fa_points": 62 * S,
         "k_select_ring": 13 * S + 16 * Lc + 16 * L + 8 * (M + F),
-        "k_fa_finish": 8 * (M + F) + 32 * L + 16 * M + 8 * M,
+        "k_fa_concat": 8 * (M + F) + 32 * L + 40 * M,
+        "k_dbscan_adj": 20 * M + c.get("M2", 0) / 8,
+        "k_dbscan_merge": c.get("M2", 0) / 8 + 12 * M,
     }.get(name, 0.0)
 
 
@@ -138,6 +140,7 @@ def main():
     assert int(finite.sum()) == int(csum["N"])
     r0 = pipe.fetch(0)
     csum["R"] = float(r0["ransac_iterations"])
+    csum["M2"] = float((cnt[:, 3].astype(np.float64) ** 2).sum())  # DBSCAN pair count
     HWB = float(H * W * B)
     per = {k: kernel_bytes(k, csum, HWB) for k in ktimes}
     dom = max((k for k in ktimes if k != "init"), key=lambda k: ktimes[k])
@@ -185,7 +188,7 @@ def main():
                          "algorithmic_bytes_per_launch": per[dom], "avg_launch_ms": round(ktimes[dom], 4)},
             "kernels_ms_per_step": {k: round(v, 4) for k, v in ktimes.items()},
             "pipeline_algorithmic_GBs": round(sum(per.values()) / (sum(ktimes.values()) * 1e-3) / 1e9, 1),
-            "per_scan_mean": {k: round(v / B, 1) for k, v in csum.items() if k != "R"},
+            "per_scan_mean": {k: round(v / B, 1) for k, v in csum.items() if k not in ("R", "M2")},
             "parity_spot_check_slot0": parity,
             "pose_delta": None,
         }

@@ -22,7 +22,9 @@ template <bool kLds> __global__ void k_label(DevCfg, DevBufs);
 __global__ void k_segment(DevCfg, const float4*, const int64_t*, DevBufs);
 __global__ void k_fa_points(DevCfg, DevBufs);
 __global__ void k_select_ring(DevCfg, DevBufs);
-__global__ void k_fa_finish(DevCfg, DevBufs);
+__global__ void k_fa_concat(DevCfg, DevBufs);
+__global__ void k_dbscan_adj(DevCfg, DevBufs);
+__global__ void k_dbscan_merge(DevCfg, DevBufs);
 
 __global__ void k_init_counts(int* counts, int B) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -39,8 +41,8 @@ using namespace llsr;
 namespace {
 const char* kKernelNames[] = {"init",          "k_project",    "k_gather_column", "k_ground_add",
                               "k_ground_elev_ransac", "k_label", "k_segment",      "k_fa_points",
-                              "k_select_ring", "k_fa_finish"};
-constexpr int kNumKernels = 10;
+                              "k_select_ring", "k_fa_concat", "k_dbscan_adj", "k_dbscan_merge"};
+constexpr int kNumKernels = 12;
 }  // namespace
 
 struct llsr_handle {
@@ -133,6 +135,7 @@ static void make_devcfg(const llsr_config& c, DevCfg& d) {
   d.RatioZ = c.RatioZ;
   d.DBFr = c.DBFr;
   d.ccl_lds = (d.H <= 16 && d.HW <= 32768) ? 1 : 0;
+  d.dbg_phase = 1 << 30;
 }
 
 template <class T>
@@ -181,6 +184,7 @@ static size_t layout(DevBufs& d, char* p0, int B, int H, int HW) {
   d.lflat = carve<float4>(p, n);
   d.db_pts = carve<float4>(p, n);
   d.db_kz = carve<float>(p, n);
+  d.db_adj = carve<uint32_t>(p, (size_t)B * kAdjCap * kAdjWords);
   return (size_t)(p - p0);
 }
 
@@ -323,7 +327,11 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   mark();
   k_select_ring<<<dim3(c.H, B), 256, 0, s>>>(c, h->d);
   mark();
-  k_fa_finish<<<B, 64, 0, s>>>(c, h->d);
+  k_fa_concat<<<B, 256, 0, s>>>(c, h->d);
+  mark();
+  k_dbscan_adj<<<dim3(32, B), 256, 0, s>>>(c, h->d);
+  mark();
+  k_dbscan_merge<<<B, 64, 0, s>>>(c, h->d);
   mark();
   HIP_OK(h, hipGetLastError());
   if (h->profiling) {
@@ -349,6 +357,43 @@ extern "C" int32_t llsr_kernel_times_ms(llsr_handle* h, float* out, int32_t cap)
   int n = 0;
   for (int k = 0; k < kNumKernels && n < cap; ++k, ++n) out[n] = (float)(h->ksum[k] / (double)h->kbatches);
   return n;
+}
+
+// Diagnostics (not part of the ABI header): re-launch kernel k on the last batch's buffers with
+// an early exit at `phase`, `reps` times; returns the mean device ms per launch (< 0 on error).
+// Used to attribute a kernel's time to its phases; results of such launches are meaningless.
+extern "C" float llsr_debug_phase_ms(llsr_handle* h, int32_t k, int32_t phase, int32_t reps) {
+  if (!h || h->last_B < 1 || reps < 1) return -1.f;
+  if (hipSetDevice(h->device) != hipSuccess) return -1.f;
+  hipStream_t s = h->stream;
+  DevCfg c = h->dc;
+  c.dbg_phase = phase;
+  const int B = h->last_B;
+  hipEvent_t e0 = h->ev[0][0], e1 = h->ev[0][1];
+  if (hipStreamSynchronize(h->last_stream ? h->last_stream : s) != hipSuccess) return -1.f;
+  (void)hipEventRecord(e0, s);
+  for (int r = 0; r < reps; ++r) {
+    switch (k) {
+      case 8: k_select_ring<<<dim3(c.H, B), 256, 0, s>>>(c, h->d); break;
+      case 9: k_fa_concat<<<B, 256, 0, s>>>(c, h->d); break;
+      case 10: k_dbscan_adj<<<dim3(32, B), 256, 0, s>>>(c, h->d); break;
+      case 11: k_dbscan_merge<<<B, 64, 0, s>>>(c, h->d); break;
+      case 7: k_fa_points<<<B, 1024, 0, s>>>(c, h->d); break;
+      case 6: k_segment<<<B, 1024, 0, s>>>(c, nullptr, nullptr, h->d); break;
+      case 5:
+        if (c.ccl_lds) k_label<true><<<B, 1024, c.HW * sizeof(int), s>>>(c, h->d);
+        else k_label<false><<<B, 1024, 0, s>>>(c, h->d);
+        break;
+      case 4: k_ground_elev_ransac<<<B, 1024, 0, s>>>(c, h->d); break;
+      case 3: k_ground_add<<<dim3((c.H + 3) / 4, B), 256, 0, s>>>(c, h->d); break;
+      default: return -2.f;
+    }
+  }
+  (void)hipEventRecord(e1, s);
+  if (hipEventSynchronize(e1) != hipSuccess) return -1.f;
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  return ms / reps;
 }
 
 extern "C" const char* llsr_kernel_name(int32_t k) {

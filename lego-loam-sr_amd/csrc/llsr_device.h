@@ -34,6 +34,7 @@ struct DevCfg {
   float scan_period, edge_thr, surf_thr;
   float fa_resY, sinResX, RatioXY, RatioZ, DBFr;
   int ccl_lds;  // union-find parent array fits LDS (H <= 16 && HW <= 32768)
+  int dbg_phase;  // diagnostics only: kernels return at phase boundary >= dbg_phase (default: never)
 };
 
 // Device buffers owned by the handle; every per-slot array has stride HW (or H for rings).
@@ -72,9 +73,14 @@ struct DevBufs {
   int* sharp;           // [B][HW]
   int* flat;            // [B][HW]
   float4* lflat;        // [B][HW]
-  float4* db_pts;       // [B][HW] DBSCAN scratch: (x0, y0, z0, kxy)
+  float4* db_pts;       // [B][HW] DBSCAN point records: (x0, y0, z0, kxy)
   float* db_kz;         // [B][HW]
+  uint32_t* db_adj;     // [B][kAdjCap][kAdjWords] eps-neighbourhood bitmask rows
 };
+
+// DBSCAN adjacency capacity per scan (edge candidates); larger M falls back to on-the-fly rows.
+constexpr int kAdjCap = 2048;
+constexpr int kAdjWords = kAdjCap / 32;
 
 // ---- wave / block primitives (wave64) ------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }

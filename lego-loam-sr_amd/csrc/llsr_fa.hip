@@ -144,16 +144,18 @@ __global__ __launch_bounds__(1024) void k_fa_points(DevCfg c, DevBufs d) {
 constexpr int kRingMax = 2048;  // >= max W
 constexpr int kWin = kRingMax + 16;
 
+// Block bitonic sort of n2 (power of two) 64-bit keys in LDS, ascending; one compare-exchange
+// pair per thread-iteration (no idle half), one barrier per stage.
 __device__ __forceinline__ void bitonic_sort_u64(uint64_t* key, int n2) {
+  const int half = n2 >> 1;
   for (int k = 2; k <= n2; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int t = threadIdx.x; t < n2; t += blockDim.x) {
-        const int ixj = t ^ j;
-        if (ixj > t) {
-          const uint64_t a = key[t], e = key[ixj];
-          const bool up = (t & k) == 0;
-          if ((a > e) == up) { key[t] = e; key[ixj] = a; }
-        }
+      for (int p = threadIdx.x; p < half; p += blockDim.x) {
+        const int t = ((p & ~(j - 1)) << 1) | (p & (j - 1));  // p with a 0 inserted at bit log2(j)
+        const int u = t | j;
+        const uint64_t a = key[t], e = key[u];
+        const bool up = (t & k) == 0;
+        if ((a > e) == up) { key[t] = e; key[u] = a; }
       }
       __syncthreads();
     }
@@ -166,16 +168,57 @@ __device__ __forceinline__ int pow2_ceil(int n) {
   return n2;
 }
 
+// Serial greedy pick (FA:1175-1259) over a candidate list already in visiting order, by one wave:
+// each chunk of 64 candidates reads `picked` once; the first still-alive candidate is selected,
+// candidates inside its suppression interval die, repeat. Steps per chunk = picks in the chunk.
+// Returns the number selected; writes labels, picked and the output list in selection order.
+__device__ __forceinline__ int greedy_wave(const int* order, int nc, int ws, uint8_t* wpick, const uint8_t* wreach,
+                                           int8_t* wlab, int8_t lab, int* outp) {
+  const int l = lane_id();
+  const unsigned long long lt = (1ull << l) - 1ull;
+  int nsel = 0;
+  for (int t0 = 0; t0 < nc; t0 += 64) {
+    const int t = t0 + l;
+    const bool valid = t < nc;
+    const int w = valid ? order[t] - ws : 0;
+    bool alive = valid && wpick[w] == 0;
+    const int r = valid ? wreach[w] : 0;
+    const int lo = w - (r >> 4), hi = w + (r & 15);
+    unsigned long long sel = 0ull;
+    unsigned long long m = __ballot(alive);
+    while (m) {
+      const int s = __ffsll((long long)m) - 1;
+      const int slo = __shfl(lo, s, 64), shi = __shfl(hi, s, 64);
+      sel |= 1ull << s;
+      if (l > s && w >= slo && w <= shi) alive = false;
+      if (l == s) alive = false;
+      m = __ballot(alive);
+    }
+    if ((sel >> l) & 1ull) {
+      wlab[w] = lab;
+      outp[nsel + __popcll(sel & lt)] = order[t];
+      for (int q = lo; q <= hi; ++q) wpick[q] = 1;
+    }
+    nsel += __popcll(sel);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  return nsel;
+}
+
 __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   __shared__ uint64_t key[kRingMax];
   __shared__ uint8_t wpick[kWin];
   __shared__ uint8_t wgnd[kWin];
   __shared__ int8_t wlab[kWin];
   __shared__ uint16_t wcol[kWin];
+  __shared__ uint8_t wreach[kWin];  // suppression reach: fwd | bwd << 4 (FA:1186-1205)
   __shared__ uint16_t cpos[kRingMax];
+  __shared__ uint16_t rstart[kRingMax + 1];
+  __shared__ int order[kRingMax + 1];
   __shared__ int tmp[8];
   __shared__ float red[6][4];
-  __shared__ int s_cnt;
+  __shared__ int s_cnt, s_sel;
   const int i = blockIdx.x, b = blockIdx.y;
   const int H = c.H, HW = c.HW;
   const size_t base = (size_t)b * HW;
@@ -200,20 +243,28 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   }
   if (tid == 0) s_cnt = 0;
   __syncthreads();
+  // Marking from `ind` runs forward while consecutive column gaps stay <= 10 (at most 5 steps,
+  // stopping at H*W) and likewise backward (stopping at 0). Column indices are static, so the
+  // reach of every selectable position is computed in parallel up front.
+  for (int t = tid; t < wn; t += nt) {
+    const int ind = ws + t;
+    int f = 0, bk = 0;
+    for (int l = 1; l <= 5 && ind + l < HW && ind + l - ws < wn; ++l) {
+      if (abs((int)wcol[ind + l - ws] - (int)wcol[ind + l - 1 - ws]) > 10) break;
+      f = l;
+    }
+    for (int l = 1; l <= 5 && ind - l >= 0 && ind - l >= ws; ++l) {
+      if (abs((int)wcol[ind - l - ws] - (int)wcol[ind - l + 1 - ws]) > 10) break;
+      bk = l;
+    }
+    wreach[t] = (uint8_t)(f | (bk << 4));
+  }
+  __syncthreads();
   auto suppress = [&](int ind) {
-    wpick[ind - ws] = 1;
-    for (int l = 1; l <= 5; ++l) {
-      if (ind + l >= HW) continue;
-      const int cd = abs((int)wcol[ind + l - ws] - (int)wcol[ind + l - 1 - ws]);
-      if (cd > 10) break;
-      wpick[ind + l - ws] = 1;
-    }
-    for (int l = -1; l >= -5; --l) {
-      if (ind + l < 0) continue;
-      const int cd = abs((int)wcol[ind + l - ws] - (int)wcol[ind + l + 1 - ws]);
-      if (cd > 10) break;
-      wpick[ind + l - ws] = 1;
-    }
+    const int w = ind - ws;
+    const int r = wreach[w];
+    const int lo = w - (r >> 4), hi = w + (r & 15);
+    for (int q = lo; q <= hi; ++q) wpick[q] = 1;
   };
   // ---- edges: statically eligible sorted-part entries, visited in descending key order ----
   for (int p = sp + tid; p < ep; p += nt) {
@@ -224,29 +275,24 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
       key[atomicAdd(&s_cnt, 1)] = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)ind;
   }
   __syncthreads();
+  if (c.dbg_phase <= 0) return;
   int nE = s_cnt;
   int n2 = pow2_ceil(nE);
   for (int t = nE + tid; t < n2; t += nt) key[t] = 0ull;
   __syncthreads();
   bitonic_sort_u64(key, n2);
-  if (tid == 0) {
-    int cnt = 0;
-    for (int t = -1; t < nE; ++t) {
-      int ind;
-      float v;
-      if (t < 0) { ind = ep; v = curv[ep]; }  // the unsorted entry at ep is visited first
-      else { const uint64_t k = key[n2 - 1 - t]; ind = (int)(uint32_t)k; v = __uint_as_float((uint32_t)(k >> 32)); }
-      const int w = ind - ws;
-      if (wpick[w] == 0 && v > c.edge_thr && wgnd[w] == 0) {
-        wlab[w] = 1;
-        d.edge_tmp[base + sp + cnt++] = ind;
-        suppress(ind);
-      }
-    }
-    rc[i] = cnt;
-    s_cnt = 0;
+  if (c.dbg_phase <= 1) return;
+  // visiting order: the unsorted entry at ep first, then descending keys (FA:1175)
+  const bool epE = curv[ep] > c.edge_thr && wgnd[ep - ws] == 0;
+  for (int t = tid; t < nE; t += nt) order[t + (epE ? 1 : 0)] = (int)(uint32_t)key[n2 - 1 - t];
+  if (tid == 0 && epE) order[0] = ep;
+  __syncthreads();
+  if (tid < 64) {
+    const int cnt = greedy_wave(order, nE + (epE ? 1 : 0), ws, wpick, wreach, wlab, (int8_t)1, d.edge_tmp + base + sp);
+    if (tid == 0) { rc[i] = cnt; s_cnt = 0; }
   }
   __syncthreads();
+  if (c.dbg_phase <= 2) return;
   // ---- flats: ascending key order, entry ep last ----
   for (int p = sp + tid; p < ep; p += nt) {
     const int ind = p == 4 ? 0 : p;
@@ -261,23 +307,17 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   for (int t = nF + tid; t < n2; t += nt) key[t] = ~0ull;
   __syncthreads();
   bitonic_sort_u64(key, n2);
-  if (tid == 0) {
-    int cnt = 0;
-    for (int t = 0; t <= nF; ++t) {
-      int ind;
-      float v;
-      if (t == nF) { ind = ep; v = curv[ep]; }
-      else { const uint64_t k = key[t]; ind = (int)(uint32_t)k; v = __uint_as_float((uint32_t)(k >> 32)); }
-      const int w = ind - ws;
-      if (wpick[w] == 0 && v < c.surf_thr && wgnd[w] == 1) {
-        wlab[w] = -1;
-        d.flat_tmp[base + sp + cnt++] = ind;
-        suppress(ind);
-      }
-    }
-    rc[H + i] = cnt;
+  // visiting order: ascending keys, then the unsorted entry at ep (FA:1211)
+  const bool epF = curv[ep] < c.surf_thr && wgnd[ep - ws] == 1;
+  for (int t = tid; t < nF; t += nt) order[t] = (int)(uint32_t)key[t];
+  if (tid == 0 && epF) order[nF] = ep;
+  __syncthreads();
+  if (tid < 64) {
+    const int cnt = greedy_wave(order, nF + (epF ? 1 : 0), ws, wpick, wreach, wlab, (int8_t)-1, d.flat_tmp + base + sp);
+    if (tid == 0) rc[H + i] = cnt;
   }
   __syncthreads();
+  if (c.dbg_phase <= 3) return;
   for (int t = tid; t < wn; t += nt) {
     d.picked[base + ws + t] = wpick[t];
     d.clabel[base + ws + t] = wlab[t];
@@ -293,6 +333,7 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   for (int k = k0; k < k1; ++k)
     if (wlab[sp + k - ws] <= 0) cpos[pos++] = (uint16_t)k;
   __syncthreads();
+  if (c.dbg_phase <= 4) return;
   const float4* lp = d.loam + base + sp;
   // ---- VoxelGrid(0.2) applyFilter (PCL 1.10), centroids summed in (voxel, input) order ----
   float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
@@ -328,51 +369,153 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
     div[a] = (int)floorf(mx[a] * inv) - minb[a] + 1;
   }
   const int mul1 = div[0], mul2 = div[0] * div[1];
-  const int L2 = pow2_ceil(L);
-  for (int t = tid; t < L2; t += nt) {
-    uint64_t k = ~0ull;
-    if (t < L) {
-      const float4 p = lp[cpos[t]];
-      const int i0 = (int)(floorf(p.x * inv) - (float)minb[0]);
-      const int i1 = (int)(floorf(p.y * inv) - (float)minb[1]);
-      const int i2 = (int)(floorf(p.z * inv) - (float)minb[2]);
-      k = ((uint64_t)(uint32_t)(i0 + i1 * mul1 + i2 * mul2) << 32) | (uint32_t)t;
-    }
-    key[t] = k;
+  // voxel id of every candidate, in ring order (points of one voxel are mostly consecutive)
+  uint32_t* vk = (uint32_t*)order;
+  for (int t = tid; t < L; t += nt) {
+    const float4 p = lp[cpos[t]];
+    const int i0 = (int)(floorf(p.x * inv) - (float)minb[0]);
+    const int i1 = (int)(floorf(p.y * inv) - (float)minb[1]);
+    const int i2 = (int)(floorf(p.z * inv) - (float)minb[2]);
+    vk[t] = (uint32_t)(i0 + i1 * mul1 + i2 * mul2);
   }
   __syncthreads();
-  bitonic_sort_u64(key, L2);
-  const int perv = (L + nt - 1) / nt;
-  const int v0 = min(tid * perv, L), v1 = min(v0 + perv, L);
+  // runs of equal voxel id in ring order -> one sort key per run: (voxel id, run index)
+  const int perr = (L + nt - 1) / nt;
+  const int r0 = min(tid * perr, L), r1 = min(r0 + perr, L);
   int heads = 0;
-  for (int t = v0; t < v1; ++t) heads += (t == 0 || (key[t] >> 32) != (key[t - 1] >> 32));
+  for (int t = r0; t < r1; ++t) heads += (t == 0 || vk[t] != vk[t - 1]);
+  int R;
+  int ro = block_excl_scan(heads, tmp, &R);
+  for (int t = r0; t < r1; ++t) {
+    if (!(t == 0 || vk[t] != vk[t - 1])) continue;
+    rstart[ro] = (uint16_t)t;
+    key[ro] = ((uint64_t)vk[t] << 32) | (uint32_t)ro;
+    ++ro;
+  }
+  if (tid == 0) rstart[R] = (uint16_t)L;
+  const int R2 = pow2_ceil(R);
+  for (int t = R + tid; t < R2; t += nt) key[t] = ~0ull;
+  __syncthreads();
+  if (c.dbg_phase <= 5) return;
+  bitonic_sort_u64(key, R2);
+  if (c.dbg_phase <= 6) return;
+  // voxels = groups of sorted runs with equal id; sum members in (run start, position) order
+  const int perv = (R + nt - 1) / nt;
+  const int v0 = min(tid * perv, R), v1 = min(v0 + perv, R);
+  int vh = 0;
+  for (int t = v0; t < v1; ++t) vh += (t == 0 || (key[t] >> 32) != (key[t - 1] >> 32));
   int V;
-  int vo = block_excl_scan(heads, tmp, &V);
+  int vo = block_excl_scan(vh, tmp, &V);
   for (int t = v0; t < v1; ++t) {
     if (!(t == 0 || (key[t] >> 32) != (key[t - 1] >> 32))) continue;
     const uint32_t vid = (uint32_t)(key[t] >> 32);
     float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
-    int e = t;
-    while (e < L && (uint32_t)(key[e] >> 32) == vid) {
-      const float4 p = lp[cpos[(uint32_t)key[e]]];
-      sx += p.x; sy += p.y; sz += p.z; si += p.w;
-      ++e;
+    int cntp = 0;
+    for (int e = t; e < R && (uint32_t)(key[e] >> 32) == vid; ++e) {
+      const int run = (int)(uint32_t)key[e];
+      for (int q = rstart[run]; q < rstart[run + 1]; ++q) {
+        const float4 p = lp[cpos[q]];
+        sx += p.x; sy += p.y; sz += p.z; si += p.w;
+        ++cntp;
+      }
     }
-    const float nn = (float)(e - t);
+    const float nn = (float)cntp;
     out[vo++] = make_float4(sx / nn, sy / nn, sz / nn, si / nn);
   }
   if (tid == 0) rc[2 * H + i] = V;
 }
 
 // ---------------------------------------------------------------------------------------------
-// K9 concatenate per-ring lists (ring order, FA:1165) and DBSCAN_EdgeFeature (FA:1318-1387)
-// + cluster run-length filter (FA:1281-1305). ONE WAVE per scan: the serial merge loop over i
-// needs a neighbourhood pass, a min-label reduction and a relabel pass per point; inside one wave
-// these are ordered by the wave's own LDS ordering (no workgroup barriers). The O(M^2) tests run
-// 64-wide. Points / labels live in LDS when M <= kDb, else in per-slot global scratch.
-// Semantics reproduced exactly: in_label_list always holds the labels of the eps-neighbours as
-// read before any update (with cluster[i] = 0), so the relabel also collapses every point whose
-// label is 0 — including not-yet-visited ones — into min_label (FA:1369-1375).
+// K9a concatenate the per-ring lists in ring order (FA:1165 loop) and prepare the DBSCAN point
+// records of the edge candidates: lidar-frame (x0, y0, z0) = LOAM (z, x, y), kxy, kz
+// (FA:1326-1336). One workgroup (256 threads) per scan.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fa_concat(DevCfg c, DevBufs d) {
+  __shared__ int roff[3][65];
+  const int b = blockIdx.x;
+  const int H = c.H;
+  const size_t base = (size_t)b * c.HW;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int* rc = d.ring_cnt + (size_t)b * 3 * H;
+  if (tid < 64) {
+    for (int q = 0; q < 3; ++q) {
+      const int v = tid < H ? rc[q * H + tid] : 0;
+      const int incl = wave_incl_scan_add(v);
+      if (tid < H) roff[q][tid] = incl - v;
+      if (tid == 63) roff[q][H] = incl;
+    }
+  }
+  __syncthreads();
+  const int M = roff[0][H];
+  for (int r = 0; r < H; ++r) {
+    const int sp = d.start_ring[b * H + r];
+    for (int t = tid; t < rc[r]; t += nt) d.less_sharp[base + roff[0][r] + t] = d.edge_tmp[base + sp + t];
+    for (int t = tid; t < rc[H + r]; t += nt) d.flat[base + roff[1][r] + t] = d.flat_tmp[base + sp + t];
+    for (int t = tid; t < rc[2 * H + r]; t += nt) d.lflat[base + roff[2][r] + t] = d.lflat_tmp[base + sp + t];
+  }
+  __syncthreads();
+  const float4* loam = d.loam + base;
+  for (int a = tid; a < M; a += nt) {
+    const float4 p = loam[d.less_sharp[base + a]];
+    const float x0 = p.z, y0 = p.x, z0 = p.y;
+    const float AB = atan2f_(z0, sqrt_(x0 * x0 + y0 * y0));
+    const float kxy = sqrt_(x0 * x0 + y0 * y0) * c.sinResX * c.RatioXY;
+    const float kz = (sqrt_(x0 * x0 + y0 * y0) * tanf_(AB + c.fa_resY) -
+                      sqrt_(x0 * x0 + y0 * y0) * tanf_(AB - c.fa_resY)) / 2 * c.RatioZ;
+    d.db_pts[base + a] = make_float4(x0, y0, z0, kxy);
+    d.db_kz[base + a] = kz;
+  }
+  if (tid == 0) {
+    int* cnt = d.counts + b * kCnt;
+    cnt[C_M] = M;
+    cnt[C_F] = roff[1][H];
+    cnt[C_L] = roff[2][H];
+  }
+}
+
+// eps test of FA:1353-1354 with point i as the centre and j's scales
+__device__ __forceinline__ bool db_near(const DevCfg& c, float4 pi, float4 pj, float kzj) {
+  const float eps = sqrt_((pi.x - pj.x) * (pi.x - pj.x) / (pj.w * pj.w) +
+                          (pi.y - pj.y) * (pi.y - pj.y) / (pj.w * pj.w) +
+                          (pi.z - pj.z) * (pi.z - pj.z) / (kzj * kzj));
+  return eps <= c.DBFr;
+}
+
+// ---------------------------------------------------------------------------------------------
+// K9b eps-neighbourhood bitmask for every (i, j) of a scan (M <= kAdjCap): one wave evaluates
+// 64 consecutive j of one row i and stores the ballot as two words. Massively parallel; this
+// takes the O(M^2) float work off DBSCAN's serial merge. grid (32, B), block 256.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_dbscan_adj(DevCfg c, DevBufs d) {
+  const int b = blockIdx.y;
+  const size_t base = (size_t)b * c.HW;
+  const int M = d.counts[b * kCnt + C_M];
+  if (M > kAdjCap) return;
+  const int nch = (M + 63) / 64;
+  const int wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwv = (gridDim.x * blockDim.x) >> 6;
+  const int l = lane_id();
+  uint32_t* adj = d.db_adj + (size_t)b * kAdjCap * kAdjWords;
+  for (int task = wv; task < M * nch; task += nwv) {
+    const int i = task / nch, ch = task - i * nch;
+    const int j = ch * 64 + l;
+    bool nb = false;
+    if (j < M) nb = db_near(c, d.db_pts[base + i], d.db_pts[base + j], d.db_kz[base + j]);
+    const unsigned long long m = __ballot(nb);
+    if (l == 0) adj[(size_t)i * kAdjWords + 2 * ch] = (uint32_t)m;
+    if (l == 1 && 2 * ch + 1 < kAdjWords) adj[(size_t)i * kAdjWords + 2 * ch + 1] = (uint32_t)(m >> 32);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K9c DBSCAN merge (FA:1342-1386) + cluster run-length filter (FA:1281-1305), ONE WAVE per scan.
+// The reference relabels every point whose label is in the neighbours' label list, including
+// label 0 (so all still-unlabelled points collapse into min_label). That is a merge of label
+// classes, done here with a union-find over label nodes 1..M plus "zero" nodes: Z0 holds every
+// not-yet-visited point, and visiting i moves i into a fresh zero node (cluster[i] = 0). A merge
+// unions the neighbours' classes — and, when a neighbour is unlabelled, every live zero class —
+// into min_label; a new label only re-points the neighbours. Checked against a literal
+// transcription of the loop in tests/test_dbscan_uf.py. Per point: O(degree) work.
 // ---------------------------------------------------------------------------------------------
 constexpr int kDb = 2048;
 
@@ -381,134 +524,173 @@ __device__ __forceinline__ void wave_fence() {
   __builtin_amdgcn_wave_barrier();
 }
 
-__global__ __launch_bounds__(64) void k_fa_finish(DevCfg c, DevBufs d) {
-  __shared__ int roff[3][65];
-  __shared__ float4 sP[kDb];
-  __shared__ int sAux[kDb + 1];   // kz (as float bits) during the merge, label histogram after
-  __shared__ int sCl[kDb];
-  __shared__ uint32_t sIn[kDb / 32];
-  __shared__ uint32_t sLb[kDb / 32 + 1];
-  const int b = blockIdx.x;
-  const int H = c.H;
-  const size_t base = (size_t)b * c.HW;
-  const int l = threadIdx.x;
-  const int* rc = d.ring_cnt + (size_t)b * 3 * H;
-  // ring offsets (exclusive scan over <= 64 rings, three lists)
-  for (int q = 0; q < 3; ++q) {
-    const int v = l < H ? rc[q * H + l] : 0;
-    const int incl = wave_incl_scan_add(v);
-    if (l < H) roff[q][l] = incl - v;
-    if (l == 63) roff[q][H] = incl;
+template <bool lds>
+__device__ __forceinline__ int uf_root(int* par, int x) {
+  while (true) {
+    const int p = par[x];
+    if (p == x) return x;
+    const int gp = par[p];
+    par[x] = gp;
+    if (gp == p) return p;
+    x = gp;
   }
-  wave_fence();
-  const int M = roff[0][H], F = roff[1][H], Lf = roff[2][H];
-  for (int r = 0; r < H; ++r) {
-    const int sp = d.start_ring[b * H + r];
-    for (int t = l; t < rc[r]; t += 64) d.less_sharp[base + roff[0][r] + t] = d.edge_tmp[base + sp + t];
-    for (int t = l; t < rc[H + r]; t += 64) d.flat[base + roff[1][r] + t] = d.flat_tmp[base + sp + t];
-    for (int t = l; t < rc[2 * H + r]; t += 64) d.lflat[base + roff[2][r] + t] = d.lflat_tmp[base + sp + t];
-  }
-  __threadfence_block();
+}
 
-  const bool lds = M <= kDb;
-  float4* P = lds ? sP : d.db_pts + base;
-  int* AUX = lds ? sAux : (int*)(d.db_kz + base);
-  int* CL = lds ? sCl : d.cluster + base;
-  uint32_t* IN = lds ? sIn : (uint32_t*)(d.ccl_b + base);
-  const int nwIn = (M + 31) / 32, nwLb = (M + 1 + 31) / 32;
-  uint32_t* LB = lds ? sLb : IN + nwIn;
-  const float4* loam = d.loam + base;
-  for (int a = l; a < M; a += 64) {
-    const float4 p = loam[d.less_sharp[base + a]];
-    const float x0 = p.z, y0 = p.x, z0 = p.y;  // LOAM -> lidar axes (FA:1327-1329)
-    const float AB = atan2f_(z0, sqrt_(x0 * x0 + y0 * y0));
-    const float kxy = sqrt_(x0 * x0 + y0 * y0) * c.sinResX * c.RatioXY;
-    const float kz = (sqrt_(x0 * x0 + y0 * y0) * tanf_(AB + c.fa_resY) -
-                      sqrt_(x0 * x0 + y0 * y0) * tanf_(AB - c.fa_resY)) / 2 * c.RatioZ;
-    P[a] = make_float4(x0, y0, z0, kxy);
-    AUX[a] = __float_as_int(kz);
-    CL[a] = 0;
-  }
-  for (int w = l; w < nwIn; w += 64) IN[w] = 0u;
-  for (int w = l; w < nwLb; w += 64) LB[w] = 0u;
-  __threadfence_block();
+template <bool lds>
+__device__ __forceinline__ void dbscan_merge(const DevCfg& c, const DevBufs& d, size_t base, int b, int M,
+                                             int* par, int* raw, int* nb, int* rt, int* live, int* shn) {
+  auto sync_ = [&]() {
+    if (lds) wave_fence();
+    else __threadfence_block();
+  };
+  const int l = lane_id();
+  const unsigned long long lt = (1ull << l) - 1ull;
+  const int Z0 = M + 1;
+  for (int x = l; x < 2 * M + 3; x += 64) par[x] = x;
+  for (int j = l; j < M; j += 64) raw[j] = Z0;
+  if (l == 0) { live[0] = Z0; shn[0] = 1; }
+  sync_();
+  const bool pre = M <= kAdjCap;
+  const uint32_t* adj = d.db_adj + (size_t)b * kAdjCap * kAdjWords;
+  const int W32 = (M + 31) / 32;
   int label = 0;
+  // rows are <= 64 words when precomputed (M <= kAdjCap): prefetch row i+1 while merging row i
+  uint32_t nextw = (pre && M > 0 && l < W32) ? adj[l] : 0u;
   for (int i = 0; i < M; ++i) {
-    const float4 pi = P[i];
-    int lmin = 999999999;
-    for (int j = l; j < M; j += 64) {
-      const float4 pj = P[j];
-      const float kzj = __int_as_float(AUX[j]);
-      const float eps = sqrt_((pi.x - pj.x) * (pi.x - pj.x) / (pj.w * pj.w) +
-                              (pi.y - pj.y) * (pi.y - pj.y) / (pj.w * pj.w) +
-                              (pi.z - pj.z) * (pi.z - pj.z) / (kzj * kzj));
-      if (eps <= c.DBFr) {
-        const int lj = j == i ? 0 : CL[j];
-        atomicOr(&IN[j >> 5], 1u << (j & 31));
-        atomicOr(&LB[lj >> 5], 1u << (lj & 31));
-        if (lj != 0 && lj < lmin) lmin = lj;
+    const int zi = M + 2 + i;
+    if (l == 0) raw[i] = zi;
+    // neighbour list of i in increasing j
+    int deg = 0;
+    bool i_in = false;
+    const float4 pi = pre ? make_float4(0.f, 0.f, 0.f, 0.f) : d.db_pts[base + i];
+    const uint32_t roww = nextw;
+    if (pre) nextw = (i + 1 < M && l < W32) ? adj[(size_t)(i + 1) * kAdjWords + l] : 0u;
+    for (int w0 = 0; w0 < W32; w0 += 64) {
+      const int w = w0 + l;
+      uint32_t word = 0u;
+      if (w < W32) {
+        if (pre) {
+          word = roww;
+        } else {
+          for (int q = 0; q < 32; ++q) {
+            const int j = 32 * w + q;
+            if (j < M && db_near(c, pi, d.db_pts[base + j], d.db_kz[base + j])) word |= 1u << q;
+          }
+        }
       }
+      if (w == (i >> 5)) i_in = (word >> (i & 31)) & 1u;
+      const int cnt = __popc(word);
+      const int ex = wave_incl_scan_add(cnt) - cnt;
+      int pos = deg + ex;
+      while (word) {
+        const int q = __ffs(word) - 1;
+        word &= word - 1u;
+        nb[pos++] = 32 * w + q;
+      }
+      deg += __shfl(ex + cnt, 63, 64);
+    }
+    i_in = __ballot(i_in) != 0ull;
+    sync_();
+    int lmin = 999999999;
+    bool zero = false;
+    for (int k = l; k < deg; k += 64) {
+      const int r = uf_root<lds>(par, raw[nb[k]]);
+      rt[k] = r;
+      if (r > M) zero = true;
+      else if (r < lmin) lmin = r;
     }
     lmin = wave_reduce_min(lmin);
-    if (lds) wave_fence(); else __threadfence_block();
+    zero = __ballot(zero) != 0ull;
+    sync_();
     if (lmin <= label) {
-      for (int j = l; j < M; j += 64) {
-        const int cur = j == i ? 0 : CL[j];
-        if (((IN[j >> 5] >> (j & 31)) & 1u) || ((LB[cur >> 5] >> (cur & 31)) & 1u)) CL[j] = lmin;
-        else if (j == i) CL[j] = 0;
+      for (int k = l; k < deg; k += 64) {
+        const int r = rt[k];
+        if (r <= M && r != lmin) par[r] = lmin;
+        raw[nb[k]] = lmin;
+      }
+      if (zero) {
+        const int nl = shn[0];
+        for (int k = l; k <= nl; k += 64) {
+          const int z = k < nl ? live[k] : zi;
+          const int r = uf_root<lds>(par, z);
+          if (r > M) par[r] = lmin;
+        }
+        sync_();
+        if (l == 0) shn[0] = 0;
+      } else if (!i_in && l == 0) {
+        live[shn[0]] = zi;
+        shn[0] += 1;
       }
     } else {
       label += 1;
-      for (int j = l; j < M; j += 64) {
-        if ((IN[j >> 5] >> (j & 31)) & 1u) CL[j] = label;
-        else if (j == i) CL[j] = 0;
+      for (int k = l; k < deg; k += 64) raw[nb[k]] = label;
+      if (!i_in && l == 0) {
+        live[shn[0]] = zi;
+        shn[0] += 1;
       }
     }
-    if (lds) wave_fence(); else __threadfence_block();
-    for (int w = l; w < nwIn; w += 64) IN[w] = 0u;
-    for (int w = l; w <= (label >> 5) && w < nwLb; w += 64) LB[w] = 0u;
-    if (lds) wave_fence(); else __threadfence_block();
+    sync_();
   }
+  // final labels -> raw (as CL) and the output array
+  for (int j = l; j < M; j += 64) {
+    const int r = uf_root<lds>(par, raw[j]);
+    const int v = r > M ? 0 : r;
+    d.cluster[base + j] = v;
+    nb[j] = v;
+  }
+  sync_();
   // ---- run lengths of the sorted labels, last run dropped; keep label r+1 if run r >= 4 ----
-  int* hist = AUX;
+  int* CL = nb;
+  int* hist = rt;
   const int NL = label + 1;
   for (int q = l; q < NL; q += 64) hist[q] = 0;
-  __threadfence_block();
+  sync_();
   for (int a = l; a < M; a += 64) atomicAdd(&hist[CL[a]], 1);
-  __threadfence_block();
+  sync_();
   int lmax = -1;
   for (int q = l; q < NL; q += 64)
     if (hist[q] > 0) lmax = q;
   lmax = wave_reduce_max(lmax);
-  for (int w = l; w < nwLb; w += 64) LB[w] = 0u;
-  __threadfence_block();
-  const unsigned long long lt = (1ull << l) - 1ull;
+  uint32_t* keep = (uint32_t*)par;  // label-indexed bitmap, par no longer needed
+  const int nwLb = (NL + 1 + 31) / 32;
+  for (int w = l; w < nwLb; w += 64) keep[w] = 0u;
+  sync_();
   int run = 0;
   for (int q0 = 0; q0 < NL; q0 += 64) {
     const int q = q0 + l;
     const bool pres = q < NL && hist[q] > 0;
     const unsigned long long m = __ballot(pres);
     const int r = run + __popcll(m & lt);
-    if (pres && q != lmax && hist[q] >= 4 && r + 1 < NL) atomicOr(&LB[(r + 1) >> 5], 1u << ((r + 1) & 31));
+    if (pres && q != lmax && hist[q] >= 4 && r + 1 < NL) atomicOr(&keep[(r + 1) >> 5], 1u << ((r + 1) & 31));
     run += __popcll(m);
   }
-  __threadfence_block();
+  sync_();
   int ns = 0;
   for (int a0 = 0; a0 < M; a0 += 64) {
     const int a = a0 + l;
-    const bool keep = a < M && ((LB[CL[a] >> 5] >> (CL[a] & 31)) & 1u);
-    const unsigned long long m = __ballot(keep);
-    if (keep) d.sharp[base + ns + __popcll(m & lt)] = d.less_sharp[base + a];
+    const bool kp = a < M && ((keep[CL[a] >> 5] >> (CL[a] & 31)) & 1u);
+    const unsigned long long m = __ballot(kp);
+    if (kp) d.sharp[base + ns + __popcll(m & lt)] = d.less_sharp[base + a];
     ns += __popcll(m);
   }
-  if (lds)
-    for (int a = l; a < M; a += 64) d.cluster[base + a] = CL[a];
-  if (l == 0) {
-    int* cnt = d.counts + b * kCnt;
-    cnt[C_M] = M;
-    cnt[C_SHARP] = ns;
-    cnt[C_F] = F;
-    cnt[C_L] = Lf;
+  if (l == 0) d.counts[b * kCnt + C_SHARP] = ns;
+}
+
+__global__ __launch_bounds__(64) void k_dbscan_merge(DevCfg c, DevBufs d) {
+  __shared__ int sPar[2 * kDb + 4];
+  __shared__ int sRaw[kDb];
+  __shared__ int sNb[kDb];
+  __shared__ int sRt[kDb + 1];
+  __shared__ int sLive[kDb + 1];
+  __shared__ int sN[1];
+  const int b = blockIdx.x;
+  const size_t base = (size_t)b * c.HW;
+  const int M = d.counts[b * kCnt + C_M];
+  if (M <= kDb) {
+    dbscan_merge<true>(c, d, base, b, M, sPar, sRaw, sNb, sRt, sLive, sN);
+  } else {  // global scratch: ccl_b (2*HW ints) parent, ccl_a raw, cluster nb, edge_tmp rt, shuf live
+    dbscan_merge<false>(c, d, base, b, M, (int*)(d.ccl_b + base), d.ccl_a + base, d.flat_tmp + base,
+                        d.edge_tmp + base, d.shuf + base, d.shuf + base + c.HW - 1);
   }
 }
 

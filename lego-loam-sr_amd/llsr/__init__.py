@@ -132,6 +132,12 @@ class Pipeline:
     def set_profiling(self, on: bool):
         self._check(lib().llsr_set_profiling(self._h, 1 if on else 0), "llsr_set_profiling")
 
+    def debug_phase_ms(self, kernel: int, phase: int, reps: int = 5) -> float:
+        """Diagnostics: mean ms of kernel `kernel` re-launched with an early exit at `phase`."""
+        f = lib().llsr_debug_phase_ms
+        f.restype, f.argtypes = C.c_float, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]
+        return float(f(self._h, kernel, phase, reps))
+
     def kernel_times(self) -> dict:
         buf = np.zeros(32, dtype=np.float32)
         n = lib().llsr_kernel_times_ms(self._h, buf.ctypes.data, 32)

@@ -1,0 +1,29 @@
+"""Attribute kernel time to phases: run one batch, then re-launch selected kernels with an
+early exit at each phase boundary (diagnostic launches; their outputs are meaningless)."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "lego-loam-sr_amd"))
+from llsr import Pipeline, default_config, synth  # noqa: E402
+
+lidar = sys.argv[1] if len(sys.argv) > 1 else "vlp16"
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+cfg = default_config(lidar, 2048 if lidar == "hdl64e" else None)
+pts, off = synth.make_batch(B, lidar, distinct=8)
+d_pts, d_off = torch.from_numpy(pts).cuda(), torch.from_numpy(off).cuda()
+pipe = Pipeline(cfg, max_batch=B, max_points=int(np.diff(off).max()))
+for _ in range(3):
+    pipe.process_batch(d_pts.data_ptr(), d_off.data_ptr(), B)
+pipe.set_profiling(True)
+pipe.process_batch(d_pts.data_ptr(), d_off.data_ptr(), B)
+res = {"kernels": pipe.kernel_times()}
+names = {3: "k_ground_add", 4: "k_ground_elev_ransac", 5: "k_label", 6: "k_segment", 7: "k_fa_points",
+         8: "k_select_ring", 9: "k_fa_concat", 10: "k_dbscan_adj", 11: "k_dbscan_merge"}
+for k, phases in ((8, range(0, 8)),):
+    res[names[k]] = {p: round(pipe.debug_phase_ms(k, p, 5), 4) for p in phases}
+print(json.dumps(res))
