@@ -16,6 +16,7 @@
 namespace llsr {
 __global__ void k_project(DevCfg, const float4*, const int64_t*, DevBufs);
 __global__ void k_gather_column(DevCfg, const float4*, const int64_t*, DevBufs);
+__global__ void k_project_fused(DevCfg, const float4*, const int64_t*, DevBufs);
 __global__ void k_ground_add(DevCfg, DevBufs);
 __global__ void k_ground_elev_ransac(DevCfg, DevBufs);
 template <bool kLds> __global__ void k_label(DevCfg, DevBufs);
@@ -222,6 +223,8 @@ extern "C" int32_t llsr_create(const llsr_config* cfg, int32_t hip_device, int32
       if (hipEventCreate(&e) != hipSuccess) { llsr_destroy(h); return LLSR_ENODEV; }
   if (h->dc.ccl_lds) {
     if (hipFuncSetAttribute((const void*)k_label<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            h->dc.HW * (int)sizeof(int)) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_project_fused, hipFuncAttributeMaxDynamicSharedMemorySize,
                             h->dc.HW * (int)sizeof(int)) != hipSuccess) {
       llsr_destroy(h);
       return LLSR_ENODEV;
@@ -305,13 +308,19 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
     ++k;
   };
   mark();
-  HIP_OK(h, hipMemsetAsync(h->d.cell_pt, 0xFF, sizeof(int) * (size_t)B * c.HW, s));
+  if (!c.ccl_lds) HIP_OK(h, hipMemsetAsync(h->d.cell_pt, 0xFF, sizeof(int) * (size_t)B * c.HW, s));
   k_init_counts<<<(B + 255) / 256, 256, 0, s>>>(h->d.counts, B);
   mark();
-  k_project<<<dim3((h->max_points + 255) / 256, B), 256, 0, s>>>(c, pts, d_offsets, h->d);
-  mark();
-  k_gather_column<<<dim3((c.W + 255) / 256, B), 256, 0, s>>>(c, pts, d_offsets, h->d);
-  mark();
+  if (c.ccl_lds) {  // fused projection + column ground pass with the cell table in LDS
+    k_project_fused<<<B, 1024, c.HW * sizeof(int), s>>>(c, pts, d_offsets, h->d);
+    mark();
+    mark();
+  } else {
+    k_project<<<dim3((h->max_points + 255) / 256, B), 256, 0, s>>>(c, pts, d_offsets, h->d);
+    mark();
+    k_gather_column<<<dim3((c.W + 255) / 256, B), 256, 0, s>>>(c, pts, d_offsets, h->d);
+    mark();
+  }
   k_ground_add<<<dim3((c.H + 3) / 4, B), 256, 0, s>>>(c, h->d);
   mark();
   k_ground_elev_ransac<<<B, 1024, 0, s>>>(c, h->d);

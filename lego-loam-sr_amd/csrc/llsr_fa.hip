@@ -525,7 +525,7 @@ __device__ __forceinline__ void wave_fence() {
 }
 
 template <bool lds>
-__device__ __forceinline__ int uf_root(int* par, int x) {
+__device__ __forceinline__ int uf_root(int* par, int x) {  // path halving
   while (true) {
     const int p = par[x];
     if (p == x) return x;
@@ -536,11 +536,33 @@ __device__ __forceinline__ int uf_root(int* par, int x) {
   }
 }
 
+// Minimum of v over lanes with `valid`, for 0 <= v < 2^nbits, by ballots (scalar work only);
+// returns 999999999 when no lane is valid.
+__device__ __forceinline__ int wave_min_ballot(int v, bool valid, int nbits) {
+  unsigned long long cand = __ballot(valid);
+  if (!cand) return 999999999;
+  const int l = lane_id();
+  int res = 0;
+  for (int bt = nbits - 1; bt >= 0; --bt) {
+    const unsigned long long z = __ballot(((cand >> l) & 1ull) && !((v >> bt) & 1));
+    if (z) cand = z;
+    else res |= 1 << bt;
+  }
+  return res;
+}
+
+// A wave's LDS instructions execute in issue order, so lanes of one wave only need the compiler
+// not to move memory operations across these points (no s_waitcnt, no cache maintenance).
+__device__ __forceinline__ void wave_order() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
 template <bool lds>
 __device__ __forceinline__ void dbscan_merge(const DevCfg& c, const DevBufs& d, size_t base, int b, int M,
                                              int* par, int* raw, int* nb, int* rt, int* live, int* shn) {
   auto sync_ = [&]() {
-    if (lds) wave_fence();
+    if (lds) wave_order();
     else __threadfence_block();
   };
   const int l = lane_id();

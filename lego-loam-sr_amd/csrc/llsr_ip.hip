@@ -124,6 +124,118 @@ __global__ __launch_bounds__(256) void k_gather_column(DevCfg c, const float4* _
 }
 
 // ---------------------------------------------------------------------------------------------
+// K1+K2 fused for range images that fit LDS (H*W <= 32768, e.g. VLP-16): one workgroup per scan.
+// Pass 1 projects every raw point (coalesced reads) and resolves IP:337-347's serial "last writer
+// wins" with an LDS atomicMax of the raw index per cell; pass 2 re-reads the points and only each
+// cell's winner writes range / full_cloud / raw intensity; empty cells get the resetParameters
+// values (IP:170-179); pass 3 runs the per-column ground test + Filter (IP:524-629) on the cell
+// arrays. No global atomics, no gather of scattered input points.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int project_cell(const DevCfg& c, float4 p, float* range_out) {
+  const float range = sqrt_(p.x * p.x + p.y * p.y + p.z * p.z);
+  *range_out = range;
+  const float va = asinf_(p.z / range);
+  const int row = trunc_i32((double)((va + c.ip_angBottom) / c.ip_resY));
+  if (row < 0 || row >= c.H) return -1;
+  const float ha = atan2f_(p.x, p.y);
+  int col = trunc_i32(-round(((double)ha - kPi / 2) / (double)c.ip_resX) + c.W * 0.5);
+  if (col >= c.W) col -= c.W;
+  if (col < 0 || col >= c.W || (double)range < 0.1) return -1;
+  return col + row * c.W;
+}
+
+__device__ __forceinline__ void ground_column(const DevCfg& c, const float4* __restrict__ full, int8_t* ground,
+                                              int j) {
+  bool haveRV = false, obs = false;
+  float RVx = 0.f, RVy = 0.f, RVz = 0.f, lx = 0.f, ly = 0.f, lz = 0.f;
+  for (int i = 0; i < c.H; ++i) {
+    const int cell = j + i * c.W;
+    const float4 f = full[cell];
+    int8_t g;
+    if (f.w == 0.0f) {
+      g = -1;
+    } else if (!haveRV) {
+      const float d0 = sqrt_(f.x * f.x + f.y * f.y);
+      RVx = f.x / d0; RVy = f.y / d0; RVz = 0.0f;
+      haveRV = true;
+      lx = f.x; ly = f.y; lz = f.z;
+      g = 1;
+    } else {
+      const float TVx = f.x - lx, TVy = f.y - ly, TVz = f.z - lz;
+      const float ang = (float)((double)acosf_((TVx * RVx + TVy * RVy + TVz * RVz) /
+                                               (sqrt_(TVx * TVx + TVy * TVy + TVz * TVz) *
+                                                sqrt_(RVx * RVx + RVy * RVy + RVz * RVz))) /
+                                kDegToRad);
+      const float D = c.use_kitti ? (i < 16 ? 60.0f : 25.0f) : 12.5f;
+      if (ang <= D) { RVx += TVx; RVy += TVy; RVz += TVz; g = 1; }
+      else g = 0;
+      lx = f.x; ly = f.y; lz = f.z;
+    }
+    if (g == 0) obs = true;
+    else if (g == 1 && obs) g = 2;
+    ground[cell] = g;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_project_fused(DevCfg c, const float4* __restrict__ pts,
+                                                        const int64_t* __restrict__ off, DevBufs d) {
+  extern __shared__ int cidx[];
+  __shared__ int tmp[32];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int HW = c.HW;
+  const size_t base = (size_t)b * HW;
+  const int64_t o0 = off[b];
+  const int n = (int)(off[b + 1] - o0);
+  for (int q = tid; q < HW; q += nt) cidx[q] = -1;
+  __syncthreads();
+  int nfin = 0, first = INT_MAX, last = -1;
+  for (int i = tid; i < n; i += nt) {
+    const float4 p = pts[o0 + i];
+    if (!finite3(p)) continue;
+    ++nfin;
+    first = i < first ? i : first;
+    last = i;
+    float r;
+    const int cell = project_cell(c, p, &r);
+    if (cell >= 0) atomicMax(&cidx[cell], i);
+  }
+  nfin = block_reduce_add(nfin, tmp);
+  first = block_reduce_min(first, tmp);
+  last = -block_reduce_min(-last, tmp);
+  if (tid == 0) {
+    int* cnt = d.counts + b * kCnt;
+    cnt[C_NPTS] = nfin;
+    cnt[C_FIRST] = first;
+    cnt[C_LAST] = last;
+  }
+  // winners write their cell; then empty cells get the reset values
+  for (int i = tid; i < n; i += nt) {
+    const float4 p = pts[o0 + i];
+    if (!finite3(p)) continue;
+    float r;
+    const int cell = project_cell(c, p, &r);
+    if (cell < 0 || cidx[cell] != i) continue;
+    const int row = cell / c.W, col = cell - row * c.W;
+    d.range[base + cell] = r;
+    d.full[base + cell] = make_float4(p.x, p.y, p.z, (float)((double)(float)row + (double)(float)col / 10000.0));
+    d.vis[base + cell] = p.w;
+  }
+  const float qnan = __builtin_nanf("");
+  for (int q = tid; q < HW; q += nt) {
+    const int pi = cidx[q];
+    d.cell_pt[base + q] = pi;
+    if (pi < 0) {
+      d.range[base + q] = FLT_MAX;
+      d.full[base + q] = make_float4(qnan, qnan, qnan, 0.0f);
+      d.vis[base + q] = 0.0f;
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < c.W; j += nt) ground_column(c, d.full + base, d.ground + base, j);
+}
+
+// ---------------------------------------------------------------------------------------------
 // K3 ADD (IP:631-671): per row, a forward then a backward recurrence "2 -> 1 if a ground cell
 // sits one or two columns behind and the step is short". The state before column j is the pair
 // (g'[j-2]==1, g'[j-1]==1), so each column is a map on 4 states; a wave composes the maps of
