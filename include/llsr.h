@@ -107,6 +107,20 @@ typedef struct llsr_scan_out {
   float* less_flat_xyzi;       /* [4*L] surfPointsLessFlat (per-ring VoxelGrid 0.2, FA:1268) */
 } llsr_scan_out;
 
+/* Result of one scan-to-map optimisation (MapOptimization::scan2MapOptimization, MO:1572-1610). */
+typedef struct llsr_lm_report {
+  int32_t iterations;     /* iter_num (MO:1581): 200 in faithful mode unless iteration 0 converges */
+  int32_t converged;      /* LMOptimization returned true */
+  int32_t degenerate;     /* isDegenerate (MO:1518-1529) */
+  float min_lambda;       /* smallest eigenvalue of J^T J at iteration 0 (MO:1515) */
+  float cf_mean;          /* mean |residual| of the last evaluated iteration (MO:1560/1568) */
+  int32_t n_corner_corr;  /* corner / surf correspondences kept at the last iteration */
+  int32_t n_surf_corr;
+  float matX0[6];         /* the iteration-0 step matX (faithful-mode parity target) */
+  float pose[6];          /* final transformTobeMapped */
+  float ms;               /* wall/device time of the optimisation, ms */
+} llsr_lm_report;
+
 typedef struct llsr_sizes {
   int32_t cells;               /* H*W: bound for every per-point array */
   int32_t rings;               /* H */

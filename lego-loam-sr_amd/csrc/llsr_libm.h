@@ -10,8 +10,8 @@
 // -ffp-contract=off, correctly-rounded f32 divide/sqrt — hipcc's default).
 //
 // Validation: oracle/libm_check.cpp compares every function against the host glibc over all
-// 2^32 float inputs (asinf, acosf, atanf, tanf on |x| < 3pi/4) and over dense random/structured
-// pairs for atan2f. See DESIGN.md §libm.
+// 2^32 float inputs (asinf, acosf, atanf; tanf, sinf, cosf on |x| < 120) and over dense
+// random/structured pairs for atan2f. See DESIGN.md §2.
 #pragma once
 #include <stdint.h>
 #include <string.h>
@@ -292,6 +292,87 @@ LLSR_HD float tanf_(float x) {
     return kernel_tanf_(y0, y1, 1 - ((n & 1) << 1));
   }
   return bitsf(0x7fc00000u);
+}
+
+
+// ---- sinf / cosf: glibc >= 2.28 sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c (sincosf.h):
+// double-precision polynomials after reduce_fast (|x| < 120). Larger |x| is outside the hot
+// path's domain (angles of a 6-DoF pose) and returns NaN so a misuse is loud.
+struct SinCosTab {
+  double sign[4];
+  double hpi_inv, hpi, c0, c1, c2, c3, c4, s1, s2, s3;
+};
+LLSR_HD const SinCosTab& sincos_tab(int k) {
+  static const SinCosTab T[2] = {
+      {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, 0x1p0, -0x1.ffffffd0c621cp-2,
+       0x1.55553e1068f19p-5, -0x1.6c087e89a359dp-10, 0x1.99343027bf8c3p-16, -0x1.555545995a603p-3,
+       0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13},
+      {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, -0x1p0, 0x1.ffffffd0c621cp-2,
+       -0x1.55553e1068f19p-5, 0x1.6c087e89a359dp-10, -0x1.99343027bf8c3p-16, -0x1.555545995a603p-3,
+       0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13}};
+  return T[k];
+}
+LLSR_HD uint32_t abstop12(float x) { return (fbits(x) >> 20) & 0x7ff; }
+// x86-64 glibc dispatches sinf/cosf (and only those of the functions used here) through an
+// ifunc to a copy of this code built with -mfma -mavx2 (sysdeps/x86_64/fpu/multiarch/s_sinf.c),
+// so every multiply feeding an add is one fused op there; restated with explicit fma so host
+// and device agree with what the reference gets on any FMA-capable x86 (libm_check pins it).
+LLSR_HD float sinf_poly(double x, double x2, const SinCosTab& p, int n) {
+  if ((n & 1) == 0) {
+    const double x3 = x * x2;
+    const double s1 = __builtin_fma(x2, p.s3, p.s2);
+    const double x7 = x3 * x2;
+    const double s = __builtin_fma(x3, p.s1, x);
+    return (float)__builtin_fma(x7, s1, s);
+  }
+  const double x4 = x2 * x2;
+  const double c2 = __builtin_fma(x2, p.c4, p.c3);
+  const double c1 = __builtin_fma(x2, p.c1, p.c0);
+  const double x6 = x4 * x2;
+  const double c = __builtin_fma(x4, p.c2, c1);
+  return (float)__builtin_fma(x6, c2, c);
+}
+LLSR_HD double reduce_fast_(double x, const SinCosTab& p, int* np) {
+  const double r = x * p.hpi_inv;
+  const int n = ((int32_t)r + 0x800000) >> 24;
+  *np = n;
+  return __builtin_fma(-(double)n, p.hpi, x);
+}
+LLSR_HD float sinf_(float y) {
+  double x = y;
+  int n;
+  const SinCosTab* p = &sincos_tab(0);
+  if (abstop12(y) < abstop12(0x1.921FB6p-1f)) {
+    const double s = x * x;
+    if (abstop12(y) < abstop12(0x1p-12f)) return y;
+    return sinf_poly(x, s, *p, 0);
+  } else if (abstop12(y) < abstop12(120.0f)) {
+    x = reduce_fast_(x, *p, &n);
+    const double s = p->sign[n & 3];
+    if (n & 2) p = &sincos_tab(1);
+    return sinf_poly(x * s, x * x, *p, n);
+  } else if (abstop12(y) < abstop12(__builtin_inff())) {
+    return bitsf(0x7fc00000u);
+  }
+  return (y - y) / (y - y);
+}
+LLSR_HD float cosf_(float y) {
+  double x = y;
+  int n;
+  const SinCosTab* p = &sincos_tab(0);
+  if (abstop12(y) < abstop12(0x1.921FB6p-1f)) {
+    const double x2 = x * x;
+    if (abstop12(y) < abstop12(0x1p-12f)) return 1.0f;
+    return sinf_poly(x, x2, *p, 1);
+  } else if (abstop12(y) < abstop12(120.0f)) {
+    x = reduce_fast_(x, *p, &n);
+    const double s = p->sign[n & 3];
+    if (n & 2) p = &sincos_tab(1);
+    return sinf_poly(x * s, x * x, *p, n ^ 1);
+  } else if (abstop12(y) < abstop12(__builtin_inff())) {
+    return bitsf(0x7fc00000u);
+  }
+  return (y - y) / (y - y);
 }
 
 }  // namespace llsr_libm

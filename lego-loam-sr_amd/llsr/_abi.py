@@ -114,6 +114,28 @@ class ScanOut(C.Structure):
     ]
 
 
+class LmReport(C.Structure):
+    """llsr_lm_report (include/llsr.h): result of one scan-to-map optimisation."""
+    _fields_ = [
+        ("iterations", C.c_int32),
+        ("converged", C.c_int32),
+        ("degenerate", C.c_int32),
+        ("min_lambda", C.c_float),
+        ("cf_mean", C.c_float),
+        ("n_corner_corr", C.c_int32),
+        ("n_surf_corr", C.c_int32),
+        ("matX0", C.c_float * 6),
+        ("pose", C.c_float * 6),
+        ("ms", C.c_float),
+    ]
+
+    def as_dict(self) -> dict:
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["matX0"] = np.array(self.matX0[:], dtype=np.float32)
+        d["pose"] = np.array(self.pose[:], dtype=np.float32)
+        return d
+
+
 class Sizes(C.Structure):
     _fields_ = [("cells", C.c_int32), ("rings", C.c_int32), ("max_points", C.c_int32),
                 ("shadow_points", C.c_int32)]

@@ -110,10 +110,15 @@ class _Scene:
 
 
 def make_scan(seed: int, lidar: str = VLP16, dropout: float = 0.02, noise: float = 0.01,
-              max_range: float = 100.0) -> np.ndarray:
-    """One raw scan as float32 [N, 4] (x, y, z, intensity), N = rings * columns (NaNs kept)."""
+              max_range: float = 100.0, origin_xy: tuple[float, float] | None = None,
+              scene_id: int | None = None) -> np.ndarray:
+    """One raw scan as float32 [N, 4] (x, y, z, intensity), N = rings * columns (NaNs kept).
+
+    The sensor sits at (0.5 * (seed % 64), U(-0.5, 0.5), 0) of scene `seed // 64`; scan-to-map
+    fixtures override both (`origin_xy`, `scene_id`) to place keyframes along one street."""
     rng = np.random.default_rng(seed)
-    scene = _Scene(np.random.default_rng(1000003 + seed // 64))  # scenes shared by 64 scans
+    scene_id = seed // 64 if scene_id is None else scene_id  # scenes shared by 64 scans
+    scene = _Scene(np.random.default_rng(1000003 + scene_id))
     elev, W = beam_layout(lidar)
     H = elev.shape[0]
     res_x = 2.0 * np.pi / W
@@ -127,6 +132,8 @@ def make_scan(seed: int, lidar: str = VLP16, dropout: float = 0.02, noise: float
     d[:, :, 2] = se[None, :]
     d = d.reshape(-1, 3)
     origin = np.array([0.5 * (seed % 64), rng.uniform(-0.5, 0.5), 0.0])
+    if origin_xy is not None:
+        origin[:2] = origin_xy
     t = scene.cast(origin, d, max_range)
     r = t + rng.normal(0.0, noise, size=t.shape)
     drop = rng.random(t.shape) < dropout

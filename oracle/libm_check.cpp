@@ -2,7 +2,7 @@
 // (lego-loam-sr_amd/csrc/llsr_libm.h) against the host glibc float functions the reference
 // links (imageProjection.cpp:313,321,559; featureAssociation.cpp:577,1330-1332).
 //
-//   libm_check [stride] [threads]
+//   libm_check [stride] [threads] [only]   (only: run just the functions whose name starts so)
 // stride=1 sweeps all 2^32 inputs per unary function; atan2f is checked on a dense grid of
 // (y, x) pairs plus every exponent/sign combination. Exit status = number of mismatching
 // functions (0 = bit-identical everywhere tested).
@@ -22,9 +22,11 @@ static bool same(float a, float b) {
   return fbits(a) == fbits(b);
 }
 
+static const char* g_only = "";
 template <class F, class G>
 static long sweep(const char* name, F port, G ref, uint64_t lo, uint64_t hi, uint64_t stride,
                   int nthreads) {
+  if (std::strncmp(name, g_only, std::strlen(g_only)) != 0) return 0;
   std::atomic<long> bad{0};
   std::atomic<int> shown{0};
   std::vector<std::thread> th;
@@ -51,6 +53,7 @@ int main(int argc, char** argv) {
   uint64_t stride = argc > 1 ? strtoull(argv[1], 0, 10) : 1;
   int nthreads = argc > 2 ? atoi(argv[2]) : (int)std::thread::hardware_concurrency();
   if (nthreads < 1) nthreads = 1;
+  g_only = argc > 3 ? argv[3] : "";
   int failed = 0;
   const uint64_t ALL = 1ull << 32;
   failed += sweep("asinf", asinf_, [](float x) { return std::asin(x); }, 0, ALL, stride, nthreads) != 0;
@@ -60,6 +63,11 @@ int main(int argc, char** argv) {
   failed += sweep("tanf+", tanf_, [](float x) { return std::tan(x); }, 0, 0x42f00000ull, stride, nthreads) != 0;
   failed += sweep("tanf-", tanf_, [](float x) { return std::tan(x); }, 0x80000000ull,
                   0x80000000ull + 0x42f00000ull, stride, nthreads) != 0;
+  // sinf / cosf on |x| < 120 (glibc's reduce_fast domain; the restated domain)
+  failed += sweep("sinf+", sinf_, [](float x) { return std::sin(x); }, 0, 0x42f00000ull, stride, nthreads) != 0;
+  failed += sweep("sinf-", sinf_, [](float x) { return std::sin(x); }, 0x80000000ull, 0x80000000ull + 0x42f00000ull, stride, nthreads) != 0;
+  failed += sweep("cosf+", cosf_, [](float x) { return std::cos(x); }, 0, 0x42f00000ull, stride, nthreads) != 0;
+  failed += sweep("cosf-", cosf_, [](float x) { return std::cos(x); }, 0x80000000ull, 0x80000000ull + 0x42f00000ull, stride, nthreads) != 0;
   // atan2f: y sweeps a strided subset of all floats, x from a structured set.
   {
     std::vector<float> xs;

@@ -30,6 +30,19 @@ void oracle_stage_ms(const oracle_state* s, double* ip_ms, double* fa_ms);
  * used to show the synthetic scenes' inlier sets do not depend on the RNG. */
 int32_t oracle_ransac_inliers(oracle_state* s, uint32_t seed, int32_t* inliers, int32_t cap);
 
+/* MapOptimization::scan2MapOptimization (MO:1572-1610) on explicit inputs: corner queries
+ * (laserCloudCornerScanDS), surf queries (laserCloudSurfTotalLastDS), corner / surf local maps
+ * (…FromMapDS), float4 x,y,z,intensity each; `pose` = transformTobeMapped in/out.
+ * cfg->mode selects faithful (update commented out, MO:1539-1545) or lm_applied. */
+int32_t oracle_scan2map(const llsr_config* cfg, const float* corner_q, int32_t Qc, const float* surf_q,
+                        int32_t Qs, const float* corner_map, int32_t Mc, const float* surf_map, int32_t Ms,
+                        float* pose, llsr_lm_report* rep);
+/* Test hooks for the Eigen restatements (llsr_eigen.h): column-major inputs. */
+int32_t oracle_eig3(const float* A, float* evals, float* evecs);
+int32_t oracle_eig6(const float* A, float* evals, float* evecs);
+void oracle_qr_solve_5x3(const float* A, const float* b, float* x);
+void oracle_qr_solve_6x6(const float* A, const float* b, float* x);
+
 #ifdef __cplusplus
 }
 #endif

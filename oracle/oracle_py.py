@@ -29,8 +29,8 @@ def lib():
     global _LIB
     if _LIB is None:
         path = os.path.join(_HERE, "_build", "liboracle.so")
-        src = os.path.join(_HERE, "oracle_ipfa.cpp")
-        if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+        srcs = [os.path.join(_HERE, f) for f in ("oracle_ipfa.cpp", "oracle_mo.cpp")]
+        if not os.path.exists(path) or os.path.getmtime(path) < max(map(os.path.getmtime, srcs)):
             build()
         L = C.CDLL(path)
         L.oracle_create.restype = C.c_void_p
@@ -42,6 +42,15 @@ def lib():
         L.oracle_stage_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.oracle_ransac_inliers.restype = C.c_int32
         L.oracle_ransac_inliers.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int32]
+        L.oracle_scan2map.restype = C.c_int32
+        L.oracle_scan2map.argtypes = [C.POINTER(_abi.Config), C.c_void_p, C.c_int32, C.c_void_p, C.c_int32,
+                                      C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p,
+                                      C.POINTER(_abi.LmReport)]
+        for f in ("oracle_eig3", "oracle_eig6"):
+            getattr(L, f).restype = C.c_int32
+            getattr(L, f).argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        for f in ("oracle_qr_solve_5x3", "oracle_qr_solve_6x6"):
+            getattr(L, f).argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         _LIB = L
     return _LIB
 
@@ -81,3 +90,49 @@ class Oracle:
         buf = np.zeros(cap, dtype=np.int32)
         n = lib().oracle_ransac_inliers(self._h, seed, buf.ctypes.data, cap)
         return buf[:n].copy()
+
+
+def _f4(a) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    if a.ndim != 2 or a.shape[1] != 4:
+        raise ValueError("expected (n, 4) float32 x,y,z,intensity")
+    return a
+
+
+def scan2map(cfg: _abi.Config, corner_q, surf_q, corner_map, surf_map, pose0) -> dict:
+    """MapOptimization::scan2MapOptimization (MO:1572-1610) on explicit clouds; returns the
+    report dict (pose = final transformTobeMapped)."""
+    cq, sq, cm, sm = (_f4(a) for a in (corner_q, surf_q, corner_map, surf_map))
+    pose = np.ascontiguousarray(pose0, dtype=np.float32).copy()
+    rep = _abi.LmReport()
+    rc = lib().oracle_scan2map(C.byref(cfg), cq.ctypes.data, len(cq), sq.ctypes.data, len(sq),
+                               cm.ctypes.data, len(cm), sm.ctypes.data, len(sm), pose.ctypes.data,
+                               C.byref(rep))
+    if rc != 0:
+        raise RuntimeError(f"oracle_scan2map: {rc}")
+    d = rep.as_dict()
+    d["pose"] = pose
+    return d
+
+
+def eig(A: np.ndarray):
+    """Eigen SelfAdjointEigenSolver restatement (3x3 or 6x6): ascending evals, evec columns."""
+    n = A.shape[0]
+    a = np.asfortranarray(A, dtype=np.float32).ravel(order="F")
+    ev = np.zeros(n, np.float32)
+    V = np.zeros(n * n, np.float32)
+    f = lib().oracle_eig3 if n == 3 else lib().oracle_eig6
+    rc = f(a.ctypes.data, ev.ctypes.data, V.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("eig did not converge")
+    return ev, V.reshape(n, n, order="F")
+
+
+def qr_solve(A: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """Eigen ColPivHouseholderQR::solve restatement for 5x3 and 6x6 systems."""
+    a = np.asfortranarray(A, dtype=np.float32).ravel(order="F")
+    b = np.ascontiguousarray(b, dtype=np.float32)
+    x = np.zeros(A.shape[1], np.float32)
+    f = lib().oracle_qr_solve_5x3 if A.shape == (5, 3) else lib().oracle_qr_solve_6x6
+    f(a.ctypes.data, b.ctypes.data, x.ctypes.data)
+    return x

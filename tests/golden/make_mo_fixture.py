@@ -1,0 +1,82 @@
+"""Build the scan-to-map fixture (BASELINE.json configs[2]); run from the repo root.
+
+A local map made the way MapOptimization makes one (extractSurroundingKeyFrames, MO:1096-1232):
+keyframes every 1 m (the 1 m keypose leaf, MO:99) along the whole 150 m synthetic street — wider
+than the 50 m surrounding-keyframe radius (loam_config.yaml:26) so the map reaches the config's
+~100k-point size (15.2k corner + 61.3k surf = 76k) — each keyframe's corner (less-sharp), surf
+(less-flat) and outlier clouds from the oracle's IP + FA feature stage, moved into the map
+frame by the known sensor pose, concatenated (MO:1219-1221) and voxel-downsampled (corner 0.2 m,
+surf 0.4 m; MO:92-94, 1225-1231). Queries follow downsampleCurrentScan (MO:1234-1267): corner
+= sharp DS 0.2, surf total = DS 0.4 of (less-flat DS 0.4 + outliers DS 0.4). True pose = the
+frame's sensor position in the LOAM frame; the optimiser starts from a seeded (0.05 rad, 0.2 m)
+perturbation. The scene, noise and oracle are seeded, so the script is deterministic.
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "lego-loam-sr_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+from llsr import _abi, synth  # noqa: E402
+import oracle_py  # noqa: E402
+
+
+def voxel_ds(p, leaf):
+    """Centroid per voxel (floor(p/leaf) keys), output in ascending voxel order."""
+    if len(p) == 0:
+        return p
+    k = np.floor(p[:, :3] / np.float32(leaf)).astype(np.int64)
+    k -= k.min(axis=0)
+    dims = k.max(axis=0) + 1
+    key = k[:, 0] + dims[0] * (k[:, 1] + dims[1] * k[:, 2])
+    order = np.argsort(key, kind="stable")
+    key, p = key[order], p[order]
+    _, start, cnt = np.unique(key, return_index=True, return_counts=True)
+    sums = np.add.reduceat(p.astype(np.float64), start, axis=0)
+    return (sums / cnt[:, None]).astype(np.float32)
+
+
+def frame_clouds(cfg, seed, x, y):
+    """(less_sharp, sharp, less_flat, outliers) of one frame in its LOAM frame, + map offset."""
+    ora = oracle_py.Oracle(cfg)
+    r = ora.process(synth.make_scan(seed, "vlp16", origin_xy=(x, y), scene_id=0))
+    loam = r["loam_xyzi"]
+    out = r["outlier_xyzi"].copy()
+    out[:, :3] = out[:, [1, 2, 0]]  # lidar -> LOAM axes (FA adjustOutlierCloud)
+    off = np.array([y, 0.0, x], dtype=np.float32)  # sensor (x, y, 0) in LOAM axes (y, z, x)
+    return loam[r["less_sharp_ind"]], loam[r["sharp_ind"]], r["less_flat_xyzi"], out, off
+
+
+def main(query_x=(5.3, 10.7, 15.2, 20.6), out="mo_map_vlp16.npz"):
+    cfg = _abi.config_for("vlp16")
+    rng = np.random.default_rng(77)
+    corner, surf = [], []
+    for k, x in enumerate(np.arange(-62.0, 89.0, 1.0)):
+        ls, _, lf, ol, off = frame_clouds(cfg, 2000 + k, x, rng.uniform(-0.5, 0.5))
+        for dst, pts in ((corner, ls), (surf, lf), (surf, ol)):
+            q = pts.copy()
+            q[:, :3] += off
+            dst.append(q)
+    corner_map = voxel_ds(np.concatenate(corner), 0.2)
+    surf_map = voxel_ds(np.concatenate(surf), 0.4)
+    frames = {}
+    for i, x in enumerate(query_x):
+        _, sharp, lf, ol, off = frame_clouds(cfg, 3000 + i, x, rng.uniform(-0.5, 0.5))
+        true = np.array([0, 0, 0, off[0], off[1], off[2]], dtype=np.float32)
+        init = true + np.concatenate([rng.uniform(-0.05, 0.05, 3), rng.uniform(-0.2, 0.2, 3)]).astype(np.float32)
+        frames[f"q{i}_corner"] = voxel_ds(sharp, 0.2)
+        frames[f"q{i}_surf"] = voxel_ds(np.concatenate([voxel_ds(lf, 0.4), voxel_ds(ol, 0.4)]), 0.4)
+        frames[f"q{i}_true"] = true
+        frames[f"q{i}_init"] = init
+    np.savez_compressed(os.path.join(HERE, out), corner_map=corner_map, surf_map=surf_map,
+                        n_queries=np.int32(len(query_x)), **frames)
+    print(f"corner map {len(corner_map)}, surf map {len(surf_map)}; queries " +
+          ", ".join(f"{len(frames[f'q{i}_corner'])}/{len(frames[f'q{i}_surf'])}" for i in range(len(query_x))))
+
+
+if __name__ == "__main__":
+    main()
