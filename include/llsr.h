@@ -168,6 +168,40 @@ const char* llsr_kernel_name(int32_t k);
 /* Enable/disable per-kernel event timing; (re)enabling clears the accumulated averages. */
 int32_t llsr_set_profiling(llsr_handle* h, int32_t enable);
 
+/* ---- MapOptimization scan-to-map (scan2MapOptimization, mapOptmization.cpp:1572-1610) ----
+ * A batch of independent problems, one per scan: the scan's corner queries
+ * (laserCloudCornerScanDS, MO:1244-1247) and surf queries (laserCloudSurfTotalLastDS,
+ * MO:1259-1266), the corner / surf local maps (laserCloud{Corner,Surf}FromMapDS, MO:1225-1231)
+ * and transformTobeMapped. Clouds are float4 rows (x, y, z, intensity) concatenated over the
+ * batch with int64 offsets [P+1], all device-resident. The handle's config supplies
+ * iterCountThres, step_size, stop_thres and mode (LLSR_MODE_FAITHFUL keeps the reference's
+ * commented-out pose update, MO:1539-1545; LLSR_MODE_LM_APPLIED applies it). */
+typedef struct llsr_s2m_batch {
+  int32_t n_problems;
+  const float* corner_q;   const int64_t* corner_q_off;
+  const float* surf_q;     const int64_t* surf_q_off;
+  const float* corner_map; const int64_t* corner_map_off;
+  const float* surf_map;   const int64_t* surf_map_off;
+  float* pose;               /* [P][6] in/out: roll, pitch, yaw, x, y, z (LOAM frame) */
+  llsr_lm_report* report;    /* [P] out (device memory); report.ms is 0 in batch mode */
+} llsr_s2m_batch;
+
+/* Size the scan-to-map buffers: up to `max_problems` problems per batch with at most the given
+ * points per cloud. Replaces MO's per-scan kd-tree allocation (MO:1575-1576). */
+int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t max_problems, int32_t max_corner_map,
+                              int32_t max_surf_map, int32_t max_corner_q, int32_t max_surf_q);
+/* Run the batch on `hip_stream` (NULL: the handle's stream). The LM's iteration count is data
+ * dependent, so the call waits on the stream every few iterations to stop once every problem
+ * has converged or reached iterCountThres; it returns when the batch is complete.
+ * LLSR_ERANGE: a cloud exceeds the reserved capacity (nothing written for that problem). */
+int32_t llsr_scan2map_batch(llsr_handle* h, const llsr_s2m_batch* batch, void* hip_stream);
+/* One problem from host buffers (the reference's call shape: scan2MapOptimization on the
+ * member clouds); reserves as needed; `pose` in/out; rep->ms = device time. */
+int32_t llsr_scan2map(llsr_handle* h, const float* corner_q, int32_t n_corner_q, const float* surf_q,
+                      int32_t n_surf_q, const float* corner_map, int32_t n_corner_map,
+                      const float* surf_map, int32_t n_surf_map, float* pose, llsr_lm_report* rep);
+
+
 #ifdef __cplusplus
 }
 #endif

@@ -12,6 +12,7 @@
 
 #include "../../include/llsr.h"
 #include "llsr_device.h"
+#include "llsr_mo.h"
 
 namespace llsr {
 __global__ void k_project(DevCfg, const float4*, const int64_t*, DevBufs);
@@ -66,6 +67,16 @@ struct llsr_handle {
   int ring_head = 0, ring_used = 0;
   double ksum[kNumKernels] = {};
   long long kbatches = 0;
+  // scan-to-map (llsr_scan2map_*): buffers sized by llsr_scan2map_reserve
+  struct {
+    int P = 0, qc = 0, qs = 0, mc = 0, ms = 0, log2T_c = 0, log2T_s = 0, blocks_c = 0, blocks = 0;
+    void* pool = nullptr;
+    S2MArgs a{};
+    int* host_flags = nullptr;   // pinned: n_active, error
+    void* stage = nullptr;       // single-problem staging (llsr_scan2map)
+    size_t stage_bytes = 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+  } mo;
   std::string err;
 };
 
@@ -238,15 +249,20 @@ extern "C" int32_t llsr_create(const llsr_config* cfg, int32_t hip_device, int32
 
 extern "C" void llsr_destroy(llsr_handle* h) {
   if (!h) return;
-  hipSetDevice(h->device);
-  if (h->stream) hipStreamSynchronize(h->stream);
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
   for (auto& set : h->ev)
     for (auto& e : set)
       if (e) (void)hipEventDestroy(e);
-  if (h->pool) hipFree(h->pool);
-  if (h->d_in) hipFree(h->d_in);
-  if (h->d_off) hipFree(h->d_off);
-  if (h->stream) hipStreamDestroy(h->stream);
+  if (h->pool) (void)hipFree(h->pool);
+  if (h->mo.pool) (void)hipFree(h->mo.pool);
+  if (h->mo.stage) (void)hipFree(h->mo.stage);
+  if (h->mo.host_flags) (void)hipHostFree(h->mo.host_flags);
+  if (h->mo.e0) (void)hipEventDestroy(h->mo.e0);
+  if (h->mo.e1) (void)hipEventDestroy(h->mo.e1);
+  if (h->d_in) (void)hipFree(h->d_in);
+  if (h->d_off) (void)hipFree(h->d_off);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
 
@@ -486,4 +502,173 @@ extern "C" int32_t llsr_process_scan(llsr_handle* h, const float* xyzi, int32_t 
   int32_t rc = llsr_process_batch(h, (const float*)h->d_in, h->d_off, 1, h->stream);
   if (rc) return rc;
   return llsr_fetch_scan(h, 0, out);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Scan-to-map (MapOptimization::scan2MapOptimization, MO:1572-1610): see llsr_mo.hip.
+
+static int log2_table(int cap) {  // table of >= 2 * cap slots (load factor <= 0.5)
+  int l = 4;
+  while ((1ll << l) < 2ll * (cap > 1 ? cap : 1)) ++l;
+  return l;
+}
+
+extern "C" int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t P, int32_t mc, int32_t ms, int32_t qc,
+                                         int32_t qs) {
+  if (!h) return LLSR_EINVAL;
+  if (P < 1 || mc < 0 || ms < 0 || qc < 0 || qs < 0 || mc > (1 << 26) || ms > (1 << 26) ||
+      qc > (1 << 24) || qs > (1 << 24))
+    return fail(h, LLSR_EINVAL, "scan2map capacities out of range");
+  HIP_OK(h, hipSetDevice(h->device));
+  auto& m = h->mo;
+  if (m.pool && P <= m.P && mc <= m.mc && ms <= m.ms && qc <= m.qc && qs <= m.qs) return LLSR_OK;
+  if (m.pool) {
+    HIP_OK(h, hipDeviceSynchronize());
+    HIP_OK(h, hipFree(m.pool));
+    m.pool = nullptr;
+  }
+  m.P = P; m.mc = mc; m.ms = ms; m.qc = qc; m.qs = qs;
+  m.log2T_c = log2_table(mc);
+  m.log2T_s = log2_table(ms);
+  m.blocks_c = (qc + 255) / 256;
+  m.blocks = m.blocks_c + (qs + 255) / 256;
+  if (m.blocks == 0) m.blocks = 1;
+  const size_t Tc = (size_t)1 << m.log2T_c, Ts = (size_t)1 << m.log2T_s;
+  const size_t bytes = sizeof(S2MProb) * P + sizeof(S2MSlot) * P * (Tc + Ts) +
+                       sizeof(float4) * P * ((size_t)mc + ms) + sizeof(int2) * P * ((size_t)mc + ms) +
+                       sizeof(int) * 2 * P + sizeof(float) * 32 * (size_t)P * m.blocks + 4096 + 8 * 256;
+  if (hipMalloc(&m.pool, bytes) != hipSuccess) {
+    m.pool = nullptr;
+    m.P = 0;
+    return fail(h, LLSR_ENOMEM, "scan2map buffers");
+  }
+  char* q = (char*)m.pool;
+  S2MArgs& a = m.a;
+  a = S2MArgs{};
+  a.prob = carve<S2MProb>(q, P);
+  a.tab_c = carve<S2MSlot>(q, P * Tc);
+  a.tab_s = carve<S2MSlot>(q, P * Ts);
+  a.pts_c = carve<float4>(q, (size_t)P * mc);
+  a.pts_s = carve<float4>(q, (size_t)P * ms);
+  a.where_c = carve<int2>(q, (size_t)P * mc);
+  a.where_s = carve<int2>(q, (size_t)P * ms);
+  a.cursor = carve<int>(q, 2 * (size_t)P);
+  a.partial = carve<float>(q, 32 * (size_t)P * m.blocks);
+  a.n_active = carve<int>(q, 2);
+  a.error = a.n_active + 1;
+  a.cap_qc = qc; a.cap_qs = qs; a.cap_mc = mc; a.cap_ms = ms;
+  a.blocks_c = m.blocks_c;
+  a.log2T_c = m.log2T_c; a.log2T_s = m.log2T_s;
+  if (!m.host_flags && hipHostMalloc((void**)&m.host_flags, 2 * sizeof(int)) != hipSuccess) {
+    m.host_flags = nullptr;
+    return fail(h, LLSR_ENOMEM, "pinned flags");
+  }
+  if (!m.e0 && (hipEventCreate(&m.e0) != hipSuccess || hipEventCreate(&m.e1) != hipSuccess))
+    return fail(h, LLSR_ENODEV, "events");
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_scan2map_batch(llsr_handle* h, const llsr_s2m_batch* b, void* hip_stream) {
+  if (!h || !b) return fail(h, LLSR_EINVAL, "null argument");
+  auto& m = h->mo;
+  if (!m.pool) return fail(h, LLSR_EINVAL, "llsr_scan2map_reserve not called");
+  const int P = b->n_problems;
+  if (P < 1 || P > m.P) return fail(h, LLSR_ERANGE, "n_problems outside [1, reserved]");
+  if (!b->corner_q_off || !b->surf_q_off || !b->corner_map_off || !b->surf_map_off || !b->pose || !b->report)
+    return fail(h, LLSR_EINVAL, "null batch array");
+  HIP_OK(h, hipSetDevice(h->device));
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+  S2MArgs a = m.a;
+  a.P = P;
+  a.applied = h->cfg.mode == LLSR_MODE_LM_APPLIED;
+  a.iter_max = h->cfg.iterCountThres;
+  a.step_size = h->cfg.step_size;
+  a.stop_thres = h->cfg.stop_thres;
+  a.cq = b->corner_q; a.cq_off = b->corner_q_off;
+  a.sq = b->surf_q; a.sq_off = b->surf_q_off;
+  a.cm = b->corner_map; a.cm_off = b->corner_map_off;
+  a.sm = b->surf_map; a.sm_off = b->surf_map_off;
+  a.pose = b->pose;
+  a.report = b->report;
+  HIP_OK(h, hipMemsetAsync(a.n_active, 0, 2 * sizeof(int), s));
+  k_s2m_setup<<<(P + 63) / 64, 64, 0, s>>>(a);
+  const int Tmax = 1 << (m.log2T_c > m.log2T_s ? m.log2T_c : m.log2T_s);
+  const int Mmax = m.mc > m.ms ? m.mc : m.ms;
+  k_s2m_grid_clear<<<dim3((Tmax + 255) / 256, P, 2), 256, 0, s>>>(a);
+  if (Mmax > 0) k_s2m_grid_insert<<<dim3((Mmax + 255) / 256, P, 2), 256, 0, s>>>(a);
+  k_s2m_grid_alloc<<<dim3((Tmax + 255) / 256, P, 2), 256, 0, s>>>(a);
+  if (Mmax > 0) k_s2m_grid_scatter<<<dim3((Mmax + 255) / 256, P, 2), 256, 0, s>>>(a);
+  HIP_OK(h, hipGetLastError());
+  // LM iterations; poll the active count every `poll` launches
+  const int poll = 4;
+  for (int it = 0; it < a.iter_max;) {
+    const int n = (a.iter_max - it) < poll ? (a.iter_max - it) : poll;
+    for (int k = 0; k < n; ++k) k_s2m_iter<<<dim3(m.blocks, P), 256, 0, s>>>(a);
+    it += n;
+    HIP_OK(h, hipGetLastError());
+    HIP_OK(h, hipMemcpyAsync(m.host_flags, a.n_active, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_OK(h, hipStreamSynchronize(s));
+    if (m.host_flags[1]) return fail(h, LLSR_ERANGE, "a scan2map cloud exceeds the reserved capacity or has bad offsets");
+    if (m.host_flags[0] == 0) break;
+  }
+  k_s2m_finish<<<(P + 63) / 64, 64, 0, s>>>(a);
+  HIP_OK(h, hipGetLastError());
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_scan2map(llsr_handle* h, const float* cq, int32_t Qc, const float* sq, int32_t Qs,
+                                 const float* cm, int32_t Mc, const float* sm, int32_t Ms, float* pose,
+                                 llsr_lm_report* rep) {
+  if (!h || !pose || !rep || Qc < 0 || Qs < 0 || Mc < 0 || Ms < 0) return fail(h, LLSR_EINVAL, "bad argument");
+  if ((Qc && !cq) || (Qs && !sq) || (Mc && !cm) || (Ms && !sm)) return fail(h, LLSR_EINVAL, "null cloud");
+  auto& m = h->mo;
+  const int P = m.pool ? m.P : 1;
+  int32_t rc = llsr_scan2map_reserve(h, P, Mc > m.mc ? Mc : m.mc, Ms > m.ms ? Ms : m.ms,
+                                     Qc > m.qc ? Qc : m.qc, Qs > m.qs ? Qs : m.qs);
+  if (rc != LLSR_OK) return rc;
+  const size_t npts = (size_t)Qc + Qs + Mc + Ms;
+  const size_t need = sizeof(float4) * npts + 8 * sizeof(int64_t) + 6 * sizeof(float) + sizeof(llsr_lm_report) +
+                      8 * 256;  // carve() pads each of the 7 pieces to 256 B
+  if (need > m.stage_bytes) {
+    if (m.stage) HIP_OK(h, hipFree(m.stage));
+    m.stage = nullptr;
+    if (hipMalloc(&m.stage, need) != hipSuccess) { m.stage_bytes = 0; return fail(h, LLSR_ENOMEM, "staging"); }
+    m.stage_bytes = need;
+  }
+  char* q = (char*)m.stage;
+  float4* d_cq = carve<float4>(q, Qc);
+  float4* d_sq = carve<float4>(q, Qs);
+  float4* d_cm = carve<float4>(q, Mc);
+  float4* d_sm = carve<float4>(q, Ms);
+  int64_t* d_off = carve<int64_t>(q, 8);
+  float* d_pose = carve<float>(q, 6);
+  llsr_lm_report* d_rep = carve<llsr_lm_report>(q, 1);
+  hipStream_t s = h->stream;
+  HIP_OK(h, hipSetDevice(h->device));
+  if (Qc) HIP_OK(h, hipMemcpyAsync(d_cq, cq, sizeof(float4) * Qc, hipMemcpyHostToDevice, s));
+  if (Qs) HIP_OK(h, hipMemcpyAsync(d_sq, sq, sizeof(float4) * Qs, hipMemcpyHostToDevice, s));
+  if (Mc) HIP_OK(h, hipMemcpyAsync(d_cm, cm, sizeof(float4) * Mc, hipMemcpyHostToDevice, s));
+  if (Ms) HIP_OK(h, hipMemcpyAsync(d_sm, sm, sizeof(float4) * Ms, hipMemcpyHostToDevice, s));
+  const int64_t offs[8] = {0, Qc, 0, Qs, 0, Mc, 0, Ms};
+  HIP_OK(h, hipMemcpyAsync(d_off, offs, sizeof offs, hipMemcpyHostToDevice, s));
+  HIP_OK(h, hipMemcpyAsync(d_pose, pose, 6 * sizeof(float), hipMemcpyHostToDevice, s));
+  llsr_s2m_batch b{};
+  b.n_problems = 1;
+  b.corner_q = (const float*)d_cq; b.corner_q_off = d_off;
+  b.surf_q = (const float*)d_sq; b.surf_q_off = d_off + 2;
+  b.corner_map = (const float*)d_cm; b.corner_map_off = d_off + 4;
+  b.surf_map = (const float*)d_sm; b.surf_map_off = d_off + 6;
+  b.pose = d_pose;
+  b.report = d_rep;
+  HIP_OK(h, hipEventRecord(m.e0, s));
+  rc = llsr_scan2map_batch(h, &b, s);
+  if (rc != LLSR_OK) return rc;
+  HIP_OK(h, hipEventRecord(m.e1, s));
+  HIP_OK(h, hipMemcpyAsync(rep, d_rep, sizeof *rep, hipMemcpyDeviceToHost, s));
+  HIP_OK(h, hipMemcpyAsync(pose, d_pose, 6 * sizeof(float), hipMemcpyDeviceToHost, s));
+  HIP_OK(h, hipStreamSynchronize(s));
+  float ms_ = 0.f;
+  HIP_OK(h, hipEventElapsedTime(&ms_, m.e0, m.e1));
+  rep->ms = ms_;
+  return LLSR_OK;
 }

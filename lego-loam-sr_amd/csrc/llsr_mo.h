@@ -1,0 +1,62 @@
+// llsr_mo.h — device data of the scan-to-map batch (llsr_mo.hip), shared with the host side.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/llsr.h"
+
+namespace llsr {
+
+// One open-addressing slot of a problem's 1 m cell table.
+struct S2MSlot {
+  uint64_t key;  // packed cell (x, y, z) or ~0 = empty
+  int start;     // first point of the cell in the cell-contiguous copy
+  int count;
+};
+
+// Per-problem optimiser state, resident in HBM for the whole batch.
+struct S2MProb {
+  int64_t qc0, qs0, mc0, ms0;  // offsets of this problem's clouds
+  int Qc, Qs, Mc, Ms;
+  float pose[6];               // transformTobeMapped
+  float cR, sR, cP, sP, cY, sY;  // cos/sin of pose[0..2] (MO:591-604, MO:1445-1450)
+  float matP[36];
+  float matX0[6];
+  float min_lambda, cf_mean;
+  int iter, active, converged, degenerate, nc, ns;
+  unsigned ticket;             // blocks of the current iteration that have finished
+  int pad_;
+};
+
+struct S2MArgs {
+  int P;
+  int applied;                 // LLSR_MODE_LM_APPLIED
+  int iter_max;                // iterCountThres
+  float step_size, stop_thres;
+  int cap_qc, cap_qs, cap_mc, cap_ms;
+  int blocks_c;                // query blocks per problem reserved for corners (rest: surf)
+  int log2T_c, log2T_s;        // table sizes per problem
+  const float* cq; const int64_t* cq_off;
+  const float* sq; const int64_t* sq_off;
+  const float* cm; const int64_t* cm_off;
+  const float* sm; const int64_t* sm_off;
+  float* pose;                 // [P][6] in/out
+  llsr_lm_report* report;      // [P]
+  S2MProb* prob;               // [P]
+  S2MSlot* tab_c; S2MSlot* tab_s;  // [P][T]
+  float4* pts_c; float4* pts_s;    // [P][cap] cell-contiguous map copies
+  int2* where_c; int2* where_s;    // [P][cap] (slot, rank) per map point
+  int* cursor;                 // [P][2]
+  float* partial;              // [P][blocks][32] block sums
+  int* n_active;               // problems still iterating
+  int* error;                  // capacity / offset violations
+};
+
+__global__ void k_s2m_setup(S2MArgs a);
+__global__ void k_s2m_grid_clear(S2MArgs a);
+__global__ void k_s2m_grid_insert(S2MArgs a);
+__global__ void k_s2m_grid_alloc(S2MArgs a);
+__global__ void k_s2m_grid_scatter(S2MArgs a);
+__global__ void k_s2m_iter(S2MArgs a);
+__global__ void k_s2m_finish(S2MArgs a);
+
+}  // namespace llsr

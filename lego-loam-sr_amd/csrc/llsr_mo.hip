@@ -1,0 +1,473 @@
+// llsr_mo.hip — MapOptimization scan-to-map on gfx950: a batch of independent problems
+// (scan2MapOptimization, mapOptmization.cpp:1572-1610), each = corner/surf query clouds of one
+// scan + its corner/surf local maps + the pose transformTobeMapped.
+//
+// Per batch:
+//   k_s2m_setup        problem bookkeeping, capacity checks, the MO:1573 guard
+//   k_s2m_grid_insert  1 m cell hash grid of both maps (kdtreeCornerFromMap / kdtreeSurfFromMap
+//   k_s2m_grid_alloc   setInputCloud, MO:1575-1576): open-addressing table of cell keys, point
+//   k_s2m_grid_scatter counts, then map points copied cell-contiguous as (x, y, z, index bits)
+//   k_s2m_iter  x it   one launch per LM iteration (MO:1578-1608) over (query block, problem):
+//                      pointAssociateToMap, kNN-5, the corner line / surf plane coefficient, the
+//                      Jacobian row, a fixed-order block reduction of the 21 + 6 normal-equation
+//                      terms; the last block of each problem (ticket) sums the block partials in
+//                      block order and runs LMOptimization's solve / degeneracy / update / stop
+//   k_s2m_finish       pose + llsr_lm_report out
+//
+// kNN-5 (nanoflann, exact, sorted) only matters when all five neighbours lie within d^2 < 1.0
+// (MO:1279 / MO:1386), so a 1 m grid over the 27 neighbouring cells finds them exactly. Each
+// thread keeps the five smallest (d^2, map index) pairs: identical to inserting candidates in
+// index order with strict '<' (the restatement in oracle/oracle_mo.cpp), independent of the
+// order the cells are visited. The per-correspondence arithmetic repeats the reference's float
+// and double operations one for one (-ffp-contract=off, glibc sinf/cosf ports, Eigen 3.3.7
+// restatements in llsr_eigen.h), so correspondences and coefficients are bit-identical to the
+// oracle; only the normal-equation summation order differs (the reference's is Eigen's GEMM
+// blocking), hence the pose tolerance of north_star (1e-4).
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <climits>
+#include <cstdint>
+
+#include "../../include/llsr.h"
+#include "llsr_device.h"
+#include "llsr_eigen.h"
+#include "llsr_mo.h"
+
+namespace llsr {
+
+using llsr_libm::bitsf;
+using llsr_libm::cosf_;
+using llsr_libm::fabs_;
+using llsr_libm::fbits;
+using llsr_libm::sinf_;
+using llsr_libm::sqrt_;
+
+namespace {
+
+constexpr uint64_t kEmpty = ~0ull;
+
+__device__ __forceinline__ int cell_coord(float v) {
+  // floor() to a cell index; NaN / huge coordinates land in a far sentinel cell (their distance
+  // test fails anyway, so where they are bucketed cannot change a result)
+  const float f = floorf(v);
+  return (f > -1048000.0f && f < 1048000.0f) ? (int)f : 1048500;
+}
+
+__device__ __forceinline__ uint64_t cell_key(int a, int b, int c) {
+  return ((uint64_t)(uint32_t)(a + 1048576) << 42) | ((uint64_t)(uint32_t)(b + 1048576) << 21) |
+         (uint64_t)(uint32_t)(c + 1048576);
+}
+
+__device__ __forceinline__ uint32_t cell_hash(uint64_t k, int log2T) {
+  return (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> (64 - log2T));
+}
+
+// Probe for `key`; returns the slot or -1.
+__device__ __forceinline__ int grid_find(const S2MSlot* __restrict__ tab, int log2T, uint64_t key) {
+  const uint32_t mask = (1u << log2T) - 1u;
+  uint32_t s = cell_hash(key, log2T);
+  for (;;) {
+    const uint64_t k = tab[s].key;
+    if (k == key) return (int)s;
+    if (k == kEmpty) return -1;
+    s = (s + 1) & mask;
+  }
+}
+
+struct Best5 {
+  float d[5];
+  int i[5];
+};
+
+__device__ __forceinline__ bool before(float da, int ia, float db, int ib) {
+  return da < db || (da == db && ia < ib);
+}
+
+// kNN-5 with d^2 < 1.0 around q in one map; returns true when five were found.
+__device__ bool knn5(const S2MSlot* __restrict__ tab, int log2T, const float4* __restrict__ pts,
+                     float qx, float qy, float qz, Best5& b) {
+#pragma unroll
+  for (int k = 0; k < 5; ++k) { b.d[k] = INFINITY; b.i[k] = INT_MAX; }
+  const int cx = cell_coord(qx), cy = cell_coord(qy), cz = cell_coord(qz);
+  for (int a = -1; a <= 1; ++a)
+    for (int bb = -1; bb <= 1; ++bb)
+      for (int c = -1; c <= 1; ++c) {
+        const int s = grid_find(tab, log2T, cell_key(cx + a, cy + bb, cz + c));
+        if (s < 0) continue;
+        const int st = tab[s].start, n = tab[s].count;
+        for (int j = st; j < st + n; ++j) {
+          const float4 p = pts[j];
+          float d = 0.0f;
+          float t = qx - p.x; d += t * t;  // nanoflann L2 accumulation order
+          t = qy - p.y; d += t * t;
+          t = qz - p.z; d += t * t;
+          const int id = (int)fbits(p.w);
+          if (!(d < 1.0f) || !before(d, id, b.d[4], b.i[4])) continue;
+          b.d[4] = d; b.i[4] = id;
+#pragma unroll
+          for (int k = 4; k > 0; --k)
+            if (before(b.d[k], b.i[k], b.d[k - 1], b.i[k - 1])) {
+              const float td = b.d[k]; b.d[k] = b.d[k - 1]; b.d[k - 1] = td;
+              const int ti = b.i[k]; b.i[k] = b.i[k - 1]; b.i[k - 1] = ti;
+            }
+        }
+      }
+  return b.d[4] < 1.0f;
+}
+
+// pointAssociateToMap (MO:606-620) with the cached sin/cos of transformTobeMapped.
+struct Assoc {
+  float cR, sR, cP, sP, cY, sY, tx, ty, tz;
+  __device__ void apply(float px, float py, float pz, float& ox, float& oy, float& oz) const {
+    const float x1 = cY * px - sY * py;
+    const float y1 = sY * px + cY * py;
+    const float z1 = pz;
+    const float x2 = x1;
+    const float y2 = cR * y1 - sR * z1;
+    const float z2 = sR * y1 + cR * z1;
+    ox = cP * x2 + sP * z2 + tx;
+    oy = y2 + ty;
+    oz = -sP * x2 + cP * z2 + tz;
+  }
+};
+
+// cornerOptimization body (MO:1274-1375) for one query; returns false when rejected.
+__device__ bool corner_coeff(const S2MSlot* tab, int log2T, const float4* pts, const float4* mapP,
+                             float x0, float y0, float z0, float& la, float& lb, float& lc, float& ld) {
+  Best5 nb;
+  if (!knn5(tab, log2T, pts, x0, y0, z0, nb)) return false;
+  float mx[5], my[5], mz[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const float4 m = mapP[nb.i[j]];
+    mx[j] = m.x; my[j] = m.y; mz[j] = m.z;
+  }
+  float cx = 0, cy = 0, cz = 0;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) { cx += mx[j]; cy += my[j]; cz += mz[j]; }
+  cx /= 5; cy /= 5; cz /= 5;
+  float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const float ax = mx[j] - cx, ay = my[j] - cy, az = mz[j] - cz;
+    a11 += ax * ax; a12 += ax * ay; a13 += ax * az; a22 += ay * ay; a23 += ay * az; a33 += az * az;
+  }
+  a11 /= 5; a12 /= 5; a13 /= 5; a22 /= 5; a23 /= 5; a33 /= 5;
+  const float A1[9] = {a11, a12, a13, a12, a22, a23, a13, a23, a33};
+  float D1[3], V1[9];
+  llsr_eigen::eig3(A1, D1, V1);
+  if (!(D1[2] > 3 * D1[1])) return false;
+  const float x1 = (float)(cx + 0.1 * V1[0]), y1 = (float)(cy + 0.1 * V1[3]), z1 = (float)(cz + 0.1 * V1[6]);
+  const float x2 = (float)(cx - 0.1 * V1[0]), y2 = (float)(cy - 0.1 * V1[3]), z2 = (float)(cz - 0.1 * V1[6]);
+  const float u = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
+  const float v = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
+  const float w = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
+  const float a012 = sqrt_(u * u + v * v + w * w);
+  const float l12 = sqrt_((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2));
+  const float a = ((y1 - y2) * u + (z1 - z2) * v) / a012 / l12;
+  const float b = -((x1 - x2) * u - (z1 - z2) * w) / a012 / l12;
+  const float c = -((x1 - x2) * v + (y1 - y2) * w) / a012 / l12;
+  const float ld2 = a012 / l12;
+  const float s = (float)(1 - 0.9 * (double)fabs_(ld2));
+  if (!((double)s > 0.1)) return false;
+  la = s * a; lb = s * b; lc = s * c; ld = s * ld2;
+  return true;
+}
+
+// surfOptimization body (MO:1383-1440) for one query.
+__device__ bool surf_coeff(const S2MSlot* tab, int log2T, const float4* pts, const float4* mapP,
+                           float x0, float y0, float z0, float& la, float& lb, float& lc, float& ld) {
+  Best5 nb;
+  if (!knn5(tab, log2T, pts, x0, y0, z0, nb)) return false;
+  float A0[15];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const float4 m = mapP[nb.i[j]];
+    A0[j] = m.x; A0[5 + j] = m.y; A0[10 + j] = m.z;
+  }
+  const float B0[5] = {-1, -1, -1, -1, -1};
+  float X0[3];
+  llsr_eigen::colpiv_qr_solve<5, 3>(A0, B0, X0);
+  float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1;
+  const float ps = sqrt_(pa * pa + pb * pb + pc * pc);
+  pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+#pragma unroll
+  for (int j = 0; j < 5; ++j)
+    if (fabs_(pa * A0[j] + pb * A0[5 + j] + pc * A0[10 + j] + pd) > 0.2f) return false;
+  const float pd2 = pa * x0 + pb * y0 + pc * z0 + pd;
+  const float r = sqrt_(sqrt_(x0 * x0 + y0 * y0 + z0 * z0));
+  const float s = (float)(1 - 0.9 * (double)fabs_(pd2) / (double)r);
+  if (!((double)s > 0.1)) return false;
+  la = s * pa; lb = s * pb; lc = s * pc; ld = s * pd2;
+  return true;
+}
+
+}  // namespace
+
+__global__ void k_s2m_setup(S2MArgs a) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.P) return;
+  S2MProb& st = a.prob[p];
+  const int64_t qc0 = a.cq_off[p], qc1 = a.cq_off[p + 1], qs0 = a.sq_off[p], qs1 = a.sq_off[p + 1];
+  const int64_t mc0 = a.cm_off[p], mc1 = a.cm_off[p + 1], ms0 = a.sm_off[p], ms1 = a.sm_off[p + 1];
+  st.qc0 = qc0; st.qs0 = qs0; st.mc0 = mc0; st.ms0 = ms0;
+  st.Qc = (int)(qc1 - qc0); st.Qs = (int)(qs1 - qs0); st.Mc = (int)(mc1 - mc0); st.Ms = (int)(ms1 - ms0);
+  int bad = 0;
+  if (qc1 < qc0 || qs1 < qs0 || mc1 < mc0 || ms1 < ms0) bad = 1;
+  if (st.Qc > a.cap_qc || st.Qs > a.cap_qs || st.Mc > a.cap_mc || st.Ms > a.cap_ms) bad = 1;
+  if (bad) {
+    atomicOr(a.error, 1);
+    st.Qc = st.Qs = st.Mc = st.Ms = 0;
+  }
+#pragma unroll
+  for (int k = 0; k < 6; ++k) { st.pose[k] = a.pose[6 * p + k]; st.matX0[k] = 0.0f; }
+  st.iter = 0; st.converged = 0; st.degenerate = 0; st.nc = 0; st.ns = 0;
+  st.min_lambda = 0.0f; st.cf_mean = 0.0f; st.ticket = 0u;
+  st.active = (!bad && st.Mc > 10 && st.Ms > 100) ? 1 : 0;  // MO:1573
+  st.cR = cosf_(st.pose[0]); st.sR = sinf_(st.pose[0]);
+  st.cP = cosf_(st.pose[1]); st.sP = sinf_(st.pose[1]);
+  st.cY = cosf_(st.pose[2]); st.sY = sinf_(st.pose[2]);
+  if (st.active) atomicAdd(a.n_active, 1);
+  a.cursor[2 * p] = 0;
+  a.cursor[2 * p + 1] = 0;
+}
+
+// blockIdx.z: 0 = corner map, 1 = surf map (all grid kernels).
+__global__ void k_s2m_grid_clear(S2MArgs a) {
+  const int p = blockIdx.y, m = blockIdx.z;
+  const int log2T = m ? a.log2T_s : a.log2T_c;
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= (1u << log2T)) return;
+  S2MSlot& t = (m ? a.tab_s : a.tab_c)[((size_t)p << log2T) + s];
+  t.key = kEmpty;
+  t.start = 0;
+  t.count = 0;
+}
+
+__global__ void k_s2m_grid_insert(S2MArgs a) {
+  const int p = blockIdx.y, m = blockIdx.z;
+  const S2MProb& st = a.prob[p];
+  const int n = m ? st.Ms : st.Mc;
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const float4 q = reinterpret_cast<const float4*>(m ? a.sm : a.cm)[(m ? st.ms0 : st.mc0) + k];
+  const uint64_t key = cell_key(cell_coord(q.x), cell_coord(q.y), cell_coord(q.z));
+  const int log2T = m ? a.log2T_s : a.log2T_c;
+  S2MSlot* tab = (m ? a.tab_s : a.tab_c) + ((size_t)p << log2T);
+  const uint32_t mask = (1u << log2T) - 1u;
+  uint32_t s = cell_hash(key, log2T);
+  for (;;) {
+    const uint64_t prev = atomicCAS((unsigned long long*)&tab[s].key, (unsigned long long)kEmpty,
+                                    (unsigned long long)key);
+    if (prev == kEmpty || prev == key) break;
+    s = (s + 1) & mask;
+  }
+  const int rank = atomicAdd(&tab[s].count, 1);
+  int2* where = (m ? a.where_s : a.where_c) + (size_t)p * (m ? a.cap_ms : a.cap_mc);
+  where[k] = make_int2((int)s, rank);
+}
+
+__global__ void k_s2m_grid_alloc(S2MArgs a) {
+  const int p = blockIdx.y, m = blockIdx.z;
+  const int log2T = m ? a.log2T_s : a.log2T_c;
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= (1u << log2T)) return;
+  S2MSlot* tab = (m ? a.tab_s : a.tab_c) + ((size_t)p << log2T);
+  const int c = tab[s].count;
+  if (c > 0) tab[s].start = atomicAdd(&a.cursor[2 * p + m], c);
+}
+
+__global__ void k_s2m_grid_scatter(S2MArgs a) {
+  const int p = blockIdx.y, m = blockIdx.z;
+  const S2MProb& st = a.prob[p];
+  const int n = m ? st.Ms : st.Mc;
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const float4 q = reinterpret_cast<const float4*>(m ? a.sm : a.cm)[(m ? st.ms0 : st.mc0) + k];
+  const int cap = m ? a.cap_ms : a.cap_mc;
+  const int2 w = (m ? a.where_s : a.where_c)[(size_t)p * cap + k];
+  const int log2T = m ? a.log2T_s : a.log2T_c;
+  const S2MSlot* tab = (m ? a.tab_s : a.tab_c) + ((size_t)p << log2T);
+  float4* dst = (m ? a.pts_s : a.pts_c) + (size_t)p * cap;
+  dst[tab[w.x].start + w.y] = make_float4(q.x, q.y, q.z, bitsf((uint32_t)k));
+}
+
+// Values reduced per block: AtA upper triangle (21), AtB (6), sum |coeff.intensity|, #corner,
+// #surf.
+constexpr int kRed = 30;
+
+__device__ void lm_step(const S2MArgs& a, S2MProb& st, const float* red) {
+  // LMOptimization (MO:1444-1570) after the Jacobian build.
+  st.iter += 1;
+  const int iterCount = st.iter - 1;
+  const int nc = (int)red[28], ns = (int)red[29];
+  st.nc = nc; st.ns = ns;
+  const int N = nc + ns;
+  bool conv = false;
+  if (N >= 50) {  // MO:1453
+    float AtA[36], AtB[6];
+    int q = 0;
+    for (int r = 0; r < 6; ++r)
+      for (int c = r; c < 6; ++c, ++q) { AtA[r + 6 * c] = red[q]; AtA[c + 6 * r] = red[q]; }
+    for (int c = 0; c < 6; ++c) AtB[c] = red[21 + c];
+    float X[6];
+    llsr_eigen::colpiv_qr_solve<6, 6>(AtA, AtB, X);
+    if (iterCount == 0) {
+      float E[6], V[36], V2[36];
+      llsr_eigen::eig_sym<6>(AtA, E, V);
+      st.min_lambda = E[0];
+      for (int k = 0; k < 36; ++k) V2[k] = V[k];
+      bool deg = false;
+      for (int i = 5; i >= 0; --i) {
+        if (E[i] < 100) {
+          for (int j = 0; j < 6; ++j) V2[i + 6 * j] = 0;
+          deg = true;
+        } else {
+          break;
+        }
+      }
+      st.degenerate = deg ? 1 : 0;
+      for (int r = 0; r < 6; ++r)  // matV.inverse() * matV2, V orthonormal: V^T * V2
+        for (int c = 0; c < 6; ++c) {
+          float acc = 0;
+          for (int k = 0; k < 6; ++k) acc += V[k + 6 * r] * V2[k + 6 * c];
+          st.matP[r + 6 * c] = acc;
+        }
+      for (int k = 0; k < 6; ++k) st.matX0[k] = X[k];
+    }
+    if (st.degenerate) {
+      float X2[6];
+      for (int k = 0; k < 6; ++k) X2[k] = X[k];
+      for (int r = 0; r < 6; ++r) {
+        float acc = 0;
+        for (int k = 0; k < 6; ++k) acc += st.matP[r + 6 * k] * X2[k];
+        X[r] = acc;
+      }
+    }
+    if (a.applied) {
+      for (int k = 0; k < 6; ++k) st.pose[k] += X[k];
+      st.cR = cosf_(st.pose[0]); st.sR = sinf_(st.pose[0]);
+      st.cP = cosf_(st.pose[1]); st.sP = sinf_(st.pose[1]);
+      st.cY = cosf_(st.pose[2]); st.sY = sinf_(st.pose[2]);
+    }
+    const float r2d = 57.29577951308232f;
+    const double e0 = (double)(X[0] * r2d), e1 = (double)(X[1] * r2d), e2 = (double)(X[2] * r2d);
+    const double t0 = (double)(X[3] * 100), t1 = (double)(X[4] * 100), t2 = (double)(X[5] * 100);
+    const float deltaR = (float)sqrt(e0 * e0 + e1 * e1 + e2 * e2);
+    const float deltaT = (float)sqrt(t0 * t0 + t1 * t1 + t2 * t2);
+    st.cf_mean = red[27] / (float)N;
+    conv = deltaR < a.stop_thres && deltaT < a.stop_thres;
+  }
+  if (conv) st.converged = 1;
+  if (conv || st.iter >= a.iter_max) {
+    st.active = 0;
+    atomicSub(a.n_active, 1);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_s2m_iter(S2MArgs a) {
+  const int p = blockIdx.y;
+  S2MProb& st = a.prob[p];
+  if (!st.active) return;
+  __shared__ float wsum[4][kRed];
+  __shared__ int is_last;
+  const int cb = a.blocks_c;
+  const bool corner = (int)blockIdx.x < cb;
+  const int qi = (corner ? blockIdx.x : blockIdx.x - cb) * 256 + threadIdx.x;
+  float v[kRed];
+#pragma unroll
+  for (int k = 0; k < kRed; ++k) v[k] = 0.0f;
+  const int Q = corner ? st.Qc : st.Qs;
+  if (qi < Q) {
+    const float4 q = reinterpret_cast<const float4*>(corner ? a.cq : a.sq)[(corner ? st.qc0 : st.qs0) + qi];
+    Assoc as{st.cR, st.sR, st.cP, st.sP, st.cY, st.sY, st.pose[3], st.pose[4], st.pose[5]};
+    float x0, y0, z0;
+    as.apply(q.x, q.y, q.z, x0, y0, z0);
+    float la, lb, lc, ld;
+    bool ok;
+    if (corner) {
+      const float4* mp = reinterpret_cast<const float4*>(a.cm) + st.mc0;
+      ok = corner_coeff(a.tab_c + ((size_t)p << a.log2T_c), a.log2T_c, a.pts_c + (size_t)p * a.cap_mc, mp,
+                        x0, y0, z0, la, lb, lc, ld);
+    } else {
+      const float4* mp = reinterpret_cast<const float4*>(a.sm) + st.ms0;
+      ok = surf_coeff(a.tab_s + ((size_t)p << a.log2T_s), a.log2T_s, a.pts_s + (size_t)p * a.cap_ms, mp,
+                      x0, y0, z0, la, lb, lc, ld);
+    }
+    if (ok) {
+      // Jacobian row (MO:1465-1490) at the current pose; srx.. are the same sin/cos values
+      const float srx = st.sR, crx = st.cR, sry = st.sP, cry = st.cP, srz = st.sY, crz = st.cY;
+      const float px = q.x, py = q.y, pz = q.z;
+      const float arx = (crx * sry * srz * px + crx * crz * sry * py - srx * sry * pz) * la +
+                        (-srx * srz * px - crz * srx * py - crx * pz) * lb +
+                        (crx * cry * srz * px + crx * cry * crz * py - cry * srx * pz) * lc;
+      const float ary = ((cry * srx * srz - crz * sry) * px + (sry * srz + cry * crz * srx) * py + crx * cry * pz) * la +
+                        ((-cry * crz - srx * sry * srz) * px + (cry * srz - crz * srx * sry) * py - crx * sry * pz) * lc;
+      const float arz = ((crz * srx * sry - cry * srz) * px + (-cry * crz - srx * sry * srz) * py) * la +
+                        (crx * crz * px - crx * srz * py) * lb +
+                        ((sry * srz + cry * crz * srx) * px + (crz * sry - cry * srx * srz) * py) * lc;
+      const float J[6] = {arx, ary, arz, la, lb, lc};
+      const float bb = -a.step_size * ld;
+      int k = 0;
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = r; c < 6; ++c, ++k) v[k] = J[r] * J[c];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) v[21 + c] = J[c] * bb;
+      v[27] = fabs_(ld);
+      v[corner ? 28 : 29] = 1.0f;
+    }
+  }
+  // fixed-order block reduction: wave butterfly, then waves 0..3 in order
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < kRed; ++k) {
+    const float s = wave_reduce_add(v[k]);
+    if (lane_id() == 0) wsum[w][k] = s;
+  }
+  __syncthreads();
+  float* part = a.partial + ((size_t)p * gridDim.x + blockIdx.x) * 32;
+  if (threadIdx.x < kRed) part[threadIdx.x] = ((wsum[0][threadIdx.x] + wsum[1][threadIdx.x]) + wsum[2][threadIdx.x]) + wsum[3][threadIdx.x];
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) is_last = atomicAdd(&st.ticket, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!is_last) return;
+  __threadfence();
+  __shared__ float red[32];
+  if (threadIdx.x < kRed) {
+    const volatile float* pp = a.partial + (size_t)p * gridDim.x * 32 + threadIdx.x;
+    float s = 0.0f;
+    for (unsigned b = 0; b < gridDim.x; ++b) s += pp[(size_t)b * 32];
+    red[threadIdx.x] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    st.ticket = 0u;
+    lm_step(a, st, red);
+  }
+}
+
+__global__ void k_s2m_finish(S2MArgs a) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.P) return;
+  const S2MProb& st = a.prob[p];
+  llsr_lm_report& r = a.report[p];
+  r.iterations = st.iter;
+  r.converged = st.converged;
+  r.degenerate = st.degenerate;
+  r.min_lambda = st.min_lambda;
+  r.cf_mean = st.cf_mean;
+  r.n_corner_corr = st.nc;
+  r.n_surf_corr = st.ns;
+  for (int k = 0; k < 6; ++k) {
+    r.matX0[k] = st.matX0[k];
+    r.pose[k] = st.pose[k];
+    a.pose[6 * p + k] = st.pose[k];
+  }
+  r.ms = 0.0f;
+}
+
+}  // namespace llsr

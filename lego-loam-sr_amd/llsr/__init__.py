@@ -6,6 +6,8 @@ Mirrors the reference's node-level interface for this path:
   -> a ProjectionOut-like dict (segmented / outlier clouds + CloudInfo fields).
 * `FeatureAssociation.extract(...)` ~ the feature stage of runFeatureAssociation
   (featureAssociation.cpp:2766-2775).
+* `MapOptimization.scan2map_optimization(...)` ~ MapOptimization::scan2MapOptimization
+  (mapOptmization.cpp:1572-1610): kNN-5 correspondences + the 6x6 LM against a local map.
 * `Pipeline.process_scan` runs both for one scan; `Pipeline.process_batch` runs B scans that are
   already resident in HBM (device pointers, e.g. from torch tensors).
 
@@ -31,6 +33,7 @@ EXPORTS = [
     "llsr_config_default", "llsr_create", "llsr_destroy", "llsr_last_error", "llsr_query_sizes",
     "llsr_reset_state", "llsr_process_scan", "llsr_process_batch", "llsr_fetch_scan",
     "llsr_batch_counts", "llsr_kernel_times_ms", "llsr_kernel_name", "llsr_set_profiling",
+    "llsr_scan2map_reserve", "llsr_scan2map_batch", "llsr_scan2map",
 ]
 
 
@@ -61,6 +64,10 @@ def lib():
         L.llsr_kernel_name.restype = C.c_char_p
         L.llsr_kernel_name.argtypes = [C.c_int32]
         L.llsr_set_profiling.argtypes = [C.c_void_p, C.c_int32]
+        L.llsr_scan2map_reserve.argtypes = [C.c_void_p] + [C.c_int32] * 5
+        L.llsr_scan2map_batch.argtypes = [C.c_void_p, C.POINTER(_abi.S2MBatch), C.c_void_p]
+        L.llsr_scan2map.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p,
+                                    C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(_abi.LmReport)]
         for fn in EXPORTS:
             if fn not in ("llsr_last_error", "llsr_kernel_name", "llsr_destroy"):
                 getattr(L, fn).restype = C.c_int32
@@ -144,6 +151,47 @@ class Pipeline:
         if n < 0:
             self._check(n, "llsr_kernel_times_ms")
         return {lib().llsr_kernel_name(k).decode(): float(buf[k]) for k in range(n)}
+
+
+    # ---- scan-to-map (MapOptimization) -------------------------------------------------------
+    def scan2map_reserve(self, problems: int, corner_map: int, surf_map: int, corner_q: int, surf_q: int):
+        self._check(lib().llsr_scan2map_reserve(self._h, problems, corner_map, surf_map, corner_q, surf_q),
+                    "llsr_scan2map_reserve")
+
+    def scan2map(self, corner_q, surf_q, corner_map, surf_map, pose) -> dict:
+        """One problem from host arrays ((n, 4) float32 clouds, pose[6]); returns the report."""
+        arrs = [np.ascontiguousarray(a, dtype=np.float32).reshape(-1, 4) for a in (corner_q, surf_q, corner_map, surf_map)]
+        pose = np.ascontiguousarray(pose, dtype=np.float32).copy()
+        rep = _abi.LmReport()
+        args = []
+        for a in arrs:
+            args += [C.c_void_p(a.ctypes.data if len(a) else None), len(a)]
+        self._check(lib().llsr_scan2map(self._h, *args, pose.ctypes.data, C.byref(rep)), "llsr_scan2map")
+        d = rep.as_dict()
+        d["pose"] = pose
+        return d
+
+    def scan2map_batch(self, ptrs: dict, P: int, stream: int = 0):
+        """Device-resident batch: ptrs maps the llsr_s2m_batch field names to device pointers."""
+        b = _abi.S2MBatch()
+        b.n_problems = P
+        for k, v in ptrs.items():
+            setattr(b, k, v)
+        self._check(lib().llsr_scan2map_batch(self._h, C.byref(b), C.c_void_p(stream)), "llsr_scan2map_batch")
+
+
+class MapOptimization:
+    """Drop-in for MapOptimization::scan2MapOptimization's arithmetic (MO:1572-1610)."""
+
+    def __init__(self, pipeline: Pipeline):
+        self.p = pipeline
+
+    def scan2map_optimization(self, laser_cloud_corner_scan_ds, laser_cloud_surf_total_last_ds,
+                              laser_cloud_corner_from_map_ds, laser_cloud_surf_from_map_ds,
+                              transform_tobe_mapped) -> dict:
+        return self.p.scan2map(laser_cloud_corner_scan_ds, laser_cloud_surf_total_last_ds,
+                               laser_cloud_corner_from_map_ds, laser_cloud_surf_from_map_ds,
+                               transform_tobe_mapped)
 
 
 class ImageProjection:

@@ -136,6 +136,19 @@ class LmReport(C.Structure):
         return d
 
 
+class S2MBatch(C.Structure):
+    """llsr_s2m_batch (include/llsr.h): device pointers of one scan-to-map batch."""
+    _fields_ = [
+        ("n_problems", C.c_int32),
+        ("corner_q", C.c_void_p), ("corner_q_off", C.c_void_p),
+        ("surf_q", C.c_void_p), ("surf_q_off", C.c_void_p),
+        ("corner_map", C.c_void_p), ("corner_map_off", C.c_void_p),
+        ("surf_map", C.c_void_p), ("surf_map_off", C.c_void_p),
+        ("pose", C.c_void_p),
+        ("report", C.c_void_p),
+    ]
+
+
 class Sizes(C.Structure):
     _fields_ = [("cells", C.c_int32), ("rings", C.c_int32), ("max_points", C.c_int32),
                 ("shadow_points", C.c_int32)]

@@ -17,7 +17,7 @@ HEADER = os.path.join(REPO, "include", "llsr.h")
 
 def _declared():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"\b(llsr_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(llsr_\w+)\s*\(", text)))
 
 
 def test_header_declares_expected_surface():

@@ -1,0 +1,175 @@
+"""GPU parity of the scan-to-map LM (MapOptimization::scan2MapOptimization, MO:1572-1610).
+
+HIP path through the C-ABI (llsr_scan2map / llsr_scan2map_batch) against the oracle
+(oracle/oracle_mo.cpp) on the committed ~76k-point map fixture (tests/golden/make_mo_fixture.py).
+
+The bar:
+  * correspondences are bit-exact — checked where the pose is identical on both sides:
+    faithful mode (the reference's commented-out update, MO:1539-1545) evaluates every
+    iteration at the input pose, so the corner / surf correspondence counts must be equal;
+  * the normal equations are summed in a different order (block tree vs the reference's Eigen
+    GEMM / the oracle's sequential sum), so matX / min_lambda / cf_mean are compared with a
+    relative tolerance of 1e-4 and the final pose with north_star's 1e-4 absolute.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py
+from llsr import Pipeline, _abi, default_config
+
+pytestmark = pytest.mark.gpu
+
+FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mo_map_vlp16.npz")
+POSE_TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def fix():
+    return np.load(FIX)
+
+
+def _cfg(mode):
+    cfg = default_config("vlp16")
+    cfg.mode = mode
+    return cfg
+
+
+def _inputs(fix, i):
+    return fix[f"q{i}_corner"], fix[f"q{i}_surf"], fix["corner_map"], fix["surf_map"], fix[f"q{i}_init"]
+
+
+def _close(a, b, rel=1e-4, atol=1e-6):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.all(np.abs(a - b) <= atol + rel * np.abs(b))
+
+
+@pytest.mark.parametrize("mode", [_abi.LLSR_MODE_LM_APPLIED, _abi.LLSR_MODE_FAITHFUL])
+def test_scan2map_matches_oracle(require_gpu, fix, mode):
+    cfg = _cfg(mode)
+    pipe = Pipeline(cfg)
+    errs = []
+    queries = range(int(fix["n_queries"])) if mode == _abi.LLSR_MODE_LM_APPLIED else [0, 2]
+    for i in queries:
+        args = _inputs(fix, i)
+        g = pipe.scan2map(*args)
+        o = oracle_py.scan2map(cfg, *args)
+        tag = f"query {i} mode {mode}"
+        if np.abs(g["pose"] - o["pose"]).max() > POSE_TOL:
+            errs.append(f"{tag}: pose {g['pose']} vs {o['pose']}")
+        for k in ("converged", "degenerate"):
+            if g[k] != o[k]:
+                errs.append(f"{tag}: {k} {g[k]} vs {o[k]}")
+        if abs(g["iterations"] - o["iterations"]) > (0 if mode == _abi.LLSR_MODE_FAITHFUL else 1):
+            errs.append(f"{tag}: iterations {g['iterations']} vs {o['iterations']}")
+        if not _close(g["matX0"], o["matX0"], atol=1e-6):
+            errs.append(f"{tag}: matX0 {g['matX0']} vs {o['matX0']}")
+        if not _close(g["min_lambda"], o["min_lambda"]):
+            errs.append(f"{tag}: min_lambda {g['min_lambda']} vs {o['min_lambda']}")
+        if not _close(g["cf_mean"], o["cf_mean"]):
+            errs.append(f"{tag}: cf_mean {g['cf_mean']} vs {o['cf_mean']}")
+        if mode == _abi.LLSR_MODE_FAITHFUL:
+            np.testing.assert_array_equal(g["pose"], args[4])
+            if (g["n_corner_corr"], g["n_surf_corr"]) != (o["n_corner_corr"], o["n_surf_corr"]):
+                errs.append(f"{tag}: correspondences {g['n_corner_corr']}/{g['n_surf_corr']} vs "
+                            f"{o['n_corner_corr']}/{o['n_surf_corr']}")
+        elif abs(g["n_corner_corr"] - o["n_corner_corr"]) + abs(g["n_surf_corr"] - o["n_surf_corr"]) > 2:
+            errs.append(f"{tag}: correspondences {g['n_corner_corr']}/{g['n_surf_corr']} vs "
+                        f"{o['n_corner_corr']}/{o['n_surf_corr']}")
+    pipe.close()
+    assert not errs, "\n".join(errs)
+
+
+def test_scan2map_batch_matches_single(require_gpu, fix):
+    """Device-resident batch of ragged problems == the oracle per problem."""
+    import torch
+    cfg = _cfg(_abi.LLSR_MODE_LM_APPLIED)
+    nq = int(fix["n_queries"])
+    probs = []
+    for p in range(6):
+        cq, sq, cm, sm, pose = _inputs(fix, p % nq)
+        if p >= nq:  # ragged: fewer queries, a cropped map, another start pose
+            cq, sq, cm, sm = cq[: len(cq) // 2], sq[: 2 * len(sq) // 3], cm[: 3 * len(cm) // 4], sm
+            pose = pose + np.float32(0.01)
+        probs.append((cq, sq, cm, sm, pose.astype(np.float32)))
+
+    def pack(k):
+        arrs = [pr[k] for pr in probs]
+        off = np.zeros(len(arrs) + 1, np.int64)
+        off[1:] = np.cumsum([len(a) for a in arrs])
+        return torch.from_numpy(np.concatenate(arrs)).cuda(), torch.from_numpy(off).cuda()
+
+    P = len(probs)
+    (cq, cqo), (sq, sqo), (cm, cmo), (sm, smo) = (pack(k) for k in range(4))
+    pose = torch.from_numpy(np.stack([pr[4] for pr in probs])).cuda()
+    rep = torch.zeros(P * C_sizeof_report() // 4, dtype=torch.float32, device="cuda")
+    pipe = Pipeline(cfg)
+    pipe.scan2map_reserve(P, max(len(pr[2]) for pr in probs), max(len(pr[3]) for pr in probs),
+                          max(len(pr[0]) for pr in probs), max(len(pr[1]) for pr in probs))
+    torch.cuda.synchronize()
+    pipe.scan2map_batch(dict(corner_q=cq.data_ptr(), corner_q_off=cqo.data_ptr(), surf_q=sq.data_ptr(),
+                             surf_q_off=sqo.data_ptr(), corner_map=cm.data_ptr(), corner_map_off=cmo.data_ptr(),
+                             surf_map=sm.data_ptr(), surf_map_off=smo.data_ptr(), pose=pose.data_ptr(),
+                             report=rep.data_ptr()), P)
+    torch.cuda.synchronize()
+    poses = pose.cpu().numpy()
+    reps = _reports(rep.cpu().numpy(), P)
+    pipe.close()
+    for p, pr in enumerate(probs):
+        o = oracle_py.scan2map(cfg, *pr)
+        assert np.abs(poses[p] - o["pose"]).max() <= POSE_TOL, (p, poses[p], o["pose"])
+        np.testing.assert_array_equal(reps[p].pose[:], poses[p])
+        assert abs(reps[p].iterations - o["iterations"]) <= 1 and reps[p].converged == o["converged"], p
+
+
+def C_sizeof_report():
+    import ctypes
+    return ctypes.sizeof(_abi.LmReport)
+
+
+def _reports(buf, P):
+    import ctypes
+    raw = buf.tobytes()
+    n = ctypes.sizeof(_abi.LmReport)
+    return [_abi.LmReport.from_buffer_copy(raw[p * n:(p + 1) * n]) for p in range(P)]
+
+
+def test_scan2map_guard_and_empty(require_gpu, fix):
+    cfg = _cfg(_abi.LLSR_MODE_LM_APPLIED)
+    pipe = Pipeline(cfg)
+    cq, sq, cm, sm, pose = _inputs(fix, 0)
+    # MO:1573 guard: <= 10 corner map points -> no optimisation, pose untouched
+    g = pipe.scan2map(cq, sq, cm[:10], sm, pose)
+    assert g["iterations"] == 0 and np.array_equal(g["pose"], pose)
+    # no queries at all: every iteration has < 50 correspondences -> iterCountThres, no update
+    g = pipe.scan2map(cq[:0], sq[:0], cm, sm, pose)
+    o = oracle_py.scan2map(cfg, cq[:0], sq[:0], cm, sm, pose)
+    assert g["iterations"] == o["iterations"] == cfg.iterCountThres
+    assert np.array_equal(g["pose"], pose) and not g["converged"]
+    # corners only
+    g = pipe.scan2map(cq, sq[:0], cm, sm, pose)
+    o = oracle_py.scan2map(cfg, cq, sq[:0], cm, sm, pose)
+    assert np.abs(g["pose"] - o["pose"]).max() <= POSE_TOL and g["iterations"] == o["iterations"]
+    pipe.close()
+
+
+def test_scan2map_capacity_error(require_gpu, fix):
+    import torch
+    from llsr import LlsrError
+    cfg = _cfg(_abi.LLSR_MODE_LM_APPLIED)
+    cq, sq, cm, sm, pose = _inputs(fix, 0)
+    pipe = Pipeline(cfg)
+    pipe.scan2map_reserve(1, 100, 100, 10, 10)
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in
+         dict(cq=cq, sq=sq, cm=cm, sm=sm, pose=pose[None]).items()}
+    offs = {k: torch.tensor([0, len(v)], dtype=torch.int64).cuda() for k, v in dict(cq=cq, sq=sq, cm=cm, sm=sm).items()}
+    rep = torch.zeros(64, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    with pytest.raises(LlsrError):
+        pipe.scan2map_batch(dict(corner_q=t["cq"].data_ptr(), corner_q_off=offs["cq"].data_ptr(),
+                                 surf_q=t["sq"].data_ptr(), surf_q_off=offs["sq"].data_ptr(),
+                                 corner_map=t["cm"].data_ptr(), corner_map_off=offs["cm"].data_ptr(),
+                                 surf_map=t["sm"].data_ptr(), surf_map_off=offs["sm"].data_ptr(),
+                                 pose=t["pose"].data_ptr(), report=rep.data_ptr()), 1)
+    pipe.close()
