@@ -37,6 +37,10 @@ int32_t oracle_ransac_inliers(oracle_state* s, uint32_t seed, int32_t* inliers, 
 int32_t oracle_scan2map(const llsr_config* cfg, const float* corner_q, int32_t Qc, const float* surf_q,
                         int32_t Qs, const float* corner_map, int32_t Mc, const float* surf_map, int32_t Ms,
                         float* pose, llsr_lm_report* rep);
+/* kNN-5 (d^2 < 1.0 accepted) of Q float4 queries in a float4 map: idx/d2 [Q][5], -1 = rejected.
+ * liboracle: the 1 m grid; oracle/_ref/libref_mo.so exports the same as ref_knn5_batch /
+ * ref_scan2map over the reference's nanoflann kd-tree. */
+int32_t oracle_knn5_batch(const float* map, int32_t M, const float* q, int32_t Q, int32_t* idx, float* d2);
 /* Test hooks for the Eigen restatements (llsr_eigen.h): column-major inputs. */
 int32_t oracle_eig3(const float* A, float* evals, float* evecs);
 int32_t oracle_eig6(const float* A, float* evals, float* evecs);

@@ -7,8 +7,14 @@
 // kNN-5 (nanoflann KdTreeFLANN::nearestKSearch, eps 0, sorted) is restated exactly where it can
 // matter: a correspondence is kept only when the 5th nearest squared distance is < 1.0, so the
 // search is a 1 m uniform grid over the 27 neighbouring cells; squared distances accumulate as
-// ((0 + dx^2) + dy^2) + dz^2 (nanoflann.hpp:431-439) and equal distances keep the first found
-// (KNNResultSet::addPoint strict '<'). Eigen calls use lego-loam-sr_amd/csrc/llsr_eigen.h.
+// ((0 + dx^2) + dy^2) + dz^2 (nanoflann.hpp:431-439, L2_Simple_Adaptor behind the SO3_Adaptor of
+// nanoflann_pcl.h) and equal distances keep the lower index. Eigen calls use
+// lego-loam-sr_amd/csrc/llsr_eigen.h.
+//
+// Built a second time by oracle/Makefile with -DLLSR_ORACLE_NANOFLANN against the reference's
+// own vendored kd-tree (LeGO-LOAM/include/lego_loam/nanoflann.hpp, included by path, std-only;
+// output oracle/_ref/libref_mo.so, never committed): the same restatement with the reference's
+// kNN, used to cross-check the grid (tests/test_mo_oracle.py) and as the MO CPU baseline.
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -19,6 +25,9 @@
 #include "../include/llsr.h"
 #include "../lego-loam-sr_amd/csrc/llsr_eigen.h"
 #include "oracle.h"
+#ifdef LLSR_ORACLE_NANOFLANN
+#include "nanoflann.hpp"
+#endif
 
 namespace {
 
@@ -67,11 +76,47 @@ struct Grid {
   }
 };
 
+#ifdef LLSR_ORACLE_NANOFLANN
+// KdTreeFLANN<PointType> of nanoflann_pcl.h: KDTreeSingleIndexAdaptor<SO3_Adaptor<float, .>, ., 3,
+// int>, leaf size 10, nearestKSearch = KNNResultSet<float, int>(k) + findNeighbors(SearchParams())
+struct CloudAdaptor {
+  const P4* pts = nullptr;
+  size_t n = 0;
+  size_t kdtree_get_point_count() const { return n; }
+  float kdtree_get_pt(const size_t idx, int dim) const { return (&pts[idx].x)[dim]; }
+  template <class BBOX> bool kdtree_get_bbox(BBOX&) const { return false; }
+};
+using KdTree = nanoflann::KDTreeSingleIndexAdaptor<nanoflann::SO3_Adaptor<float, CloudAdaptor>, CloudAdaptor, 3, int>;
+struct Knn {
+  CloudAdaptor ad;
+  KdTree* tree = nullptr;
+  ~Knn() { delete tree; }
+  void build(const P4* p, int np) {
+    ad.pts = p;
+    ad.n = (size_t)np;
+    delete tree;
+    tree = new KdTree(3, ad);
+    tree->buildIndex();
+  }
+  // same contract as Grid::knn5: 5 when the five nearest all have d^2 < 1.0
+  int knn5(const P4& q, int* idx, float* d2) const {
+    nanoflann::KNNResultSet<float, int> rs(5);
+    rs.init(idx, d2);
+    tree->findNeighbors(rs, &q.x, nanoflann::SearchParams());
+    return (rs.size() == 5 && d2[4] < 1.0f) ? 5 : 0;
+  }
+};
+#define ORACLE_FN(name) ref_##name
+#else
+using Knn = Grid;
+#define ORACLE_FN(name) oracle_##name
+#endif
+
 struct Coeff { P4 ori; float cx, cy, cz, ci; };
 
 }  // namespace
 
-extern "C" int32_t oracle_scan2map(const llsr_config* cfg, const float* cq, int32_t Qc, const float* sq,
+extern "C" int32_t ORACLE_FN(scan2map)(const llsr_config* cfg, const float* cq, int32_t Qc, const float* sq,
                                    int32_t Qs, const float* cm, int32_t Mc, const float* sm, int32_t Ms,
                                    float* pose, llsr_lm_report* rep) {
   if (!cfg || !pose || !rep || Qc < 0 || Qs < 0 || Mc < 0 || Ms < 0) return LLSR_EINVAL;
@@ -88,7 +133,7 @@ extern "C" int32_t oracle_scan2map(const llsr_config* cfg, const float* cq, int3
     return LLSR_OK;
   }
   auto t0 = std::chrono::steady_clock::now();
-  Grid gc, gs;
+  Knn gc, gs;
   gc.build(cornerM, Mc);
   gs.build(surfM, Ms);
   const bool applied = cfg->mode == LLSR_MODE_LM_APPLIED;
@@ -266,7 +311,26 @@ extern "C" int32_t oracle_scan2map(const llsr_config* cfg, const float* cq, int3
   return LLSR_OK;
 }
 
+// kNN-5 of Q queries against one map (cross-check hook): idx/d2 [Q][5]; returns #accepted and
+// writes -1 indices for rejected queries.
+extern "C" int32_t ORACLE_FN(knn5_batch)(const float* map, int32_t M, const float* q, int32_t Q, int32_t* idx,
+                                         float* d2) {
+  Knn k;
+  k.build(reinterpret_cast<const P4*>(map), M);
+  int acc = 0;
+  for (int i = 0; i < Q; ++i) {
+    if (k.knn5(reinterpret_cast<const P4*>(q)[i], idx + 5 * i, d2 + 5 * i) == 5) {
+      ++acc;
+    } else {
+      for (int j = 0; j < 5; ++j) { idx[5 * i + j] = -1; d2[5 * i + j] = 0.0f; }
+    }
+  }
+  return acc;
+}
+
+#ifndef LLSR_ORACLE_NANOFLANN
 extern "C" int32_t oracle_eig3(const float* A, float* e, float* v) { return llsr_eigen::eig3(A, e, v); }
 extern "C" int32_t oracle_eig6(const float* A, float* e, float* v) { return llsr_eigen::eig_sym<6>(A, e, v); }
 extern "C" void oracle_qr_solve_5x3(const float* A, const float* b, float* x) { llsr_eigen::colpiv_qr_solve<5, 3>(A, b, x); }
 extern "C" void oracle_qr_solve_6x6(const float* A, const float* b, float* x) { llsr_eigen::colpiv_qr_solve<6, 6>(A, b, x); }
+#endif

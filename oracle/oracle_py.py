@@ -42,17 +42,45 @@ def lib():
         L.oracle_stage_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.oracle_ransac_inliers.restype = C.c_int32
         L.oracle_ransac_inliers.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int32]
-        L.oracle_scan2map.restype = C.c_int32
-        L.oracle_scan2map.argtypes = [C.POINTER(_abi.Config), C.c_void_p, C.c_int32, C.c_void_p, C.c_int32,
-                                      C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p,
-                                      C.POINTER(_abi.LmReport)]
         for f in ("oracle_eig3", "oracle_eig6"):
             getattr(L, f).restype = C.c_int32
             getattr(L, f).argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         for f in ("oracle_qr_solve_5x3", "oracle_qr_solve_6x6"):
             getattr(L, f).argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        _bind_mo(L, "oracle_")
         _LIB = L
     return _LIB
+
+
+def _bind_mo(L, prefix):
+    f = getattr(L, prefix + "scan2map")
+    f.restype = C.c_int32
+    f.argtypes = [C.POINTER(_abi.Config), C.c_void_p, C.c_int32, C.c_void_p, C.c_int32,
+                  C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(_abi.LmReport)]
+    f = getattr(L, prefix + "knn5_batch")
+    f.restype = C.c_int32
+    f.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+
+
+_REF = None
+REF_PATH = os.path.join(_HERE, "_ref", "libref_mo.so")
+REF_SRC = "/root/reference/LeGO-LOAM/include/lego_loam/nanoflann.hpp"
+
+
+def ref_lib():
+    """oracle/_ref/libref_mo.so: the MO restatement over the reference's own nanoflann kd-tree.
+    Built from /root/reference when that exists (build container); elsewhere only the prebuilt
+    copy can be used. Returns None when neither is available."""
+    global _REF
+    if _REF is None:
+        if os.path.exists(REF_SRC):
+            subprocess.run(["make", "-s", "-C", _HERE, "ref"], check=True)
+        if not os.path.exists(REF_PATH):
+            return None
+        L = C.CDLL(REF_PATH)
+        _bind_mo(L, "ref_")
+        _REF = L
+    return _REF
 
 
 class Oracle:
@@ -99,20 +127,41 @@ def _f4(a) -> np.ndarray:
     return a
 
 
-def scan2map(cfg: _abi.Config, corner_q, surf_q, corner_map, surf_map, pose0) -> dict:
+def _mo_fn(name, knn):
+    if knn == "grid":
+        return getattr(lib(), "oracle_" + name)
+    if knn == "kdtree":
+        L = ref_lib()
+        if L is None:
+            raise FileNotFoundError(f"{REF_PATH} not built (needs {REF_SRC})")
+        return getattr(L, "ref_" + name)
+    raise ValueError(knn)
+
+
+def scan2map(cfg: _abi.Config, corner_q, surf_q, corner_map, surf_map, pose0, knn: str = "grid") -> dict:
     """MapOptimization::scan2MapOptimization (MO:1572-1610) on explicit clouds; returns the
-    report dict (pose = final transformTobeMapped)."""
+    report dict (pose = final transformTobeMapped). knn: "grid" (self-contained restatement)
+    or "kdtree" (the reference's nanoflann, oracle/_ref)."""
     cq, sq, cm, sm = (_f4(a) for a in (corner_q, surf_q, corner_map, surf_map))
     pose = np.ascontiguousarray(pose0, dtype=np.float32).copy()
     rep = _abi.LmReport()
-    rc = lib().oracle_scan2map(C.byref(cfg), cq.ctypes.data, len(cq), sq.ctypes.data, len(sq),
-                               cm.ctypes.data, len(cm), sm.ctypes.data, len(sm), pose.ctypes.data,
-                               C.byref(rep))
+    rc = _mo_fn("scan2map", knn)(C.byref(cfg), cq.ctypes.data, len(cq), sq.ctypes.data, len(sq),
+                                 cm.ctypes.data, len(cm), sm.ctypes.data, len(sm), pose.ctypes.data,
+                                 C.byref(rep))
     if rc != 0:
         raise RuntimeError(f"oracle_scan2map: {rc}")
     d = rep.as_dict()
     d["pose"] = pose
     return d
+
+
+def knn5(map_pts, queries, knn: str = "grid"):
+    """kNN-5 with the MO acceptance (5th d^2 < 1.0): (idx [Q,5] with -1 rows = rejected, d2)."""
+    m, q = _f4(map_pts), _f4(queries)
+    idx = np.zeros((len(q), 5), np.int32)
+    d2 = np.zeros((len(q), 5), np.float32)
+    _mo_fn("knn5_batch", knn)(m.ctypes.data, len(m), q.ctypes.data, len(q), idx.ctypes.data, d2.ctypes.data)
+    return idx, d2
 
 
 def eig(A: np.ndarray):

@@ -111,3 +111,37 @@ def test_empty_map_is_a_no_op(fix):
                            fix["surf_map"], fix["q0_init"])
     np.testing.assert_array_equal(r["pose"], fix["q0_init"])
     assert r["iterations"] == 0
+
+
+def _need_ref():
+    if oracle_py.ref_lib() is None:
+        pytest.skip("oracle/_ref/libref_mo.so not built (needs /root/reference)")
+
+
+@pytest.mark.parametrize("which", ["corner_map", "surf_map"])
+def test_grid_knn_equals_reference_kdtree(fix, which):
+    """The restatement's 1 m grid == the reference's nanoflann kd-tree (nanoflann_pcl.h:
+    SO3_Adaptor over L2_Simple, leaf 10), index for index and bit for bit in d^2."""
+    _need_ref()
+    m = fix[which]
+    rng = np.random.default_rng(11)
+    q = m[rng.integers(0, len(m), 20000)].copy()
+    q[:, :3] += rng.normal(0.0, 0.3, (len(q), 3)).astype(np.float32)
+    ig, dg = oracle_py.knn5(m, q, "grid")
+    ik, dk = oracle_py.knn5(m, q, "kdtree")
+    assert (ig[:, 0] >= 0).sum() > 10000
+    np.testing.assert_array_equal(ig, ik)
+    np.testing.assert_array_equal(dg, dk)
+
+
+@pytest.mark.parametrize("mode", [_abi.LLSR_MODE_LM_APPLIED, _abi.LLSR_MODE_FAITHFUL])
+def test_scan2map_grid_equals_reference_kdtree(fix, mode):
+    _need_ref()
+    cfg = _abi.config_for("vlp16")
+    cfg.mode = mode
+    args = (fix["q1_corner"], fix["q1_surf"], fix["corner_map"], fix["surf_map"], fix["q1_init"])
+    rg = oracle_py.scan2map(cfg, *args)
+    rk = oracle_py.scan2map(cfg, *args, knn="kdtree")
+    for k in rg:
+        if k != "ms":
+            np.testing.assert_array_equal(np.asarray(rg[k]), np.asarray(rk[k]), err_msg=k)
