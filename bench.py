@@ -5,6 +5,11 @@ cluster segmentation (ImageProjection) + curvature / feature extraction (Feature
 feature stage), labels / feature indices bit-exact vs the CPU path. A "step" is one pass of the
 hot path over one batch of B scans per GPU that is already resident in HBM.
 
+The same JSON line carries a second measured leg, "scan2map" (BASELINE.json configs[2]): batches
+of P scan-to-map problems (MapOptimization::scan2MapOptimization) against the ~76k-point local
+map of tests/golden/mo_map_vlp16.npz, in lm_applied and faithful (200-iteration) mode, with the
+pose delta against the CPU restatement and its own CPU baseline.
+
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
 
 N > 1 is launched by torch.distributed.run (one rank per GPU). Scans are batch-sharded: every
@@ -74,6 +79,143 @@ def cpu_baseline(scans: list[np.ndarray], budget_s: float) -> dict:
             "ip_ms": ip_ms / n, "fa_features_ms": fa_ms / n}
 
 
+def s2m_bytes_per_iteration(Qc: int, Qs: int, blocks: int) -> float:
+    """query 16 B + 5 neighbours x 16 B per query, 29 partial words per block."""
+    return 96.0 * (Qc + Qs) + 116.0 * blocks
+
+
+def scan2map_leg(dev, mode_name: str, P: int, steps: int, warmup: int, dist, run_cpu: bool,
+                 cpu_seconds: float) -> dict:
+    """Config 3: P independent scan-to-map problems per step; each problem carries its own copy of
+    the local map (its kd-tree/grid is rebuilt every step, as MO rebuilds it every scan,
+    MO:1575-1576), one of the fixture's query scans and its own seeded start pose."""
+    import torch
+    from llsr import Pipeline, _abi, default_config
+    z = np.load(os.path.join(REPO, "tests", "golden", "mo_map_vlp16.npz"))
+    nq = int(z["n_queries"])
+    mode = {"lm_applied": _abi.LLSR_MODE_LM_APPLIED, "faithful": _abi.LLSR_MODE_FAITHFUL}[mode_name]
+    cfg = default_config("vlp16")
+    cfg.mode = mode
+    cm, sm = z["corner_map"], z["surf_map"]
+    rng = np.random.default_rng(99)
+    probs = []
+    for p in range(P):
+        q = p % nq
+        pose = z[f"q{q}_true"] + np.concatenate([rng.uniform(-0.05, 0.05, 3), rng.uniform(-0.2, 0.2, 3)])
+        probs.append((z[f"q{q}_corner"], z[f"q{q}_surf"], cm, sm, pose.astype(np.float32)))
+
+    def pack(k):
+        arrs = [pr[k] for pr in probs]
+        off = np.zeros(P + 1, np.int64)
+        off[1:] = np.cumsum([len(a) for a in arrs])
+        return torch.from_numpy(np.concatenate(arrs)).to(dev), torch.from_numpy(off).to(dev)
+
+    (cq, cqo), (sq, sqo), (dcm, cmo), (dsm, smo) = (pack(k) for k in range(4))
+    pose0 = torch.from_numpy(np.stack([pr[4] for pr in probs])).to(dev)
+    pose = pose0.clone()
+    rep = torch.zeros((P, ctypes_sizeof_report() // 4), dtype=torch.float32, device=dev)
+    pipe = Pipeline(cfg, device=dev)
+    Qc = max(len(pr[0]) for pr in probs)
+    Qs = max(len(pr[1]) for pr in probs)
+    pipe.scan2map_reserve(P, len(cm), len(sm), Qc, Qs)
+    ptrs = dict(corner_q=cq.data_ptr(), corner_q_off=cqo.data_ptr(), surf_q=sq.data_ptr(),
+                surf_q_off=sqo.data_ptr(), corner_map=dcm.data_ptr(), corner_map_off=cmo.data_ptr(),
+                surf_map=dsm.data_ptr(), surf_map_off=smo.data_ptr(), pose=pose.data_ptr(),
+                report=rep.data_ptr())
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        pose.copy_(pose0)  # every step solves the same P problems from their start poses
+        pipe.scan2map_batch(ptrs, P, stream.cuda_stream)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    pipe.set_profiling(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    st = pipe.scan2map_stats()
+    pipe.set_profiling(False)
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    world = dist.get_world_size() if dist else 1
+    from llsr import _abi as abi_
+    raw = rep.cpu().numpy().tobytes()
+    n = ctypes_sizeof_report()
+    reps = [abi_.LmReport.from_buffer_copy(raw[p * n:(p + 1) * n]) for p in range(P)]
+    iters = np.array([r.iterations for r in reps], np.float64)
+    poses = pose.cpu().numpy()
+    blocks = (Qc + 255) // 256 + (Qs + 255) // 256
+    lm_bytes = sum(r.iterations * s2m_bytes_per_iteration(len(pr[0]), len(pr[1]), blocks)
+                   for r, pr in zip(reps, probs))
+    per_launch_ms = st["iterate_ms"] / max(1, st["iteration_launches"])
+    launches_per_batch = st["iteration_launches"] / max(1, st["batches"])
+    achieved = lm_bytes / (st["iterate_ms"] / max(1, st["batches"]) * 1e-3) / 1e9
+    out = {
+        "workload": "configs[2]: scan-to-map LM (corner/surf kNN-5 correspondences + 6x6 normal "
+                    f"equations + solve) against a {len(cm) + len(sm)}-point local map, mode {mode_name}",
+        "value": round(P * steps * world / el, 1), "unit": "scan-to-map problems/s",
+        "problems_per_gpu_per_step": P, "steps": steps, "ms_per_step": round(el / steps * 1e3, 3),
+        "map_points": {"corner": len(cm), "surf": len(sm)},
+        "queries_per_problem": {"corner": float(np.mean([len(pr[0]) for pr in probs])),
+                                "surf": float(np.mean([len(pr[1]) for pr in probs]))},
+        "iterations_mean": float(iters.mean()), "iterations_max": int(iters.max()),
+        "converged_frac": float(np.mean([r.converged for r in reps])),
+        "grid_build_ms_per_step": round(st["grid_ms"] / max(1, st["batches"]), 4),
+        "iterate_ms_per_step": round(st["iterate_ms"] / max(1, st["batches"]), 4),
+        "k_s2m_iter_launches_per_step": launches_per_batch,
+        "roofline": {"bound": "hbm", "kernel": "k_s2m_iter", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None, "algorithmic_bytes_per_step": lm_bytes,
+                     "avg_launch_ms": round(per_launch_ms, 4),
+                     "note": "iterate window includes the host's convergence polls (every 4 launches)"},
+    }
+    if run_cpu:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle_py
+        knn = "kdtree" if oracle_py.ref_lib() is not None else "grid"
+        ncheck = min(P, nq if mode_name == "lm_applied" else 2)
+        deltas = []
+        t_cpu, n_cpu = 0.0, 0
+        for p in range(ncheck):
+            o = oracle_py.scan2map(cfg, *probs[p], knn=knn)
+            deltas.append(float(np.abs(poses[p] - o["pose"]).max()))
+            t_cpu += o["ms"] * 1e-3
+            n_cpu += 1
+        p = ncheck
+        while t_cpu < cpu_seconds and n_cpu < 10000:
+            o = oracle_py.scan2map(cfg, *probs[p % P], knn=knn)
+            t_cpu += o["ms"] * 1e-3
+            n_cpu += 1
+            p += 1
+        out["pose_delta_max"] = max(deltas)
+        out["pose_delta_problems"] = ncheck
+        out["cpu_baseline"] = {
+            "value": round(n_cpu / t_cpu, 2), "unit": "scan-to-map problems/s", "cores": 1, "kind": "port",
+            "sample": f"{n_cpu} problems of this batch through the C++ MO restatement ({mode_name}, kNN = "
+                      f"{'the reference nanoflann kd-tree, oracle/_ref' if knn == 'kdtree' else 'grid restatement'}"
+                      f", tree build included), 1 thread, {t_cpu:.1f} s"}
+        out["speedup_vs_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
+    pipe.close()
+    return out
+
+
+def ctypes_sizeof_report() -> int:
+    import ctypes
+    from llsr import _abi
+    return ctypes.sizeof(_abi.LmReport)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -85,6 +227,9 @@ def main():
                     help="handles/HIP streams used round-robin, so consecutive batches overlap")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--s2m-problems", type=int, default=256, help="scan-to-map problems per GPU per step")
+    ap.add_argument("--s2m-steps", type=int, default=5)
+    ap.add_argument("--s2m-modes", default="lm_applied,faithful", help="comma list; empty = skip the leg")
     args = ap.parse_args()
 
     import torch
@@ -180,6 +325,12 @@ def main():
         if rec and t.get("batch"):
             traffic = rec["hbm_bytes"] / t["batch"] * B
 
+    s2m = {}
+    for mode_name in [m for m in args.s2m_modes.split(",") if m]:
+        s2m[mode_name] = scan2map_leg(dev, mode_name, args.s2m_problems, args.s2m_steps, 1, dist,
+                                      rank == 0 and not args.no_cpu and world == 1,
+                                      min(args.cpu_seconds, 12.0))
+
     if rank == 0:
         out = {
             "metric": "scans/sec (VLP-16 1800x16) at 1/2/4/8 GPUs; pose delta vs CPU ref",
@@ -207,7 +358,8 @@ def main():
             "pipeline_algorithmic_GBs": round(sum(per.values()) / (sum(ktimes.values()) * 1e-3) / 1e9, 1),
             "per_scan_mean": {k: round(v / B, 1) for k, v in csum.items() if k not in ("R", "M2")},
             "parity_spot_check_slot0": parity,
-            "pose_delta": None,
+            "pose_delta": s2m.get("lm_applied", {}).get("pose_delta_max"),
+            "scan2map": s2m,
         }
         if not args.no_cpu and world == 1:
             scans = [pts[off[k]:off[k + 1]] for k in range(min(args.distinct, B))]

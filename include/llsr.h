@@ -195,6 +195,15 @@ int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t max_problems, int32_t max_
  * has converged or reached iterCountThres; it returns when the batch is complete.
  * LLSR_ERANGE: a cloud exceeds the reserved capacity (nothing written for that problem). */
 int32_t llsr_scan2map_batch(llsr_handle* h, const llsr_s2m_batch* batch, void* hip_stream);
+/* Device time of the scan-to-map batches run since profiling was (re)enabled
+ * (llsr_set_profiling), from HIP events on the launch stream. */
+typedef struct llsr_s2m_stats {
+  int32_t batches;
+  int32_t iteration_launches;  /* k_s2m_iter launches, summed over batches */
+  float grid_ms;               /* setup + cell-table build, summed */
+  float iterate_ms;            /* first to last LM launch incl. the host's convergence polls, summed */
+} llsr_s2m_stats;
+int32_t llsr_scan2map_stats(llsr_handle* h, llsr_s2m_stats* out);
 /* One problem from host buffers (the reference's call shape: scan2MapOptimization on the
  * member clouds); reserves as needed; `pose` in/out; rep->ms = device time. */
 int32_t llsr_scan2map(llsr_handle* h, const float* corner_q, int32_t n_corner_q, const float* surf_q,

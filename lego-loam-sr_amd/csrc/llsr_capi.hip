@@ -76,6 +76,8 @@ struct llsr_handle {
     void* stage = nullptr;       // single-problem staging (llsr_scan2map)
     size_t stage_bytes = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipEvent_t p0 = nullptr, p1 = nullptr, p2 = nullptr;  // profiling: start, grid built, LM done
+    llsr_s2m_stats stats{};
   } mo;
   std::string err;
 };
@@ -260,6 +262,8 @@ extern "C" void llsr_destroy(llsr_handle* h) {
   if (h->mo.host_flags) (void)hipHostFree(h->mo.host_flags);
   if (h->mo.e0) (void)hipEventDestroy(h->mo.e0);
   if (h->mo.e1) (void)hipEventDestroy(h->mo.e1);
+  for (hipEvent_t e : {h->mo.p0, h->mo.p1, h->mo.p2})
+    if (e) (void)hipEventDestroy(e);
   if (h->d_in) (void)hipFree(h->d_in);
   if (h->d_off) (void)hipFree(h->d_off);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -304,6 +308,7 @@ extern "C" int32_t llsr_set_profiling(llsr_handle* h, int32_t enable) {
   while (h->ring_used > 0) retire_oldest(h);
   for (double& v : h->ksum) v = 0.0;
   h->kbatches = 0;
+  h->mo.stats = llsr_s2m_stats{};
   h->profiling = enable != 0;
   return LLSR_OK;
 }
@@ -563,7 +568,9 @@ extern "C" int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t P, int32_t mc, 
     m.host_flags = nullptr;
     return fail(h, LLSR_ENOMEM, "pinned flags");
   }
-  if (!m.e0 && (hipEventCreate(&m.e0) != hipSuccess || hipEventCreate(&m.e1) != hipSuccess))
+  if (!m.e0 && (hipEventCreate(&m.e0) != hipSuccess || hipEventCreate(&m.e1) != hipSuccess ||
+                 hipEventCreate(&m.p0) != hipSuccess || hipEventCreate(&m.p1) != hipSuccess ||
+                 hipEventCreate(&m.p2) != hipSuccess))
     return fail(h, LLSR_ENODEV, "events");
   return LLSR_OK;
 }
@@ -590,6 +597,7 @@ extern "C" int32_t llsr_scan2map_batch(llsr_handle* h, const llsr_s2m_batch* b, 
   a.sm = b->surf_map; a.sm_off = b->surf_map_off;
   a.pose = b->pose;
   a.report = b->report;
+  if (h->profiling) HIP_OK(h, hipEventRecord(m.p0, s));
   HIP_OK(h, hipMemsetAsync(a.n_active, 0, 2 * sizeof(int), s));
   k_s2m_setup<<<(P + 63) / 64, 64, 0, s>>>(a);
   const int Tmax = 1 << (m.log2T_c > m.log2T_s ? m.log2T_c : m.log2T_s);
@@ -599,20 +607,40 @@ extern "C" int32_t llsr_scan2map_batch(llsr_handle* h, const llsr_s2m_batch* b, 
   k_s2m_grid_alloc<<<dim3((Tmax + 255) / 256, P, 2), 256, 0, s>>>(a);
   if (Mmax > 0) k_s2m_grid_scatter<<<dim3((Mmax + 255) / 256, P, 2), 256, 0, s>>>(a);
   HIP_OK(h, hipGetLastError());
+  if (h->profiling) HIP_OK(h, hipEventRecord(m.p1, s));
   // LM iterations; poll the active count every `poll` launches
   const int poll = 4;
+  int launches = 0;
   for (int it = 0; it < a.iter_max;) {
     const int n = (a.iter_max - it) < poll ? (a.iter_max - it) : poll;
     for (int k = 0; k < n; ++k) k_s2m_iter<<<dim3(m.blocks, P), 256, 0, s>>>(a);
     it += n;
+    launches += n;
     HIP_OK(h, hipGetLastError());
     HIP_OK(h, hipMemcpyAsync(m.host_flags, a.n_active, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_OK(h, hipStreamSynchronize(s));
     if (m.host_flags[1]) return fail(h, LLSR_ERANGE, "a scan2map cloud exceeds the reserved capacity or has bad offsets");
     if (m.host_flags[0] == 0) break;
   }
+  if (h->profiling) HIP_OK(h, hipEventRecord(m.p2, s));
   k_s2m_finish<<<(P + 63) / 64, 64, 0, s>>>(a);
   HIP_OK(h, hipGetLastError());
+  if (h->profiling) {
+    float g = 0.f, it = 0.f;
+    HIP_OK(h, hipEventSynchronize(m.p2));
+    HIP_OK(h, hipEventElapsedTime(&g, m.p0, m.p1));
+    HIP_OK(h, hipEventElapsedTime(&it, m.p1, m.p2));
+    m.stats.batches += 1;
+    m.stats.iteration_launches += launches;
+    m.stats.grid_ms += g;
+    m.stats.iterate_ms += it;
+  }
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_scan2map_stats(llsr_handle* h, llsr_s2m_stats* out) {
+  if (!h || !out) return LLSR_EINVAL;
+  *out = h->mo.stats;
   return LLSR_OK;
 }
 

@@ -33,7 +33,7 @@ EXPORTS = [
     "llsr_config_default", "llsr_create", "llsr_destroy", "llsr_last_error", "llsr_query_sizes",
     "llsr_reset_state", "llsr_process_scan", "llsr_process_batch", "llsr_fetch_scan",
     "llsr_batch_counts", "llsr_kernel_times_ms", "llsr_kernel_name", "llsr_set_profiling",
-    "llsr_scan2map_reserve", "llsr_scan2map_batch", "llsr_scan2map",
+    "llsr_scan2map_reserve", "llsr_scan2map_batch", "llsr_scan2map", "llsr_scan2map_stats",
 ]
 
 
@@ -66,6 +66,7 @@ def lib():
         L.llsr_set_profiling.argtypes = [C.c_void_p, C.c_int32]
         L.llsr_scan2map_reserve.argtypes = [C.c_void_p] + [C.c_int32] * 5
         L.llsr_scan2map_batch.argtypes = [C.c_void_p, C.POINTER(_abi.S2MBatch), C.c_void_p]
+        L.llsr_scan2map_stats.argtypes = [C.c_void_p, C.POINTER(_abi.S2MStats)]
         L.llsr_scan2map.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p,
                                     C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(_abi.LmReport)]
         for fn in EXPORTS:
@@ -178,6 +179,12 @@ class Pipeline:
         for k, v in ptrs.items():
             setattr(b, k, v)
         self._check(lib().llsr_scan2map_batch(self._h, C.byref(b), C.c_void_p(stream)), "llsr_scan2map_batch")
+
+
+    def scan2map_stats(self) -> dict:
+        st = _abi.S2MStats()
+        self._check(lib().llsr_scan2map_stats(self._h, C.byref(st)), "llsr_scan2map_stats")
+        return {k: getattr(st, k) for k, _ in st._fields_}
 
 
 class MapOptimization:

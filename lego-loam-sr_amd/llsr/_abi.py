@@ -149,6 +149,11 @@ class S2MBatch(C.Structure):
     ]
 
 
+class S2MStats(C.Structure):
+    _fields_ = [("batches", C.c_int32), ("iteration_launches", C.c_int32), ("grid_ms", C.c_float),
+                ("iterate_ms", C.c_float)]
+
+
 class Sizes(C.Structure):
     _fields_ = [("cells", C.c_int32), ("rings", C.c_int32), ("max_points", C.c_int32),
                 ("shadow_points", C.c_int32)]
