@@ -537,7 +537,6 @@ extern "C" int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t P, int32_t mc, 
   m.log2T_s = log2_table(ms);
   m.blocks_c = (qc + 255) / 256;
   m.blocks = m.blocks_c + (qs + 255) / 256;
-  if (m.blocks == 0) m.blocks = 1;
   const size_t Tc = (size_t)1 << m.log2T_c, Ts = (size_t)1 << m.log2T_s;
   const size_t bytes = sizeof(S2MProb) * P + sizeof(S2MSlot) * P * (Tc + Ts) +
                        sizeof(float4) * P * ((size_t)mc + ms) + sizeof(int2) * P * ((size_t)mc + ms) +
@@ -563,6 +562,7 @@ extern "C" int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t P, int32_t mc, 
   a.error = a.n_active + 1;
   a.cap_qc = qc; a.cap_qs = qs; a.cap_mc = mc; a.cap_ms = ms;
   a.blocks_c = m.blocks_c;
+  a.blocks = m.blocks;
   a.log2T_c = m.log2T_c; a.log2T_s = m.log2T_s;
   if (!m.host_flags && hipHostMalloc((void**)&m.host_flags, 2 * sizeof(int)) != hipSuccess) {
     m.host_flags = nullptr;
@@ -613,7 +613,10 @@ extern "C" int32_t llsr_scan2map_batch(llsr_handle* h, const llsr_s2m_batch* b, 
   int launches = 0;
   for (int it = 0; it < a.iter_max;) {
     const int n = (a.iter_max - it) < poll ? (a.iter_max - it) : poll;
-    for (int k = 0; k < n; ++k) k_s2m_iter<<<dim3(m.blocks, P), 256, 0, s>>>(a);
+    for (int k = 0; k < n; ++k) {
+      if (m.blocks) k_s2m_iter<<<dim3(m.blocks, P), 256, 0, s>>>(a);
+      k_s2m_solve<<<(P + 63) / 64, 64, 0, s>>>(a);
+    }
     it += n;
     launches += n;
     HIP_OK(h, hipGetLastError());

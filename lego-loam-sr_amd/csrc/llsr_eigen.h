@@ -260,38 +260,52 @@ LLSR_HD int eig_sym(const float* A, float* evals, float* V) {
 }
 
 // ColPivHouseholderQR<Matrix<float, R, C>>(A).solve(b): least-squares x (A column-major, R x C).
+// Every loop has a compile-time trip count and the pivot swap / un-permutation select by
+// comparison instead of indexing with a runtime column, so on the device the arrays stay in
+// registers; the arithmetic and its order are those of Eigen's algorithm.
 template <int R, int C>
 LLSR_HD void colpiv_qr_solve(const float* Ain, const float* b, float* x) {
   float A[R * C];
+#pragma unroll
   for (int q = 0; q < R * C; ++q) A[q] = Ain[q];
-  const int size = R < C ? R : C;
+  constexpr int size = R < C ? R : C;
   float hc[C], nu[C], nd[C];
   int perm[C];
+#pragma unroll
   for (int k = 0; k < C; ++k) perm[k] = k;
+#pragma unroll
   for (int k = 0; k < C; ++k) {
     float sq = 0.0f;
+#pragma unroll
     for (int r = 0; r < R; ++r) sq += A[r + R * k] * A[r + R * k];
     nd[k] = sqrt_(sq);
     nu[k] = nd[k];
   }
   float maxn = 0.0f;
+#pragma unroll
   for (int k = 0; k < C; ++k) maxn = nu[k] > maxn ? nu[k] : maxn;
   const float eps = 1.1920929e-07f;
   const float thr_helper = (maxn * eps) * (maxn * eps) / (float)R;
   const float downdate_thr = sqrt_(eps);
   int nonzero = size;
   float maxpivot = 0.0f;
+#pragma unroll
   for (int k = 0; k < size; ++k) {
     int big = k;
     float bn = nu[k];
+#pragma unroll
     for (int j = k + 1; j < C; ++j)
       if (nu[j] > bn) { bn = nu[j]; big = j; }
     if (nonzero == size && bn * bn < thr_helper * (float)(R - k)) nonzero = k;
-    if (big != k) {
-      for (int r = 0; r < R; ++r) { const float t = A[r + R * k]; A[r + R * k] = A[r + R * big]; A[r + R * big] = t; }
-      float t = nu[k]; nu[k] = nu[big]; nu[big] = t;
-      t = nd[k]; nd[k] = nd[big]; nd[big] = t;
-      const int ti = perm[k]; perm[k] = perm[big]; perm[big] = ti;
+#pragma unroll
+    for (int j = k + 1; j < C; ++j) {
+      if (j == big) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) { const float t = A[r + R * k]; A[r + R * k] = A[r + R * j]; A[r + R * j] = t; }
+        float t = nu[k]; nu[k] = nu[j]; nu[j] = t;
+        t = nd[k]; nd[k] = nd[j]; nd[j] = t;
+        const int ti = perm[k]; perm[k] = perm[j]; perm[j] = ti;
+      }
     }
     float tau, beta;
     make_householder(&A[k + R * k], R - k, tau, beta);
@@ -300,14 +314,18 @@ LLSR_HD void colpiv_qr_solve(const float* Ain, const float* b, float* x) {
     hc[k] = tau;
     // apply H_k to the remaining columns
     if (tau != 0.0f) {
+#pragma unroll
       for (int j = k + 1; j < C; ++j) {
         float t = 0.0f;
+#pragma unroll
         for (int r = k + 1; r < R; ++r) t += A[r + R * k] * A[r + R * j];
         t += A[k + R * j];
         A[k + R * j] -= tau * t;
+#pragma unroll
         for (int r = k + 1; r < R; ++r) A[r + R * j] -= tau * A[r + R * k] * t;
       }
     }
+#pragma unroll
     for (int j = k + 1; j < C; ++j) {
       if (nu[j] != 0.0f) {
         float temp = fabs_(A[k + R * j]) / nu[j];
@@ -317,6 +335,7 @@ LLSR_HD void colpiv_qr_solve(const float* Ain, const float* b, float* x) {
         const float temp2 = temp * (ratio * ratio);
         if (temp2 <= downdate_thr) {
           float sq = 0.0f;
+#pragma unroll
           for (int r = k + 1; r < R; ++r) sq += A[r + R * j] * A[r + R * j];
           nd[j] = sqrt_(sq);
           nu[j] = nd[j];
@@ -328,22 +347,36 @@ LLSR_HD void colpiv_qr_solve(const float* Ain, const float* b, float* x) {
   }
   // c = Q^T b, then solve R_top c = c, then un-permute
   float cv[R];
+#pragma unroll
   for (int r = 0; r < R; ++r) cv[r] = b[r];
-  for (int k = 0; k < nonzero; ++k) {
+#pragma unroll
+  for (int k = 0; k < size; ++k) {
     const float tau = hc[k];
-    if (tau == 0.0f) continue;
+    if (k >= nonzero || tau == 0.0f) continue;
     float t = cv[k];
+#pragma unroll
     for (int r = k + 1; r < R; ++r) t += A[r + R * k] * cv[r];
     cv[k] -= tau * t;
+#pragma unroll
     for (int r = k + 1; r < R; ++r) cv[r] -= tau * A[r + R * k] * t;
   }
-  for (int i = nonzero - 1; i >= 0; --i) {
+#pragma unroll
+  for (int i = size - 1; i >= 0; --i) {
+    if (i >= nonzero) continue;
     float acc = cv[i];
-    for (int j = i + 1; j < nonzero; ++j) acc -= A[i + R * j] * cv[j];
+#pragma unroll
+    for (int j = i + 1; j < size; ++j)
+      if (j < nonzero) acc -= A[i + R * j] * cv[j];
     cv[i] = acc / A[i + R * i];
   }
-  for (int i = 0; i < C; ++i) x[i] = 0.0f;
-  for (int i = 0; i < nonzero; ++i) x[perm[i]] = cv[i];
+#pragma unroll
+  for (int j = 0; j < C; ++j) {
+    float v = 0.0f;
+#pragma unroll
+    for (int i = 0; i < size; ++i)
+      if (i < nonzero && perm[i] == j) v = cv[i];
+    x[j] = v;
+  }
 }
 
 }  // namespace llsr_eigen

@@ -23,8 +23,7 @@ struct S2MProb {
   float matX0[6];
   float min_lambda, cf_mean;
   int iter, active, converged, degenerate, nc, ns;
-  unsigned ticket;             // blocks of the current iteration that have finished
-  int pad_;
+  int pad_[2];
 };
 
 struct S2MArgs {
@@ -34,6 +33,7 @@ struct S2MArgs {
   float step_size, stop_thres;
   int cap_qc, cap_qs, cap_mc, cap_ms;
   int blocks_c;                // query blocks per problem reserved for corners (rest: surf)
+  int blocks;                  // query blocks per problem (grid.x of k_s2m_iter)
   int log2T_c, log2T_s;        // table sizes per problem
   const float* cq; const int64_t* cq_off;
   const float* sq; const int64_t* sq_off;
@@ -57,6 +57,7 @@ __global__ void k_s2m_grid_insert(S2MArgs a);
 __global__ void k_s2m_grid_alloc(S2MArgs a);
 __global__ void k_s2m_grid_scatter(S2MArgs a);
 __global__ void k_s2m_iter(S2MArgs a);
+__global__ void k_s2m_solve(S2MArgs a);
 __global__ void k_s2m_finish(S2MArgs a);
 
 }  // namespace llsr

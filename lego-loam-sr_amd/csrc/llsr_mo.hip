@@ -10,8 +10,9 @@
 //   k_s2m_iter  x it   one launch per LM iteration (MO:1578-1608) over (query block, problem):
 //                      pointAssociateToMap, kNN-5, the corner line / surf plane coefficient, the
 //                      Jacobian row, a fixed-order block reduction of the 21 + 6 normal-equation
-//                      terms; the last block of each problem (ticket) sums the block partials in
-//                      block order and runs LMOptimization's solve / degeneracy / update / stop
+//                      terms into per-block partials
+//   k_s2m_solve x it   one thread per problem: the block partials summed in block order, then
+//                      LMOptimization's solve / degeneracy / update / stop test
 //   k_s2m_finish       pose + llsr_lm_report out
 //
 // kNN-5 (nanoflann, exact, sorted) only matters when all five neighbours lie within d^2 < 1.0
@@ -90,29 +91,30 @@ __device__ bool knn5(const S2MSlot* __restrict__ tab, int log2T, const float4* _
 #pragma unroll
   for (int k = 0; k < 5; ++k) { b.d[k] = INFINITY; b.i[k] = INT_MAX; }
   const int cx = cell_coord(qx), cy = cell_coord(qy), cz = cell_coord(qz);
-  for (int a = -1; a <= 1; ++a)
-    for (int bb = -1; bb <= 1; ++bb)
-      for (int c = -1; c <= 1; ++c) {
-        const int s = grid_find(tab, log2T, cell_key(cx + a, cy + bb, cz + c));
-        if (s < 0) continue;
-        const int st = tab[s].start, n = tab[s].count;
-        for (int j = st; j < st + n; ++j) {
-          const float4 p = pts[j];
-          float d = 0.0f;
-          float t = qx - p.x; d += t * t;  // nanoflann L2 accumulation order
-          t = qy - p.y; d += t * t;
-          t = qz - p.z; d += t * t;
-          const int id = (int)fbits(p.w);
-          if (!(d < 1.0f) || !before(d, id, b.d[4], b.i[4])) continue;
-          b.d[4] = d; b.i[4] = id;
+  // cells visited one at a time (not unrolled): keeps the kernel at ~71 VGPRs / 7 waves per
+  // SIMD, which beat issuing all 27 probes up front (96+ VGPRs) on MI355X
+#pragma unroll 1
+  for (int c = 0; c < 27; ++c) {
+    const int s = grid_find(tab, log2T, cell_key(cx + c / 9 - 1, cy + (c / 3) % 3 - 1, cz + c % 3 - 1));
+    if (s < 0) continue;
+    const int st = tab[s].start, n = tab[s].count;
+    for (int j = st; j < st + n; ++j) {
+      const float4 p = pts[j];
+      float d = 0.0f;
+      float t = qx - p.x; d += t * t;  // nanoflann L2 accumulation order
+      t = qy - p.y; d += t * t;
+      t = qz - p.z; d += t * t;
+      const int id = (int)fbits(p.w);
+      if (!(d < 1.0f) || !before(d, id, b.d[4], b.i[4])) continue;
+      b.d[4] = d; b.i[4] = id;
 #pragma unroll
-          for (int k = 4; k > 0; --k)
-            if (before(b.d[k], b.i[k], b.d[k - 1], b.i[k - 1])) {
-              const float td = b.d[k]; b.d[k] = b.d[k - 1]; b.d[k - 1] = td;
-              const int ti = b.i[k]; b.i[k] = b.i[k - 1]; b.i[k - 1] = ti;
-            }
+      for (int k = 4; k > 0; --k)
+        if (before(b.d[k], b.i[k], b.d[k - 1], b.i[k - 1])) {
+          const float td = b.d[k]; b.d[k] = b.d[k - 1]; b.d[k - 1] = td;
+          const int ti = b.i[k]; b.i[k] = b.i[k - 1]; b.i[k - 1] = ti;
         }
-      }
+    }
+  }
   return b.d[4] < 1.0f;
 }
 
@@ -223,7 +225,7 @@ __global__ void k_s2m_setup(S2MArgs a) {
 #pragma unroll
   for (int k = 0; k < 6; ++k) { st.pose[k] = a.pose[6 * p + k]; st.matX0[k] = 0.0f; }
   st.iter = 0; st.converged = 0; st.degenerate = 0; st.nc = 0; st.ns = 0;
-  st.min_lambda = 0.0f; st.cf_mean = 0.0f; st.ticket = 0u;
+  st.min_lambda = 0.0f; st.cf_mean = 0.0f;
   st.active = (!bad && st.Mc > 10 && st.Ms > 100) ? 1 : 0;  // MO:1573
   st.cR = cosf_(st.pose[0]); st.sR = sinf_(st.pose[0]);
   st.cP = cosf_(st.pose[1]); st.sP = sinf_(st.pose[1]);
@@ -257,10 +259,11 @@ __global__ void k_s2m_grid_insert(S2MArgs a) {
   S2MSlot* tab = (m ? a.tab_s : a.tab_c) + ((size_t)p << log2T);
   const uint32_t mask = (1u << log2T) - 1u;
   uint32_t s = cell_hash(key, log2T);
-  for (;;) {
-    const uint64_t prev = atomicCAS((unsigned long long*)&tab[s].key, (unsigned long long)kEmpty,
-                                    (unsigned long long)key);
-    if (prev == kEmpty || prev == key) break;
+  for (;;) {  // a plain load first: most cells already exist (~2.5 points per cell)
+    uint64_t k = __hip_atomic_load((unsigned long long*)&tab[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k == kEmpty)
+      k = atomicCAS((unsigned long long*)&tab[s].key, (unsigned long long)kEmpty, (unsigned long long)key);
+    if (k == kEmpty || k == key) break;
     s = (s + 1) & mask;
   }
   const int rank = atomicAdd(&tab[s].count, 1);
@@ -268,14 +271,26 @@ __global__ void k_s2m_grid_insert(S2MArgs a) {
   where[k] = make_int2((int)s, rank);
 }
 
-__global__ void k_s2m_grid_alloc(S2MArgs a) {
+__global__ __launch_bounds__(256) void k_s2m_grid_alloc(S2MArgs a) {
+  // Cell ranges: a block scan of the slot counts, then ONE cursor atomic per block (the cells'
+  // order in the copy is irrelevant: kNN ties are broken by map index, not by position).
   const int p = blockIdx.y, m = blockIdx.z;
   const int log2T = m ? a.log2T_s : a.log2T_c;
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= (1u << log2T)) return;
+  if (blockIdx.x * blockDim.x >= (1u << log2T)) return;  // block-uniform
   S2MSlot* tab = (m ? a.tab_s : a.tab_c) + ((size_t)p << log2T);
-  const int c = tab[s].count;
-  if (c > 0) tab[s].start = atomicAdd(&a.cursor[2 * p + m], c);
+  const int c = s < (1u << log2T) ? tab[s].count : 0;
+  __shared__ int wtot[4];
+  __shared__ int base;
+  const int incl = wave_incl_scan_add(c);
+  const int w = threadIdx.x >> 6;
+  if (lane_id() == 63) wtot[w] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) base = atomicAdd(&a.cursor[2 * p + m], wtot[0] + wtot[1] + wtot[2] + wtot[3]);
+  __syncthreads();
+  int off = base;
+  for (int k = 0; k < w; ++k) off += wtot[k];
+  if (c > 0) tab[s].start = off + incl - c;
 }
 
 __global__ void k_s2m_grid_scatter(S2MArgs a) {
@@ -366,15 +381,15 @@ __device__ void lm_step(const S2MArgs& a, S2MProb& st, const float* red) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_s2m_iter(S2MArgs a) {
-  const int p = blockIdx.y;
+// One block of queries: kCorner = corner queries (partial slots [0, blocks_c)), else surf queries
+// (partial slots [blocks_c, blocks)).
+template <bool kCorner>
+__device__ __forceinline__ void s2m_block(const S2MArgs& a, int p, int qb) {
   S2MProb& st = a.prob[p];
   if (!st.active) return;
   __shared__ float wsum[4][kRed];
-  __shared__ int is_last;
-  const int cb = a.blocks_c;
-  const bool corner = (int)blockIdx.x < cb;
-  const int qi = (corner ? blockIdx.x : blockIdx.x - cb) * 256 + threadIdx.x;
+  constexpr bool corner = kCorner;
+  const int qi = qb * 256 + threadIdx.x;
   float v[kRed];
 #pragma unroll
   for (int k = 0; k < kRed; ++k) v[k] = 0.0f;
@@ -386,7 +401,7 @@ __global__ __launch_bounds__(256) void k_s2m_iter(S2MArgs a) {
     as.apply(q.x, q.y, q.z, x0, y0, z0);
     float la, lb, lc, ld;
     bool ok;
-    if (corner) {
+    if constexpr (kCorner) {
       const float4* mp = reinterpret_cast<const float4*>(a.cm) + st.mc0;
       ok = corner_coeff(a.tab_c + ((size_t)p << a.log2T_c), a.log2T_c, a.pts_c + (size_t)p * a.cap_mc, mp,
                         x0, y0, z0, la, lb, lc, ld);
@@ -428,26 +443,31 @@ __global__ __launch_bounds__(256) void k_s2m_iter(S2MArgs a) {
     if (lane_id() == 0) wsum[w][k] = s;
   }
   __syncthreads();
-  float* part = a.partial + ((size_t)p * gridDim.x + blockIdx.x) * 32;
+  float* part = a.partial + ((size_t)p * a.blocks + (kCorner ? 0 : a.blocks_c) + qb) * 32;
   if (threadIdx.x < kRed) part[threadIdx.x] = ((wsum[0][threadIdx.x] + wsum[1][threadIdx.x]) + wsum[2][threadIdx.x]) + wsum[3][threadIdx.x];
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) is_last = atomicAdd(&st.ticket, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!is_last) return;
-  __threadfence();
-  __shared__ float red[32];
-  if (threadIdx.x < kRed) {
-    const volatile float* pp = a.partial + (size_t)p * gridDim.x * 32 + threadIdx.x;
-    float s = 0.0f;
-    for (unsigned b = 0; b < gridDim.x; ++b) s += pp[(size_t)b * 32];
-    red[threadIdx.x] = s;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    st.ticket = 0u;
-    lm_step(a, st, red);
-  }
+}
+
+// grid (blocks, P): corner blocks first, then surf blocks; the branch is block-uniform.
+__global__ __launch_bounds__(256) void k_s2m_iter(S2MArgs a) {
+  if ((int)blockIdx.x < a.blocks_c)
+    s2m_block<true>(a, blockIdx.y, blockIdx.x);
+  else
+    s2m_block<false>(a, blockIdx.y, blockIdx.x - a.blocks_c);
+}
+
+
+// One thread per problem: block partials summed in block order, then the LM step.
+__global__ __launch_bounds__(64) void k_s2m_solve(S2MArgs a) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.P) return;
+  S2MProb& st = a.prob[p];
+  if (!st.active) return;
+  float red[kRed];
+  for (int k = 0; k < kRed; ++k) red[k] = 0.0f;
+  const float* pp = a.partial + (size_t)p * a.blocks * 32;
+  for (int b = 0; b < a.blocks; ++b)
+    for (int k = 0; k < kRed; ++k) red[k] += pp[(size_t)b * 32 + k];
+  lm_step(a, st, red);
 }
 
 __global__ void k_s2m_finish(S2MArgs a) {

@@ -26,7 +26,7 @@ from ._abi import Config, config_for  # noqa: F401
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _PKG = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(_PKG, "libllsr.so")
+LIB_PATH = os.environ.get("LLSR_LIB") or os.path.join(_PKG, "libllsr.so")  # override: A/B builds
 _LIB = None
 
 EXPORTS = [
