@@ -168,6 +168,54 @@ const char* llsr_kernel_name(int32_t k);
 /* Enable/disable per-kernel event timing; (re)enabling clears the accumulated averages. */
 int32_t llsr_set_profiling(llsr_handle* h, int32_t enable);
 
+/* ---- FeatureAssociation scan-to-scan LM (updateTransformation, featureAssociation.cpp:2505-2535) ----
+ * Two-step LM between consecutive scans: surf phase (rx, rz, ty; FA:1699-2010) then corner
+ * phase (ry, tx, tz; FA:1580-1697, 2013-2143), each <= 100 iterations, kNN-1 + ring-constrained
+ * neighbour search every 5th iteration. Inputs per scan (float4 x, y, z, intensity, LOAM frame):
+ * cornerPointsSharp and surfPointsFlat (with the 160 shadow points, FA:1310-1314) of the
+ * current scan; laserCloudCornerLast / laserCloudSurfLast of the previous one (after
+ * TransformToEnd + shadow points, FA:2660-2712). */
+typedef struct llsr_s2s_report {
+  int32_t surf_iterations;    /* iterCount1 when the surf loop ended (index of the converged step, or 100) */
+  int32_t corner_iterations;  /* iterCount2 likewise (the reference's odometry_itertimes, FA:2800) */
+  int32_t n_surf_corr;        /* correspondences at the last evaluated iteration of each phase */
+  int32_t n_corner_corr;
+  int32_t degenerate;         /* isDegenerate after the call (member state, FA:1975-1980) */
+  int32_t skipped;            /* 1: last clouds too small, transformCur untouched (FA:2506) */
+  float transform_cur[6];     /* rx, ry, rz, tx, ty, tz after updateTransformation */
+  float ms;
+} llsr_s2s_report;
+
+/* The 160 virtual shadow points of GenerateShadowPoint (FA:412-439), float4 [160]. */
+int32_t llsr_shadow_points(float* out_xyzi);
+
+typedef struct llsr_s2s_batch {
+  int32_t n_problems;
+  const float* sharp;       const int64_t* sharp_off;        /* cornerPointsSharp */
+  const float* flat;        const int64_t* flat_off;         /* surfPointsFlat + shadow points */
+  const float* corner_last; const int64_t* corner_last_off;  /* laserCloudCornerLast */
+  const float* surf_last;   const int64_t* surf_last_off;    /* laserCloudSurfLast */
+  float* transform_cur;     /* [P][6] in/out */
+  int32_t* is_degenerate;   /* [P] in/out (member state) */
+  llsr_s2s_report* report;  /* [P] out (device memory) */
+} llsr_s2s_batch;
+
+/* Size the scan-to-scan buffers (problems per batch, points per cloud). */
+int32_t llsr_scan2scan_reserve(llsr_handle* h, int32_t max_problems, int32_t max_sharp, int32_t max_flat,
+                               int32_t max_corner_last, int32_t max_surf_last);
+/* Enqueue a batch on `hip_stream` (NULL: the handle's stream); fully asynchronous: every
+ * iteration runs inside one kernel. LLSR_ERANGE is reported by a later call's check of the
+ * device error flag (llsr_scan2scan_check) when a cloud exceeded the reservation. */
+int32_t llsr_scan2scan_batch(llsr_handle* h, const llsr_s2s_batch* batch, void* hip_stream);
+/* Synchronise the last scan-to-scan batch and report capacity violations (LLSR_ERANGE). */
+int32_t llsr_scan2scan_check(llsr_handle* h);
+/* One scan from host buffers; reserves as needed; transform_cur / is_degenerate in/out. */
+int32_t llsr_scan2scan(llsr_handle* h, const float* sharp, int32_t n_sharp, const float* flat, int32_t n_flat,
+                       const float* corner_last, int32_t n_corner_last, const float* surf_last,
+                       int32_t n_surf_last, float* transform_cur, int32_t* is_degenerate,
+                       llsr_s2s_report* rep);
+
+
 /* ---- MapOptimization scan-to-map (scan2MapOptimization, mapOptmization.cpp:1572-1610) ----
  * A batch of independent problems, one per scan: the scan's corner queries
  * (laserCloudCornerScanDS, MO:1244-1247) and surf queries (laserCloudSurfTotalLastDS,

@@ -12,7 +12,9 @@
 
 #include "../../include/llsr.h"
 #include "llsr_device.h"
+#include "llsr_grid.h"
 #include "llsr_mo.h"
+#include "llsr_s2s.h"
 
 namespace llsr {
 __global__ void k_project(DevCfg, const float4*, const int64_t*, DevBufs);
@@ -79,6 +81,17 @@ struct llsr_handle {
     hipEvent_t p0 = nullptr, p1 = nullptr, p2 = nullptr;  // profiling: start, grid built, LM done
     llsr_s2m_stats stats{};
   } mo;
+  // scan-to-scan (llsr_scan2scan_*)
+  struct {
+    int P = 0, ms = 0, f = 0, nc = 0, ns = 0;
+    void* pool = nullptr;
+    S2SArgs a{};
+    int* host_flag = nullptr;
+    void* stage = nullptr;
+    size_t stage_bytes = 0;
+    hipStream_t last = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+  } s2s;
   std::string err;
 };
 
@@ -258,6 +271,11 @@ extern "C" void llsr_destroy(llsr_handle* h) {
       if (e) (void)hipEventDestroy(e);
   if (h->pool) (void)hipFree(h->pool);
   if (h->mo.pool) (void)hipFree(h->mo.pool);
+  if (h->s2s.pool) (void)hipFree(h->s2s.pool);
+  if (h->s2s.stage) (void)hipFree(h->s2s.stage);
+  if (h->s2s.host_flag) (void)hipHostFree(h->s2s.host_flag);
+  if (h->s2s.e0) (void)hipEventDestroy(h->s2s.e0);
+  if (h->s2s.e1) (void)hipEventDestroy(h->s2s.e1);
   if (h->mo.stage) (void)hipFree(h->mo.stage);
   if (h->mo.host_flags) (void)hipHostFree(h->mo.host_flags);
   if (h->mo.e0) (void)hipEventDestroy(h->mo.e0);
@@ -512,12 +530,6 @@ extern "C" int32_t llsr_process_scan(llsr_handle* h, const float* xyzi, int32_t 
 // ---------------------------------------------------------------------------------------------
 // Scan-to-map (MapOptimization::scan2MapOptimization, MO:1572-1610): see llsr_mo.hip.
 
-static int log2_table(int cap) {  // table of >= 2 * cap slots (load factor <= 0.5)
-  int l = 4;
-  while ((1ll << l) < 2ll * (cap > 1 ? cap : 1)) ++l;
-  return l;
-}
-
 extern "C" int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t P, int32_t mc, int32_t ms, int32_t qc,
                                          int32_t qs) {
   if (!h) return LLSR_EINVAL;
@@ -533,12 +545,12 @@ extern "C" int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t P, int32_t mc, 
     m.pool = nullptr;
   }
   m.P = P; m.mc = mc; m.ms = ms; m.qc = qc; m.qs = qs;
-  m.log2T_c = log2_table(mc);
-  m.log2T_s = log2_table(ms);
+  m.log2T_c = grid_log2_table(mc);
+  m.log2T_s = grid_log2_table(ms);
   m.blocks_c = (qc + 255) / 256;
   m.blocks = m.blocks_c + (qs + 255) / 256;
   const size_t Tc = (size_t)1 << m.log2T_c, Ts = (size_t)1 << m.log2T_s;
-  const size_t bytes = sizeof(S2MProb) * P + sizeof(S2MSlot) * P * (Tc + Ts) +
+  const size_t bytes = sizeof(S2MProb) * P + sizeof(CellSlot) * P * (Tc + Ts) +
                        sizeof(float4) * P * ((size_t)mc + ms) + sizeof(int2) * P * ((size_t)mc + ms) +
                        sizeof(int) * 2 * P + sizeof(float) * 32 * (size_t)P * m.blocks + 4096 + 8 * 256;
   if (hipMalloc(&m.pool, bytes) != hipSuccess) {
@@ -550,20 +562,24 @@ extern "C" int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t P, int32_t mc, 
   S2MArgs& a = m.a;
   a = S2MArgs{};
   a.prob = carve<S2MProb>(q, P);
-  a.tab_c = carve<S2MSlot>(q, P * Tc);
-  a.tab_s = carve<S2MSlot>(q, P * Ts);
-  a.pts_c = carve<float4>(q, (size_t)P * mc);
-  a.pts_s = carve<float4>(q, (size_t)P * ms);
-  a.where_c = carve<int2>(q, (size_t)P * mc);
-  a.where_s = carve<int2>(q, (size_t)P * ms);
-  a.cursor = carve<int>(q, 2 * (size_t)P);
+  CellGrid& gc = a.grids.g[0];
+  CellGrid& gs = a.grids.g[1];
+  gc.tab = carve<CellSlot>(q, P * Tc);
+  gs.tab = carve<CellSlot>(q, P * Ts);
+  gc.sorted = carve<float4>(q, (size_t)P * mc);
+  gs.sorted = carve<float4>(q, (size_t)P * ms);
+  gc.where = carve<int2>(q, (size_t)P * mc);
+  gs.where = carve<int2>(q, (size_t)P * ms);
+  gc.cursor = carve<int>(q, (size_t)P);
+  gs.cursor = carve<int>(q, (size_t)P);
+  gc.cap = mc; gs.cap = ms;
+  gc.log2T = m.log2T_c; gs.log2T = m.log2T_s;
   a.partial = carve<float>(q, 32 * (size_t)P * m.blocks);
   a.n_active = carve<int>(q, 2);
   a.error = a.n_active + 1;
   a.cap_qc = qc; a.cap_qs = qs; a.cap_mc = mc; a.cap_ms = ms;
   a.blocks_c = m.blocks_c;
   a.blocks = m.blocks;
-  a.log2T_c = m.log2T_c; a.log2T_s = m.log2T_s;
   if (!m.host_flags && hipHostMalloc((void**)&m.host_flags, 2 * sizeof(int)) != hipSuccess) {
     m.host_flags = nullptr;
     return fail(h, LLSR_ENOMEM, "pinned flags");
@@ -599,13 +615,13 @@ extern "C" int32_t llsr_scan2map_batch(llsr_handle* h, const llsr_s2m_batch* b, 
   a.report = b->report;
   if (h->profiling) HIP_OK(h, hipEventRecord(m.p0, s));
   HIP_OK(h, hipMemsetAsync(a.n_active, 0, 2 * sizeof(int), s));
+  a.grids.P = P;
+  a.grids.g[0].src = reinterpret_cast<const float4*>(b->corner_map);
+  a.grids.g[0].off = b->corner_map_off;
+  a.grids.g[1].src = reinterpret_cast<const float4*>(b->surf_map);
+  a.grids.g[1].off = b->surf_map_off;
   k_s2m_setup<<<(P + 63) / 64, 64, 0, s>>>(a);
-  const int Tmax = 1 << (m.log2T_c > m.log2T_s ? m.log2T_c : m.log2T_s);
-  const int Mmax = m.mc > m.ms ? m.mc : m.ms;
-  k_s2m_grid_clear<<<dim3((Tmax + 255) / 256, P, 2), 256, 0, s>>>(a);
-  if (Mmax > 0) k_s2m_grid_insert<<<dim3((Mmax + 255) / 256, P, 2), 256, 0, s>>>(a);
-  k_s2m_grid_alloc<<<dim3((Tmax + 255) / 256, P, 2), 256, 0, s>>>(a);
-  if (Mmax > 0) k_s2m_grid_scatter<<<dim3((Mmax + 255) / 256, P, 2), 256, 0, s>>>(a);
+  grid_build(a.grids, s);
   HIP_OK(h, hipGetLastError());
   if (h->profiling) HIP_OK(h, hipEventRecord(m.p1, s));
   // LM iterations; poll the active count every `poll` launches
@@ -698,6 +714,194 @@ extern "C" int32_t llsr_scan2map(llsr_handle* h, const float* cq, int32_t Qc, co
   HIP_OK(h, hipMemcpyAsync(rep, d_rep, sizeof *rep, hipMemcpyDeviceToHost, s));
   HIP_OK(h, hipMemcpyAsync(pose, d_pose, 6 * sizeof(float), hipMemcpyDeviceToHost, s));
   HIP_OK(h, hipStreamSynchronize(s));
+  float ms_ = 0.f;
+  HIP_OK(h, hipEventElapsedTime(&ms_, m.e0, m.e1));
+  rep->ms = ms_;
+  return LLSR_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Scan-to-scan (FeatureAssociation::updateTransformation, FA:2505-2535): see llsr_fa_lm.hip.
+
+extern "C" int32_t llsr_shadow_points(float* out) {
+  // GenerateShadowPoint (FA:412-439) with lidar_to_body_centor = (0.008, 0, -0.035) (FA:300),
+  // row_size 16, col_size 10 (FA:301); computed on the host with the same libm as the reference.
+  if (!out) return LLSR_EINVAL;
+  const double c0 = 0.008, c1 = 0.0, c2 = -0.035;
+  const int row_size = 16, col_size = 10;
+  const double row_angle = (std::atan2(0.120, 0.05) * 2) / (row_size - 1);
+  const double col_angle = (std::atan2(0.077, 0.05) * 2) / (col_size - 1);
+  int k = 0;
+  for (int row = 0; row < row_size; row++) {
+    const float row_x = (float)(0.05 * std::tan((((row_size - 1.0) / 2.0) * row_angle) - (row * row_angle)));
+    for (int col = 0; col < col_size; col++) {
+      const float col_y = (float)(0.05 * std::tan((((col_size - 1.0) / 2.0) * col_angle) - (col * col_angle)));
+      out[4 * k + 0] = (float)(col_y + c1);
+      out[4 * k + 1] = (float)(-(0.035f + 0.05f) + c2);
+      out[4 * k + 2] = (float)(row_x + c0);
+      out[4 * k + 3] = (float)((double)((float)row + (float)17) + (double)(float)col / 10000.0);
+      ++k;
+    }
+  }
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_scan2scan_reserve(llsr_handle* h, int32_t P, int32_t ms, int32_t f, int32_t nc, int32_t ns) {
+  if (!h) return LLSR_EINVAL;
+  if (P < 1 || ms < 0 || f < 0 || nc < 0 || ns < 0 || ms > (1 << 24) || f > (1 << 24) || nc > (1 << 24) || ns > (1 << 24))
+    return fail(h, LLSR_EINVAL, "scan2scan capacities out of range");
+  HIP_OK(h, hipSetDevice(h->device));
+  auto& m = h->s2s;
+  if (m.pool && P <= m.P && ms <= m.ms && f <= m.f && nc <= m.nc && ns <= m.ns) return LLSR_OK;
+  if (m.pool) {
+    HIP_OK(h, hipDeviceSynchronize());
+    HIP_OK(h, hipFree(m.pool));
+    m.pool = nullptr;
+  }
+  m.P = P; m.ms = ms; m.f = f; m.nc = nc; m.ns = ns;
+  const int lc = grid_log2_table(nc), ls = grid_log2_table(ns);
+  const size_t Tc = (size_t)1 << lc, Ts = (size_t)1 << ls;
+  const size_t capq = (size_t)(ms > f ? ms : f) + 1;
+  const size_t bytes = sizeof(CellSlot) * P * (Tc + Ts) + (sizeof(float4) + sizeof(int2)) * P * ((size_t)nc + ns) +
+                       sizeof(int) * 2 * P + (3 * sizeof(int) + sizeof(float4)) * P * capq + 64 + 12 * 256;
+  if (hipMalloc(&m.pool, bytes) != hipSuccess) {
+    m.pool = nullptr;
+    m.P = 0;
+    return fail(h, LLSR_ENOMEM, "scan2scan buffers");
+  }
+  char* q = (char*)m.pool;
+  S2SArgs& a = m.a;
+  a = S2SArgs{};
+  CellGrid& gc = a.grids.g[0];
+  CellGrid& gs = a.grids.g[1];
+  gc.tab = carve<CellSlot>(q, P * Tc);
+  gs.tab = carve<CellSlot>(q, P * Ts);
+  gc.sorted = carve<float4>(q, (size_t)P * nc);
+  gs.sorted = carve<float4>(q, (size_t)P * ns);
+  gc.where = carve<int2>(q, (size_t)P * nc);
+  gs.where = carve<int2>(q, (size_t)P * ns);
+  gc.cursor = carve<int>(q, (size_t)P);
+  gs.cursor = carve<int>(q, (size_t)P);
+  gc.cap = nc; gs.cap = ns;
+  gc.log2T = lc; gs.log2T = ls;
+  a.idx = carve<int>(q, 3 * (size_t)P * capq);
+  a.rows = carve<float4>(q, (size_t)P * capq);
+  a.error = carve<int>(q, 1);
+  a.cap_sharp = ms;
+  a.cap_flat = f;
+  if (!m.host_flag && hipHostMalloc((void**)&m.host_flag, sizeof(int)) != hipSuccess) {
+    m.host_flag = nullptr;
+    return fail(h, LLSR_ENOMEM, "pinned flag");
+  }
+  if (!m.e0 && (hipEventCreate(&m.e0) != hipSuccess || hipEventCreate(&m.e1) != hipSuccess))
+    return fail(h, LLSR_ENODEV, "events");
+  HIP_OK(h, hipMemset(a.error, 0, sizeof(int)));
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_scan2scan_batch(llsr_handle* h, const llsr_s2s_batch* b, void* hip_stream) {
+  if (!h || !b) return fail(h, LLSR_EINVAL, "null argument");
+  auto& m = h->s2s;
+  if (!m.pool) return fail(h, LLSR_EINVAL, "llsr_scan2scan_reserve not called");
+  const int P = b->n_problems;
+  if (P < 1 || P > m.P) return fail(h, LLSR_ERANGE, "n_problems outside [1, reserved]");
+  if (!b->sharp_off || !b->flat_off || !b->corner_last_off || !b->surf_last_off || !b->transform_cur ||
+      !b->is_degenerate || !b->report)
+    return fail(h, LLSR_EINVAL, "null batch array");
+  HIP_OK(h, hipSetDevice(h->device));
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+  S2SArgs a = m.a;
+  a.P = P;
+  a.dist_sqr = h->cfg.nearest_feature_search_distance * h->cfg.nearest_feature_search_distance;  // FA:152
+  a.sharp = reinterpret_cast<const float4*>(b->sharp); a.sharp_off = b->sharp_off;
+  a.flat = reinterpret_cast<const float4*>(b->flat); a.flat_off = b->flat_off;
+  a.grids.P = P;
+  a.grids.g[0].src = reinterpret_cast<const float4*>(b->corner_last);
+  a.grids.g[0].off = b->corner_last_off;
+  a.grids.g[1].src = reinterpret_cast<const float4*>(b->surf_last);
+  a.grids.g[1].off = b->surf_last_off;
+  a.tcur = b->transform_cur;
+  a.degen = b->is_degenerate;
+  a.report = b->report;
+  grid_build(a.grids, s);
+  k_s2s_lm<<<P, 256, 0, s>>>(a);
+  HIP_OK(h, hipGetLastError());
+  m.last = s;
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_scan2scan_check(llsr_handle* h) {
+  if (!h) return LLSR_EINVAL;
+  auto& m = h->s2s;
+  if (!m.pool) return LLSR_OK;
+  HIP_OK(h, hipSetDevice(h->device));
+  hipStream_t s = m.last ? m.last : h->stream;
+  HIP_OK(h, hipMemcpyAsync(m.host_flag, m.a.error, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_OK(h, hipStreamSynchronize(s));
+  if (*m.host_flag) {
+    HIP_OK(h, hipMemsetAsync(m.a.error, 0, sizeof(int), s));
+    HIP_OK(h, hipStreamSynchronize(s));
+    return fail(h, LLSR_ERANGE, "a scan2scan cloud exceeds the reserved capacity or has bad offsets");
+  }
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_scan2scan(llsr_handle* h, const float* sharp, int32_t Ms, const float* flat, int32_t F,
+                                  const float* cl, int32_t Nc, const float* sl, int32_t Ns, float* tcur,
+                                  int32_t* degen, llsr_s2s_report* rep) {
+  if (!h || !tcur || !degen || !rep || Ms < 0 || F < 0 || Nc < 0 || Ns < 0) return fail(h, LLSR_EINVAL, "bad argument");
+  if ((Ms && !sharp) || (F && !flat) || (Nc && !cl) || (Ns && !sl)) return fail(h, LLSR_EINVAL, "null cloud");
+  auto& m = h->s2s;
+  const int P = m.pool ? m.P : 1;
+  int32_t rc = llsr_scan2scan_reserve(h, P, Ms > m.ms ? Ms : m.ms, F > m.f ? F : m.f, Nc > m.nc ? Nc : m.nc,
+                                      Ns > m.ns ? Ns : m.ns);
+  if (rc != LLSR_OK) return rc;
+  const size_t npts = (size_t)Ms + F + Nc + Ns;
+  const size_t need = sizeof(float4) * npts + 8 * sizeof(int64_t) + 6 * sizeof(float) + sizeof(int) +
+                      sizeof(llsr_s2s_report) + 9 * 256;
+  if (need > m.stage_bytes) {
+    if (m.stage) HIP_OK(h, hipFree(m.stage));
+    m.stage = nullptr;
+    if (hipMalloc(&m.stage, need) != hipSuccess) { m.stage_bytes = 0; return fail(h, LLSR_ENOMEM, "staging"); }
+    m.stage_bytes = need;
+  }
+  char* q = (char*)m.stage;
+  float4* d_sh = carve<float4>(q, Ms);
+  float4* d_fl = carve<float4>(q, F);
+  float4* d_cl = carve<float4>(q, Nc);
+  float4* d_sl = carve<float4>(q, Ns);
+  int64_t* d_off = carve<int64_t>(q, 8);
+  float* d_t = carve<float>(q, 6);
+  int* d_deg = carve<int>(q, 1);
+  llsr_s2s_report* d_rep = carve<llsr_s2s_report>(q, 1);
+  hipStream_t s = h->stream;
+  HIP_OK(h, hipSetDevice(h->device));
+  if (Ms) HIP_OK(h, hipMemcpyAsync(d_sh, sharp, sizeof(float4) * Ms, hipMemcpyHostToDevice, s));
+  if (F) HIP_OK(h, hipMemcpyAsync(d_fl, flat, sizeof(float4) * F, hipMemcpyHostToDevice, s));
+  if (Nc) HIP_OK(h, hipMemcpyAsync(d_cl, cl, sizeof(float4) * Nc, hipMemcpyHostToDevice, s));
+  if (Ns) HIP_OK(h, hipMemcpyAsync(d_sl, sl, sizeof(float4) * Ns, hipMemcpyHostToDevice, s));
+  const int64_t offs[8] = {0, Ms, 0, F, 0, Nc, 0, Ns};
+  HIP_OK(h, hipMemcpyAsync(d_off, offs, sizeof offs, hipMemcpyHostToDevice, s));
+  HIP_OK(h, hipMemcpyAsync(d_t, tcur, 6 * sizeof(float), hipMemcpyHostToDevice, s));
+  HIP_OK(h, hipMemcpyAsync(d_deg, degen, sizeof(int), hipMemcpyHostToDevice, s));
+  llsr_s2s_batch b{};
+  b.n_problems = 1;
+  b.sharp = (const float*)d_sh; b.sharp_off = d_off;
+  b.flat = (const float*)d_fl; b.flat_off = d_off + 2;
+  b.corner_last = (const float*)d_cl; b.corner_last_off = d_off + 4;
+  b.surf_last = (const float*)d_sl; b.surf_last_off = d_off + 6;
+  b.transform_cur = d_t;
+  b.is_degenerate = d_deg;
+  b.report = d_rep;
+  HIP_OK(h, hipEventRecord(m.e0, s));
+  rc = llsr_scan2scan_batch(h, &b, s);
+  if (rc != LLSR_OK) return rc;
+  HIP_OK(h, hipEventRecord(m.e1, s));
+  HIP_OK(h, hipMemcpyAsync(rep, d_rep, sizeof *rep, hipMemcpyDeviceToHost, s));
+  HIP_OK(h, hipMemcpyAsync(tcur, d_t, 6 * sizeof(float), hipMemcpyDeviceToHost, s));
+  HIP_OK(h, hipMemcpyAsync(degen, d_deg, sizeof(int), hipMemcpyDeviceToHost, s));
+  rc = llsr_scan2scan_check(h);
+  if (rc != LLSR_OK) return rc;
   float ms_ = 0.f;
   HIP_OK(h, hipEventElapsedTime(&ms_, m.e0, m.e1));
   rep->ms = ms_;

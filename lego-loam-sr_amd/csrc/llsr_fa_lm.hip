@@ -1,0 +1,435 @@
+// llsr_fa_lm.hip — FeatureAssociation scan-to-scan LM on gfx950 (updateTransformation,
+// featureAssociation.cpp:2505-2535) for a batch of independent scans.
+//
+// k_s2s_lm: one 256-thread workgroup per scan runs the whole two-phase optimisation in-kernel
+// (no host round trips): surf phase (FA:2508-2516) then corner phase (FA:2519-2527), each up to
+// 100 iterations. Per iteration:
+//   A  every thread takes queries q = tid, tid + 256, ...: TransformToStart (FA:1389-1412); on
+//      iterations % 5 == 0 the kNN-1 in the last cloud (exact shell search over its 1 m cell
+//      grid, llsr_grid.h, brute force beyond kMaxShell) and the ring-constrained scans for the
+//      second / third tripod point in the last cloud's own order (FA:1588-1647, 1737-1803);
+//      then the line / plane coefficient (FA:1650-1695, 1806-1842) and the Jacobian row of
+//      calculateTransformation{Surf,Corner} (FA:1893-1913, 2046-2062), written to a row buffer;
+//   B  13 lanes of wave 0 sum the rows in correspondence order — one lane per entry of the
+//      3x3 AtA / 3-vector AtB, plus the count — the oracle's summation order exactly;
+//   C  thread 0: ColPivHouseholderQR solve, SelfAdjointEigenSolver degeneracy test at
+//      iteration 0, projection, pose update, NaN reset, stop test (FA:1915-2009, 2064-2142).
+// Float / double typing follows each reference line, sin/cos are the glibc ports, so results
+// are bit-identical to the CPU restatement (oracle/oracle_fa_lm.cpp).
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+#include "llsr_device.h"
+#include "llsr_eigen.h"
+#include "llsr_grid.h"
+#include "llsr_s2s.h"
+
+namespace llsr {
+
+using llsr_libm::cosf_;
+using llsr_libm::fabs_;
+using llsr_libm::fbits;
+using llsr_libm::sinf_;
+using llsr_libm::sqrt_;
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxShell = 4;  // grid shells searched before the exact brute-force fallback
+
+// TransformToStart (FA:1389-1412)
+__device__ __forceinline__ float4 to_start(const float* t, float4 pi) {
+  const float s = 10 * (pi.w - (float)trunc_i32(pi.w));
+  const float rx = s * t[0], ry = s * t[1], rz = s * t[2];
+  const float tx = s * t[3], ty = s * t[4], tz = s * t[5];
+  const float crz = cosf_(rz), srz = sinf_(rz);
+  const float crx = cosf_(rx), srx = sinf_(rx);
+  const float cry = cosf_(ry), sry = sinf_(ry);
+  const float x1 = crz * (pi.x - tx) + srz * (pi.y - ty);
+  const float y1 = -srz * (pi.x - tx) + crz * (pi.y - ty);
+  const float z1 = (pi.z - tz);
+  const float x2 = x1;
+  const float y2 = crx * y1 + srx * z1;
+  const float z2 = -srx * y1 + crx * z1;
+  return make_float4(cry * x2 - sry * z2, y2, sry * x2 + cry * z2, pi.w);
+}
+
+// (last - sel)^2 as written at FA:1609-1614
+__device__ __forceinline__ float sqdis(float4 a, float4 b) {
+  return (a.x - b.x) * (a.x - b.x) + (a.y - b.y) * (a.y - b.y) + (a.z - b.z) * (a.z - b.z);
+}
+
+// nanoflann L2_Simple (query - point), accumulated from 0
+__device__ __forceinline__ float l2(float4 q, float4 p) {
+  float d = 0.0f, t;
+  t = q.x - p.x; d += t * t;
+  t = q.y - p.y; d += t * t;
+  t = q.z - p.z; d += t * t;
+  return d;
+}
+
+// Exact nearest neighbour of q in grid g of problem p (KdTreeFLANN::nearestKSearch, k = 1;
+// ties -> lower index). Stops once the searched shells provably contain the nearest point or
+// nothing nearer than dist_sqr can remain outside them.
+__device__ void nn1(const CellGrid& g, int p, float4 q, float dist_sqr, int& bi, float& bd) {
+  const CellSlot* tab = g.table(p);
+  const float4* pts = g.cells(p);
+  bd = INFINITY;
+  bi = INT_MAX;
+  const int cx = cell_coord(q.x), cy = cell_coord(q.y), cz = cell_coord(q.z);
+  for (int h = 0; h <= kMaxShell; ++h) {
+    for (int dx = -h; dx <= h; ++dx)
+      for (int dy = -h; dy <= h; ++dy) {
+        const int step = (h == 0 || dx == -h || dx == h || dy == -h || dy == h) ? 1 : 2 * h;
+        for (int dz = -h; dz <= h; dz += step) {
+          const int s = grid_find(tab, g.log2T, cell_key(cx + dx, cy + dy, cz + dz));
+          if (s < 0) continue;
+          const int st = tab[s].start, n = tab[s].count;
+          for (int j = st; j < st + n; ++j) {
+            const float4 c = pts[j];
+            const float d = l2(q, c);
+            const int id = (int)fbits(c.w);
+            if (nn_before(d, id, bd, bi)) { bd = d; bi = id; }
+          }
+        }
+      }
+    // every point outside the searched block is at least r away (float slack 1e-5)
+    float r = q.x - (float)(cx - h);
+    r = fminf(r, (float)(cx + h + 1) - q.x);
+    r = fminf(r, q.y - (float)(cy - h));
+    r = fminf(r, (float)(cy + h + 1) - q.y);
+    r = fminf(r, q.z - (float)(cz - h));
+    r = fminf(r, (float)(cz + h + 1) - q.z);
+    const float r2 = r * r * (1.0f - 1e-5f);
+    if (bd < r2 || r2 >= dist_sqr) return;
+  }
+  const float4* src = g.src + g.off[p];
+  const int n = g.count(p);
+  bd = INFINITY;
+  bi = INT_MAX;
+  for (int k = 0; k < n; ++k) {
+    const float d = l2(q, src[k]);
+    if (d < bd) { bd = d; bi = k; }
+  }
+}
+
+// findCorrespondingCornerFeatures search (FA:1587-1648); `fwd` = the reference's forward bound
+// (cornerPointsSharpNum), clamped to the last cloud.
+__device__ void corner_search(const CellGrid& g, int p, const float4* cl, int Nc, int fwd, float4 sel,
+                              float dist_sqr, int& i1, int& i2) {
+  int nn;
+  float nd;
+  nn1(g, p, sel, dist_sqr, nn, nd);
+  i1 = -1;
+  i2 = -1;
+  if (!(nd < dist_sqr)) return;
+  i1 = nn;
+  const int cs = trunc_i32(cl[nn].w);
+  float m2 = dist_sqr;
+  const int end = fwd < Nc ? fwd : Nc;
+  for (int j = nn + 1; j < end; j++) {
+    const float4 c = cl[j];
+    const int rj = trunc_i32(c.w);
+    if ((double)rj > (double)cs + 2.5) break;
+    const float d = sqdis(c, sel);
+    if (rj > cs && d < m2) { m2 = d; i2 = j; }
+  }
+  for (int j = nn - 1; j >= 0; j--) {
+    const float4 c = cl[j];
+    const int rj = trunc_i32(c.w);
+    if ((double)rj < (double)cs - 2.5) break;
+    const float d = sqdis(c, sel);
+    if (rj < cs && d < m2) { m2 = d; i2 = j; }
+  }
+}
+
+// findCorrespondingSurfFeatures search (FA:1724-1809)
+__device__ void surf_search(const CellGrid& g, int p, const float4* sl, int Ns, int fwd, float4 sel,
+                            float dist_sqr, int& i1, int& i2, int& i3) {
+  int nn;
+  float nd;
+  nn1(g, p, sel, dist_sqr, nn, nd);
+  i1 = -1;
+  i2 = -1;
+  i3 = -1;
+  if (!(nd < dist_sqr)) return;
+  i1 = nn;
+  const int cs = trunc_i32(sl[nn].w);
+  float m2 = dist_sqr, m3 = dist_sqr;
+  const int end = fwd < Ns ? fwd : Ns;
+  for (int j = nn + 1; j < end; j++) {
+    const float4 c = sl[j];
+    const int rj = trunc_i32(c.w);
+    if ((double)rj > (double)cs + 2.5) break;
+    const float d = sqdis(c, sel);
+    if (rj <= cs) {
+      if (d < m2) { m2 = d; i2 = j; }
+    } else {
+      if (d < m3) { m3 = d; i3 = j; }
+    }
+  }
+  for (int j = nn - 1; j >= 0; j--) {
+    const float4 c = sl[j];
+    const int rj = trunc_i32(c.w);
+    if ((double)rj < (double)cs - 2.5) break;
+    const float d = sqdis(c, sel);
+    if (rj >= cs) {
+      if (d < m2) { m2 = d; i2 = j; }
+    } else {
+      if (d < m3) { m3 = d; i3 = j; }
+    }
+  }
+}
+
+// Jacobian constants of calculateTransformationSurf (FA:1858-1891) / ...Corner (FA:2025-2043)
+struct JacSurf {
+  float a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11, crx, b2, b6, c1, c2, c3, c4, c5, c6, c7, c8, c9;
+  __device__ explicit JacSurf(const float* t) {
+    const float srx = sinf_(t[0]), crx_ = cosf_(t[0]);
+    const float sry = sinf_(t[1]), cry = cosf_(t[1]);
+    const float srz = sinf_(t[2]), crz = cosf_(t[2]);
+    const float tx = t[3], ty = t[4], tz = t[5];
+    crx = crx_;
+    a1 = crx * sry * srz; a2 = crx * crz * sry; a3 = srx * sry;
+    a4 = tx * a1 - ty * a2 - tz * a3;
+    a5 = srx * srz; a6 = crz * srx;
+    a7 = ty * a6 - tz * crx - tx * a5;
+    a8 = crx * cry * srz; a9 = crx * cry * crz; a10 = cry * srx;
+    a11 = tz * a10 + ty * a9 - tx * a8;
+    const float b1 = -crz * sry - cry * srx * srz;
+    b2 = cry * crz * srx - sry * srz;
+    const float b5 = cry * crz - srx * sry * srz;
+    b6 = cry * srz + crz * srx * sry;
+    c1 = -b6; c2 = b5; c3 = tx * b6 - ty * b5; c4 = -crx * crz; c5 = crx * srz;
+    c6 = ty * c5 + tx * -c4; c7 = b2; c8 = -b1; c9 = tx * -b2 - ty * -b1;
+  }
+  __device__ void row(float4 p, float cx, float cy, float cz, float* J) const {
+    J[0] = (-a1 * p.x + a2 * p.y + a3 * p.z + a4) * cx + (a5 * p.x - a6 * p.y + crx * p.z + a7) * cy +
+           (a8 * p.x - a9 * p.y - a10 * p.z + a11) * cz;
+    J[1] = (c1 * p.x + c2 * p.y + c3) * cx + (c4 * p.x - c5 * p.y + c6) * cy + (c7 * p.x + c8 * p.y + c9) * cz;
+    J[2] = -b6 * cx + c4 * cy + b2 * cz;
+  }
+};
+
+struct JacCorner {
+  float b1, b2, b3, b4, b5, b6, b7, b8, c5, srx;
+  __device__ explicit JacCorner(const float* t) {
+    srx = sinf_(t[0]);
+    const float crx = cosf_(t[0]);
+    const float sry = sinf_(t[1]), cry = cosf_(t[1]);
+    const float srz = sinf_(t[2]), crz = cosf_(t[2]);
+    const float tx = t[3], ty = t[4], tz = t[5];
+    b1 = -crz * sry - cry * srx * srz;
+    b2 = cry * crz * srx - sry * srz;
+    b3 = crx * cry;
+    b4 = tx * -b1 + ty * -b2 + tz * b3;
+    b5 = cry * crz - srx * sry * srz;
+    b6 = cry * srz + crz * srx * sry;
+    b7 = crx * sry;
+    b8 = tz * b7 - ty * b6 - tx * b5;
+    c5 = crx * srz;
+  }
+  __device__ void row(float4 p, float cx, float cy, float cz, float* J) const {
+    J[0] = (b1 * p.x + b2 * p.y - b3 * p.z + b4) * cx + (b5 * p.x + b6 * p.y - b7 * p.z + b8) * cz;
+    J[1] = -b5 * cx + c5 * cy + b1 * cz;
+    J[2] = b7 * cx - srx * cy - b3 * cz;
+  }
+};
+
+}  // namespace
+
+__global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
+  const int p = blockIdx.x;
+  const int tid = threadIdx.x;
+  __shared__ float t[6];
+  __shared__ float matP[9];
+  __shared__ float sums[12];
+  __shared__ int cnt, isDeg, stop, n_corr[2], iters[2];
+  const CellGrid& gc = a.grids.g[0];
+  const CellGrid& gs = a.grids.g[1];
+  const int64_t ms0 = a.sharp_off[p], ms1 = a.sharp_off[p + 1], f0 = a.flat_off[p], f1 = a.flat_off[p + 1];
+  const int64_t nc = gc.off[p + 1] - gc.off[p], ns = gs.off[p + 1] - gs.off[p];
+  const bool bad = ms1 < ms0 || f1 < f0 || nc < 0 || ns < 0 || ms1 - ms0 > a.cap_sharp || f1 - f0 > a.cap_flat ||
+                   nc > gc.cap || ns > gs.cap;
+  const int Ms = bad ? 0 : (int)(ms1 - ms0), F = bad ? 0 : (int)(f1 - f0);
+  const int Nc = bad ? 0 : (int)nc, Ns = bad ? 0 : (int)ns;
+  if (tid == 0) {
+    for (int k = 0; k < 6; ++k) t[k] = a.tcur[6 * p + k];
+    isDeg = a.degen[p];
+    n_corr[0] = n_corr[1] = 0;
+    iters[0] = iters[1] = 0;
+    if (bad) atomicOr(a.error, 1);
+  }
+  __syncthreads();
+  const bool skipped = bad || Nc < 10 || Ns < 100;  // FA:2506
+  if (!skipped) {
+    const float4* cl = gc.src + gc.off[p];
+    const float4* sl = gs.src + gs.off[p];
+    const int capq = a.cap_sharp > a.cap_flat ? a.cap_sharp : a.cap_flat;
+    int* idx = a.idx + (size_t)p * capq * 3;
+    float4* rows = a.rows + (size_t)p * capq;
+    for (int phase = 0; phase < 2; ++phase) {  // 0: surf (FA:2508-2516), 1: corner (FA:2519-2527)
+      const bool surf = phase == 0;
+      const float4* qry = surf ? a.flat + f0 : a.sharp + ms0;
+      const int Q = surf ? F : Ms;
+      if (tid == 0)
+        for (int k = 0; k < 9; ++k) matP[k] = (k % 4 == 0) ? 1.0f : 0.0f;
+      __syncthreads();
+      int it = 0;
+      for (it = 0; it < 100; ++it) {
+        // ---- A: correspondences + Jacobian rows at the current transformCur ----
+        float tl[6];
+        for (int k = 0; k < 6; ++k) tl[k] = t[k];
+        for (int q = tid; q < Q; q += kThreads) {
+          const float4 pi = qry[q];
+          const float4 sel = to_start(tl, pi);
+          int* ix = idx + 3 * q;
+          if (it % 5 == 0) {
+            int i1, i2, i3 = -1;
+            if (surf)
+              surf_search(gs, p, sl, Ns, F, sel, a.dist_sqr, i1, i2, i3);
+            else
+              corner_search(gc, p, cl, Nc, Ms, sel, a.dist_sqr, i1, i2);
+            ix[0] = i1; ix[1] = i2; ix[2] = i3;
+          }
+          float4 row = make_float4(0.f, 0.f, 0.f, __uint_as_float(0x7fc00000u));
+          if (surf) {
+            if (ix[1] >= 0 && ix[2] >= 0) {
+              const float4 t1 = sl[ix[0]], t2 = sl[ix[1]], t3 = sl[ix[2]];
+              float pa = (t2.y - t1.y) * (t3.z - t1.z) - (t3.y - t1.y) * (t2.z - t1.z);
+              float pb = (t2.z - t1.z) * (t3.x - t1.x) - (t3.z - t1.z) * (t2.x - t1.x);
+              float pc = (t2.x - t1.x) * (t3.y - t1.y) - (t3.x - t1.x) * (t2.y - t1.y);
+              float pd = -(pa * t1.x + pb * t1.y + pc * t1.z);
+              const float ps = sqrt_(pa * pa + pb * pb + pc * pc);
+              pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+              const float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
+              float s = 1;
+              if (it >= 5)
+                s = (float)(1 - 1.8 * (double)fabs_(pd2) /
+                                    (double)sqrt_(sqrt_(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z)));
+              if ((double)s > 0.1 && pd2 != 0) {
+                float J[3];
+                JacSurf(tl).row(pi, s * pa, s * pb, s * pc, J);
+                row = make_float4(J[0], J[1], J[2], (float)(-0.05 * (double)(s * pd2)));
+              }
+            }
+          } else if (ix[1] >= 0) {
+            const float4 t1 = cl[ix[0]], t2 = cl[ix[1]];
+            const float x0 = sel.x, y0 = sel.y, z0 = sel.z;
+            const float x1 = t1.x, y1 = t1.y, z1 = t1.z, x2 = t2.x, y2 = t2.y, z2 = t2.z;
+            const float m11 = ((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1));
+            const float m22 = ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1));
+            const float m33 = ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1));
+            const float a012 = sqrt_(m11 * m11 + m22 * m22 + m33 * m33);
+            const float l12 = sqrt_((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2));
+            const float la = ((y1 - y2) * m11 + (z1 - z2) * m22) / a012 / l12;
+            const float lb = -((x1 - x2) * m11 - (z1 - z2) * m33) / a012 / l12;
+            const float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
+            const float ld2 = a012 / l12;
+            float s = 1;
+            if (it >= 5) s = (float)(1 - 1.8 * (double)fabs_(ld2));
+            if ((double)s > 0.1 && ld2 != 0) {
+              float J[3];
+              JacCorner(tl).row(pi, s * la, s * lb, s * lc, J);
+              row = make_float4(J[0], J[1], J[2], (float)(-0.05 * (double)(s * ld2)));
+            }
+          }
+          rows[q] = row;
+        }
+        __syncthreads();
+        // ---- B: AtA / AtB summed in correspondence order, one lane per entry ----
+        if (tid < 13) {
+          const int r = tid % 3, c = (tid / 3) % 3;
+          float acc = 0.0f;
+          int n = 0;
+          for (int q = 0; q < Q; ++q) {
+            const float4 w = rows[q];
+            if (w.w != w.w) continue;  // no correspondence
+            const float J[3] = {w.x, w.y, w.z};
+            if (tid < 9) acc += J[r] * J[c];
+            else if (tid < 12) acc += J[tid - 9] * w.w;
+            else ++n;
+          }
+          if (tid < 12) sums[tid] = acc;
+          else cnt = n;
+        }
+        __syncthreads();
+        // ---- C: solve and update (thread 0) ----
+        if (tid == 0) {
+          stop = 0;
+          n_corr[phase] = cnt;
+          if (cnt >= 10) {  // FA:2514 / 2525
+            float AtA[9], AtB[3], X[3];
+            for (int k = 0; k < 9; ++k) AtA[k] = sums[k];  // lane r + 3c -> column-major (r, c)
+            for (int k = 0; k < 3; ++k) AtB[k] = sums[9 + k];
+            llsr_eigen::colpiv_qr_solve<3, 3>(AtA, AtB, X);
+            if (it == 0) {
+              float E[3], V[9], V2[9];
+              llsr_eigen::eig3(AtA, E, V);
+              for (int k = 0; k < 9; ++k) V2[k] = V[k];
+              int deg = 0;
+              for (int i = 2; i >= 0; --i) {
+                if (E[i] < 10) {
+                  for (int j = 0; j < 3; ++j) V2[i + 3 * j] = 0;
+                  deg = 1;
+                } else {
+                  break;
+                }
+              }
+              isDeg = deg;
+              for (int r = 0; r < 3; ++r)  // matV.inverse() * matV2, V orthonormal: V^T * V2
+                for (int c = 0; c < 3; ++c) {
+                  float acc = 0;
+                  for (int k = 0; k < 3; ++k) acc += V[k + 3 * r] * V2[k + 3 * c];
+                  matP[r + 3 * c] = acc;
+                }
+            }
+            if (isDeg) {
+              const float X2[3] = {X[0], X[1], X[2]};
+              for (int r = 0; r < 3; ++r) X[r] = matP[r] * X2[0] + matP[r + 3] * X2[1] + matP[r + 6] * X2[2];
+            }
+            const float r2d = (float)(180.0 / 3.14159265358979323846);  // FA:56
+            double dR, dT;
+            if (surf) {
+              t[0] += X[0]; t[2] += X[1]; t[4] += X[2];
+              const double e0 = (double)(r2d * X[0]), e1 = (double)(r2d * X[1]), e2 = (double)(X[2] * 100);
+              dR = (double)(float)sqrt(e0 * e0 + e1 * e1);
+              dT = (double)(float)sqrt(e2 * e2);
+            } else {
+              t[1] += X[0]; t[3] += X[1]; t[5] += X[2];
+              const double e0 = (double)(r2d * X[0]), e1 = (double)(X[1] * 100), e2 = (double)(X[2] * 100);
+              dR = (double)(float)sqrt(e0 * e0);
+              dT = (double)(float)sqrt(e1 * e1 + e2 * e2);
+            }
+            for (int k = 0; k < 6; ++k)
+              if (t[k] != t[k]) t[k] = 0;
+            stop = (dR < 0.1 && dT < 0.1) ? 1 : 0;
+          }
+        }
+        __syncthreads();
+        if (stop) break;
+      }
+      if (tid == 0) iters[phase] = it;
+      __syncthreads();
+    }
+  }
+  if (tid == 0) {
+    llsr_s2s_report& r = a.report[p];
+    r.surf_iterations = skipped ? 0 : iters[0];
+    r.corner_iterations = skipped ? 0 : iters[1];
+    r.n_surf_corr = n_corr[0];
+    r.n_corner_corr = n_corr[1];
+    r.degenerate = isDeg;
+    r.skipped = skipped ? 1 : 0;
+    for (int k = 0; k < 6; ++k) {
+      r.transform_cur[k] = t[k];
+      a.tcur[6 * p + k] = t[k];
+    }
+    r.ms = 0.0f;
+    a.degen[p] = isDeg;
+  }
+}
+
+}  // namespace llsr

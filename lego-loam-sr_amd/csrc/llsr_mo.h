@@ -3,15 +3,9 @@
 #include <stdint.h>
 
 #include "../../include/llsr.h"
+#include "llsr_grid.h"
 
 namespace llsr {
-
-// One open-addressing slot of a problem's 1 m cell table.
-struct S2MSlot {
-  uint64_t key;  // packed cell (x, y, z) or ~0 = empty
-  int start;     // first point of the cell in the cell-contiguous copy
-  int count;
-};
 
 // Per-problem optimiser state, resident in HBM for the whole batch.
 struct S2MProb {
@@ -34,7 +28,6 @@ struct S2MArgs {
   int cap_qc, cap_qs, cap_mc, cap_ms;
   int blocks_c;                // query blocks per problem reserved for corners (rest: surf)
   int blocks;                  // query blocks per problem (grid.x of k_s2m_iter)
-  int log2T_c, log2T_s;        // table sizes per problem
   const float* cq; const int64_t* cq_off;
   const float* sq; const int64_t* sq_off;
   const float* cm; const int64_t* cm_off;
@@ -42,20 +35,13 @@ struct S2MArgs {
   float* pose;                 // [P][6] in/out
   llsr_lm_report* report;      // [P]
   S2MProb* prob;               // [P]
-  S2MSlot* tab_c; S2MSlot* tab_s;  // [P][T]
-  float4* pts_c; float4* pts_s;    // [P][cap] cell-contiguous map copies
-  int2* where_c; int2* where_s;    // [P][cap] (slot, rank) per map point
-  int* cursor;                 // [P][2]
+  CellGrids2 grids;            // g[0] corner map, g[1] surf map
   float* partial;              // [P][blocks][32] block sums
   int* n_active;               // problems still iterating
   int* error;                  // capacity / offset violations
 };
 
 __global__ void k_s2m_setup(S2MArgs a);
-__global__ void k_s2m_grid_clear(S2MArgs a);
-__global__ void k_s2m_grid_insert(S2MArgs a);
-__global__ void k_s2m_grid_alloc(S2MArgs a);
-__global__ void k_s2m_grid_scatter(S2MArgs a);
 __global__ void k_s2m_iter(S2MArgs a);
 __global__ void k_s2m_solve(S2MArgs a);
 __global__ void k_s2m_finish(S2MArgs a);

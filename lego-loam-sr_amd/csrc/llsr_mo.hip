@@ -4,9 +4,8 @@
 //
 // Per batch:
 //   k_s2m_setup        problem bookkeeping, capacity checks, the MO:1573 guard
-//   k_s2m_grid_insert  1 m cell hash grid of both maps (kdtreeCornerFromMap / kdtreeSurfFromMap
-//   k_s2m_grid_alloc   setInputCloud, MO:1575-1576): open-addressing table of cell keys, point
-//   k_s2m_grid_scatter counts, then map points copied cell-contiguous as (x, y, z, index bits)
+//   k_grid_*           1 m cell grids of both maps (kdtreeCornerFromMap / kdtreeSurfFromMap
+//                      setInputCloud, MO:1575-1576), llsr_grid.h
 //   k_s2m_iter  x it   one launch per LM iteration (MO:1578-1608) over (query block, problem):
 //                      pointAssociateToMap, kNN-5, the corner line / surf plane coefficient, the
 //                      Jacobian row, a fixed-order block reduction of the 21 + 6 normal-equation
@@ -33,6 +32,7 @@
 #include "../../include/llsr.h"
 #include "llsr_device.h"
 #include "llsr_eigen.h"
+#include "llsr_grid.h"
 #include "llsr_mo.h"
 
 namespace llsr {
@@ -46,47 +46,13 @@ using llsr_libm::sqrt_;
 
 namespace {
 
-constexpr uint64_t kEmpty = ~0ull;
-
-__device__ __forceinline__ int cell_coord(float v) {
-  // floor() to a cell index; NaN / huge coordinates land in a far sentinel cell (their distance
-  // test fails anyway, so where they are bucketed cannot change a result)
-  const float f = floorf(v);
-  return (f > -1048000.0f && f < 1048000.0f) ? (int)f : 1048500;
-}
-
-__device__ __forceinline__ uint64_t cell_key(int a, int b, int c) {
-  return ((uint64_t)(uint32_t)(a + 1048576) << 42) | ((uint64_t)(uint32_t)(b + 1048576) << 21) |
-         (uint64_t)(uint32_t)(c + 1048576);
-}
-
-__device__ __forceinline__ uint32_t cell_hash(uint64_t k, int log2T) {
-  return (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> (64 - log2T));
-}
-
-// Probe for `key`; returns the slot or -1.
-__device__ __forceinline__ int grid_find(const S2MSlot* __restrict__ tab, int log2T, uint64_t key) {
-  const uint32_t mask = (1u << log2T) - 1u;
-  uint32_t s = cell_hash(key, log2T);
-  for (;;) {
-    const uint64_t k = tab[s].key;
-    if (k == key) return (int)s;
-    if (k == kEmpty) return -1;
-    s = (s + 1) & mask;
-  }
-}
-
 struct Best5 {
   float d[5];
   int i[5];
 };
 
-__device__ __forceinline__ bool before(float da, int ia, float db, int ib) {
-  return da < db || (da == db && ia < ib);
-}
-
 // kNN-5 with d^2 < 1.0 around q in one map; returns true when five were found.
-__device__ bool knn5(const S2MSlot* __restrict__ tab, int log2T, const float4* __restrict__ pts,
+__device__ bool knn5(const CellSlot* __restrict__ tab, int log2T, const float4* __restrict__ pts,
                      float qx, float qy, float qz, Best5& b) {
 #pragma unroll
   for (int k = 0; k < 5; ++k) { b.d[k] = INFINITY; b.i[k] = INT_MAX; }
@@ -105,11 +71,11 @@ __device__ bool knn5(const S2MSlot* __restrict__ tab, int log2T, const float4* _
       t = qy - p.y; d += t * t;
       t = qz - p.z; d += t * t;
       const int id = (int)fbits(p.w);
-      if (!(d < 1.0f) || !before(d, id, b.d[4], b.i[4])) continue;
+      if (!(d < 1.0f) || !nn_before(d, id, b.d[4], b.i[4])) continue;
       b.d[4] = d; b.i[4] = id;
 #pragma unroll
       for (int k = 4; k > 0; --k)
-        if (before(b.d[k], b.i[k], b.d[k - 1], b.i[k - 1])) {
+        if (nn_before(b.d[k], b.i[k], b.d[k - 1], b.i[k - 1])) {
           const float td = b.d[k]; b.d[k] = b.d[k - 1]; b.d[k - 1] = td;
           const int ti = b.i[k]; b.i[k] = b.i[k - 1]; b.i[k - 1] = ti;
         }
@@ -135,7 +101,7 @@ struct Assoc {
 };
 
 // cornerOptimization body (MO:1274-1375) for one query; returns false when rejected.
-__device__ bool corner_coeff(const S2MSlot* tab, int log2T, const float4* pts, const float4* mapP,
+__device__ bool corner_coeff(const CellSlot* tab, int log2T, const float4* pts, const float4* mapP,
                              float x0, float y0, float z0, float& la, float& lb, float& lc, float& ld) {
   Best5 nb;
   if (!knn5(tab, log2T, pts, x0, y0, z0, nb)) return false;
@@ -178,7 +144,7 @@ __device__ bool corner_coeff(const S2MSlot* tab, int log2T, const float4* pts, c
 }
 
 // surfOptimization body (MO:1383-1440) for one query.
-__device__ bool surf_coeff(const S2MSlot* tab, int log2T, const float4* pts, const float4* mapP,
+__device__ bool surf_coeff(const CellSlot* tab, int log2T, const float4* pts, const float4* mapP,
                            float x0, float y0, float z0, float& la, float& lb, float& lc, float& ld) {
   Best5 nb;
   if (!knn5(tab, log2T, pts, x0, y0, z0, nb)) return false;
@@ -231,81 +197,6 @@ __global__ void k_s2m_setup(S2MArgs a) {
   st.cP = cosf_(st.pose[1]); st.sP = sinf_(st.pose[1]);
   st.cY = cosf_(st.pose[2]); st.sY = sinf_(st.pose[2]);
   if (st.active) atomicAdd(a.n_active, 1);
-  a.cursor[2 * p] = 0;
-  a.cursor[2 * p + 1] = 0;
-}
-
-// blockIdx.z: 0 = corner map, 1 = surf map (all grid kernels).
-__global__ void k_s2m_grid_clear(S2MArgs a) {
-  const int p = blockIdx.y, m = blockIdx.z;
-  const int log2T = m ? a.log2T_s : a.log2T_c;
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= (1u << log2T)) return;
-  S2MSlot& t = (m ? a.tab_s : a.tab_c)[((size_t)p << log2T) + s];
-  t.key = kEmpty;
-  t.start = 0;
-  t.count = 0;
-}
-
-__global__ void k_s2m_grid_insert(S2MArgs a) {
-  const int p = blockIdx.y, m = blockIdx.z;
-  const S2MProb& st = a.prob[p];
-  const int n = m ? st.Ms : st.Mc;
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  const float4 q = reinterpret_cast<const float4*>(m ? a.sm : a.cm)[(m ? st.ms0 : st.mc0) + k];
-  const uint64_t key = cell_key(cell_coord(q.x), cell_coord(q.y), cell_coord(q.z));
-  const int log2T = m ? a.log2T_s : a.log2T_c;
-  S2MSlot* tab = (m ? a.tab_s : a.tab_c) + ((size_t)p << log2T);
-  const uint32_t mask = (1u << log2T) - 1u;
-  uint32_t s = cell_hash(key, log2T);
-  for (;;) {  // a plain load first: most cells already exist (~2.5 points per cell)
-    uint64_t k = __hip_atomic_load((unsigned long long*)&tab[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (k == kEmpty)
-      k = atomicCAS((unsigned long long*)&tab[s].key, (unsigned long long)kEmpty, (unsigned long long)key);
-    if (k == kEmpty || k == key) break;
-    s = (s + 1) & mask;
-  }
-  const int rank = atomicAdd(&tab[s].count, 1);
-  int2* where = (m ? a.where_s : a.where_c) + (size_t)p * (m ? a.cap_ms : a.cap_mc);
-  where[k] = make_int2((int)s, rank);
-}
-
-__global__ __launch_bounds__(256) void k_s2m_grid_alloc(S2MArgs a) {
-  // Cell ranges: a block scan of the slot counts, then ONE cursor atomic per block (the cells'
-  // order in the copy is irrelevant: kNN ties are broken by map index, not by position).
-  const int p = blockIdx.y, m = blockIdx.z;
-  const int log2T = m ? a.log2T_s : a.log2T_c;
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (blockIdx.x * blockDim.x >= (1u << log2T)) return;  // block-uniform
-  S2MSlot* tab = (m ? a.tab_s : a.tab_c) + ((size_t)p << log2T);
-  const int c = s < (1u << log2T) ? tab[s].count : 0;
-  __shared__ int wtot[4];
-  __shared__ int base;
-  const int incl = wave_incl_scan_add(c);
-  const int w = threadIdx.x >> 6;
-  if (lane_id() == 63) wtot[w] = incl;
-  __syncthreads();
-  if (threadIdx.x == 0) base = atomicAdd(&a.cursor[2 * p + m], wtot[0] + wtot[1] + wtot[2] + wtot[3]);
-  __syncthreads();
-  int off = base;
-  for (int k = 0; k < w; ++k) off += wtot[k];
-  if (c > 0) tab[s].start = off + incl - c;
-}
-
-__global__ void k_s2m_grid_scatter(S2MArgs a) {
-  const int p = blockIdx.y, m = blockIdx.z;
-  const S2MProb& st = a.prob[p];
-  const int n = m ? st.Ms : st.Mc;
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  const float4 q = reinterpret_cast<const float4*>(m ? a.sm : a.cm)[(m ? st.ms0 : st.mc0) + k];
-  const int cap = m ? a.cap_ms : a.cap_mc;
-  const int2 w = (m ? a.where_s : a.where_c)[(size_t)p * cap + k];
-  const int log2T = m ? a.log2T_s : a.log2T_c;
-  const S2MSlot* tab = (m ? a.tab_s : a.tab_c) + ((size_t)p << log2T);
-  float4* dst = (m ? a.pts_s : a.pts_c) + (size_t)p * cap;
-  dst[tab[w.x].start + w.y] = make_float4(q.x, q.y, q.z, bitsf((uint32_t)k));
 }
 
 // Values reduced per block: AtA upper triangle (21), AtB (6), sum |coeff.intensity|, #corner,
@@ -403,11 +294,11 @@ __device__ __forceinline__ void s2m_block(const S2MArgs& a, int p, int qb) {
     bool ok;
     if constexpr (kCorner) {
       const float4* mp = reinterpret_cast<const float4*>(a.cm) + st.mc0;
-      ok = corner_coeff(a.tab_c + ((size_t)p << a.log2T_c), a.log2T_c, a.pts_c + (size_t)p * a.cap_mc, mp,
+      ok = corner_coeff(a.grids.g[0].table(p), a.grids.g[0].log2T, a.grids.g[0].cells(p), mp,
                         x0, y0, z0, la, lb, lc, ld);
     } else {
       const float4* mp = reinterpret_cast<const float4*>(a.sm) + st.ms0;
-      ok = surf_coeff(a.tab_s + ((size_t)p << a.log2T_s), a.log2T_s, a.pts_s + (size_t)p * a.cap_ms, mp,
+      ok = surf_coeff(a.grids.g[1].table(p), a.grids.g[1].log2T, a.grids.g[1].cells(p), mp,
                       x0, y0, z0, la, lb, lc, ld);
     }
     if (ok) {

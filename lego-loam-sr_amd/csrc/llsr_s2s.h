@@ -1,0 +1,27 @@
+// llsr_s2s.h — device data of the scan-to-scan LM batch (llsr_fa_lm.hip).
+#pragma once
+#include <stdint.h>
+
+#include "../../include/llsr.h"
+#include "llsr_grid.h"
+
+namespace llsr {
+
+struct S2SArgs {
+  int P;
+  float dist_sqr;              // nearest_feature_search_distance^2 (FA:152)
+  int cap_sharp, cap_flat;     // queries per problem reserved
+  const float4* sharp; const int64_t* sharp_off;   // cornerPointsSharp
+  const float4* flat;  const int64_t* flat_off;    // surfPointsFlat (+ shadow points)
+  CellGrids2 grids;            // g[0] laserCloudCornerLast, g[1] laserCloudSurfLast
+  float* tcur;                 // [P][6] transformCur in/out
+  int* degen;                  // [P] isDegenerate in/out
+  llsr_s2s_report* report;     // [P]
+  int* idx;                    // [P][max(cap_sharp, cap_flat)][3] correspondence indices
+  float4* rows;                // [P][max(cap_sharp, cap_flat)] Jacobian row (3) + b, w = NaN: none
+  int* error;                  // capacity violations
+};
+
+__global__ void k_s2s_lm(S2SArgs a);
+
+}  // namespace llsr

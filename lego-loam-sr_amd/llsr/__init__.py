@@ -34,6 +34,8 @@ EXPORTS = [
     "llsr_reset_state", "llsr_process_scan", "llsr_process_batch", "llsr_fetch_scan",
     "llsr_batch_counts", "llsr_kernel_times_ms", "llsr_kernel_name", "llsr_set_profiling",
     "llsr_scan2map_reserve", "llsr_scan2map_batch", "llsr_scan2map", "llsr_scan2map_stats",
+    "llsr_shadow_points", "llsr_scan2scan_reserve", "llsr_scan2scan_batch", "llsr_scan2scan_check",
+    "llsr_scan2scan",
 ]
 
 
@@ -67,6 +69,13 @@ def lib():
         L.llsr_scan2map_reserve.argtypes = [C.c_void_p] + [C.c_int32] * 5
         L.llsr_scan2map_batch.argtypes = [C.c_void_p, C.POINTER(_abi.S2MBatch), C.c_void_p]
         L.llsr_scan2map_stats.argtypes = [C.c_void_p, C.POINTER(_abi.S2MStats)]
+        L.llsr_shadow_points.argtypes = [C.c_void_p]
+        L.llsr_scan2scan_reserve.argtypes = [C.c_void_p] + [C.c_int32] * 5
+        L.llsr_scan2scan_batch.argtypes = [C.c_void_p, C.POINTER(_abi.S2SBatch), C.c_void_p]
+        L.llsr_scan2scan_check.argtypes = [C.c_void_p]
+        L.llsr_scan2scan.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p,
+                                     C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
+                                     C.POINTER(_abi.S2SReport)]
         L.llsr_scan2map.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p,
                                     C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(_abi.LmReport)]
         for fn in EXPORTS:
@@ -185,6 +194,63 @@ class Pipeline:
         st = _abi.S2MStats()
         self._check(lib().llsr_scan2map_stats(self._h, C.byref(st)), "llsr_scan2map_stats")
         return {k: getattr(st, k) for k, _ in st._fields_}
+
+
+    # ---- scan-to-scan (FeatureAssociation::updateTransformation) ------------------------------
+    def scan2scan_reserve(self, problems: int, sharp: int, flat: int, corner_last: int, surf_last: int):
+        self._check(lib().llsr_scan2scan_reserve(self._h, problems, sharp, flat, corner_last, surf_last),
+                    "llsr_scan2scan_reserve")
+
+    def scan2scan(self, sharp, flat, corner_last, surf_last, transform_cur, is_degenerate: int = 0) -> dict:
+        """One scan from host arrays; returns the report (+ transform_cur, is_degenerate)."""
+        arrs = [np.ascontiguousarray(a, dtype=np.float32).reshape(-1, 4) for a in (sharp, flat, corner_last, surf_last)]
+        t = np.ascontiguousarray(transform_cur, dtype=np.float32).copy()
+        deg = C.c_int32(is_degenerate)
+        rep = _abi.S2SReport()
+        args = []
+        for a in arrs:
+            args += [C.c_void_p(a.ctypes.data if len(a) else None), len(a)]
+        self._check(lib().llsr_scan2scan(self._h, *args, t.ctypes.data, C.byref(deg), C.byref(rep)), "llsr_scan2scan")
+        d = rep.as_dict()
+        d["transform_cur"] = t
+        d["is_degenerate"] = deg.value
+        return d
+
+    def scan2scan_batch(self, ptrs: dict, P: int, stream: int = 0):
+        b = _abi.S2SBatch()
+        b.n_problems = P
+        for k, v in ptrs.items():
+            setattr(b, k, v)
+        self._check(lib().llsr_scan2scan_batch(self._h, C.byref(b), C.c_void_p(stream)), "llsr_scan2scan_batch")
+
+    def scan2scan_check(self):
+        self._check(lib().llsr_scan2scan_check(self._h), "llsr_scan2scan_check")
+
+
+def shadow_points() -> np.ndarray:
+    """GenerateShadowPoint (FA:412-439): the 160 virtual points appended to the flat / surf-last clouds."""
+    out = np.zeros((160, 4), np.float32)
+    rc = lib().llsr_shadow_points(out.ctypes.data)
+    if rc != 0:
+        raise LlsrError(f"llsr_shadow_points: {rc}")
+    return out
+
+
+class FeatureAssociation:
+    """Drop-in for FeatureAssociation::updateTransformation's arithmetic (FA:2505-2535)."""
+
+    def __init__(self, pipeline: Pipeline):
+        self.p = pipeline
+        self.transform_cur = np.zeros(6, np.float32)
+        self.is_degenerate = 0
+
+    def update_transformation(self, corner_points_sharp, surf_points_flat, laser_cloud_corner_last,
+                              laser_cloud_surf_last) -> dict:
+        r = self.p.scan2scan(corner_points_sharp, surf_points_flat, laser_cloud_corner_last,
+                             laser_cloud_surf_last, self.transform_cur, self.is_degenerate)
+        self.transform_cur = r["transform_cur"]
+        self.is_degenerate = r["is_degenerate"]
+        return r
 
 
 class MapOptimization:

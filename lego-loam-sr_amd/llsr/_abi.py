@@ -136,6 +136,39 @@ class LmReport(C.Structure):
         return d
 
 
+class S2SReport(C.Structure):
+    """llsr_s2s_report (include/llsr.h): result of one scan-to-scan updateTransformation."""
+    _fields_ = [
+        ("surf_iterations", C.c_int32),
+        ("corner_iterations", C.c_int32),
+        ("n_surf_corr", C.c_int32),
+        ("n_corner_corr", C.c_int32),
+        ("degenerate", C.c_int32),
+        ("skipped", C.c_int32),
+        ("transform_cur", C.c_float * 6),
+        ("ms", C.c_float),
+    ]
+
+    def as_dict(self) -> dict:
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["transform_cur"] = np.array(self.transform_cur[:], dtype=np.float32)
+        return d
+
+
+class S2SBatch(C.Structure):
+    """llsr_s2s_batch (include/llsr.h): device pointers of one scan-to-scan batch."""
+    _fields_ = [
+        ("n_problems", C.c_int32),
+        ("sharp", C.c_void_p), ("sharp_off", C.c_void_p),
+        ("flat", C.c_void_p), ("flat_off", C.c_void_p),
+        ("corner_last", C.c_void_p), ("corner_last_off", C.c_void_p),
+        ("surf_last", C.c_void_p), ("surf_last_off", C.c_void_p),
+        ("transform_cur", C.c_void_p),
+        ("is_degenerate", C.c_void_p),
+        ("report", C.c_void_p),
+    ]
+
+
 class S2MBatch(C.Structure):
     """llsr_s2m_batch (include/llsr.h): device pointers of one scan-to-map batch."""
     _fields_ = [

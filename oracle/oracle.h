@@ -41,6 +41,16 @@ int32_t oracle_scan2map(const llsr_config* cfg, const float* corner_q, int32_t Q
  * liboracle: the 1 m grid; oracle/_ref/libref_mo.so exports the same as ref_knn5_batch /
  * ref_scan2map over the reference's nanoflann kd-tree. */
 int32_t oracle_knn5_batch(const float* map, int32_t M, const float* q, int32_t Q, int32_t* idx, float* d2);
+/* FeatureAssociation::updateTransformation (FA:2505-2535) on explicit clouds (see llsr.h).
+ * transform_cur and is_degenerate are in/out (member state of the reference node). */
+int32_t oracle_scan2scan(const llsr_config* cfg, const float* sharp, int32_t n_sharp, const float* flat,
+                         int32_t n_flat, const float* corner_last, int32_t n_corner_last,
+                         const float* surf_last, int32_t n_surf_last, float* transform_cur,
+                         int32_t* is_degenerate, llsr_s2s_report* rep);
+/* TransformToEnd (FA:1414-1490, no-IMU branch) of n float4 points in place. */
+void oracle_transform_to_end(const float* transform_cur, float* xyzi, int32_t n);
+/* GenerateShadowPoint (FA:412-439). */
+void oracle_shadow_points(float* out_xyzi);
 /* Test hooks for the Eigen restatements (llsr_eigen.h): column-major inputs. */
 int32_t oracle_eig3(const float* A, float* evals, float* evecs);
 int32_t oracle_eig6(const float* A, float* evals, float* evecs);

@@ -29,7 +29,7 @@ def lib():
     global _LIB
     if _LIB is None:
         path = os.path.join(_HERE, "_build", "liboracle.so")
-        srcs = [os.path.join(_HERE, f) for f in ("oracle_ipfa.cpp", "oracle_mo.cpp")]
+        srcs = [os.path.join(_HERE, f) for f in ("oracle_ipfa.cpp", "oracle_mo.cpp", "oracle_fa_lm.cpp")]
         if not os.path.exists(path) or os.path.getmtime(path) < max(map(os.path.getmtime, srcs)):
             build()
         L = C.CDLL(path)
@@ -48,11 +48,17 @@ def lib():
         for f in ("oracle_qr_solve_5x3", "oracle_qr_solve_6x6"):
             getattr(L, f).argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         _bind_mo(L, "oracle_")
+        L.oracle_transform_to_end.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+        L.oracle_shadow_points.argtypes = [C.c_void_p]
         _LIB = L
     return _LIB
 
 
 def _bind_mo(L, prefix):
+    f = getattr(L, prefix + "scan2scan")
+    f.restype = C.c_int32
+    f.argtypes = [C.POINTER(_abi.Config), C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32,
+                  C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.POINTER(_abi.S2SReport)]
     f = getattr(L, prefix + "scan2map")
     f.restype = C.c_int32
     f.argtypes = [C.POINTER(_abi.Config), C.c_void_p, C.c_int32, C.c_void_p, C.c_int32,
@@ -185,3 +191,48 @@ def qr_solve(A: np.ndarray, b: np.ndarray) -> np.ndarray:
     f = lib().oracle_qr_solve_5x3 if A.shape == (5, 3) else lib().oracle_qr_solve_6x6
     f(a.ctypes.data, b.ctypes.data, x.ctypes.data)
     return x
+
+
+def scan2scan(cfg: _abi.Config, sharp, flat, corner_last, surf_last, transform_cur, is_degenerate: int = 0,
+              knn: str = "grid") -> dict:
+    """FeatureAssociation::updateTransformation (FA:2505-2535) on explicit clouds. knn: "grid"
+    (brute-force restatement) or "kdtree" (the reference's nanoflann, oracle/_ref)."""
+    a, b, c, d = (_f4(x) for x in (sharp, flat, corner_last, surf_last))
+    t = np.ascontiguousarray(transform_cur, dtype=np.float32).copy()
+    deg = C.c_int32(is_degenerate)
+    rep = _abi.S2SReport()
+    rc = _mo_fn("scan2scan", knn)(C.byref(cfg), a.ctypes.data, len(a), b.ctypes.data, len(b), c.ctypes.data, len(c),
+                                  d.ctypes.data, len(d), t.ctypes.data, C.byref(deg), C.byref(rep))
+    if rc != 0:
+        raise RuntimeError(f"oracle_scan2scan: {rc}")
+    out = rep.as_dict()
+    out["transform_cur"] = t
+    out["is_degenerate"] = deg.value
+    return out
+
+
+def transform_to_end(transform_cur, xyzi) -> np.ndarray:
+    p = _f4(xyzi).copy()
+    t = np.ascontiguousarray(transform_cur, dtype=np.float32)
+    lib().oracle_transform_to_end(t.ctypes.data, p.ctypes.data, len(p))
+    return p
+
+
+def shadow_points() -> np.ndarray:
+    out = np.zeros((160, 4), np.float32)
+    lib().oracle_shadow_points(out.ctypes.data)
+    return out
+
+
+def fa_lm_inputs(prev: dict, cur: dict, transform_prev=None):
+    """(sharp, flat, corner_last, surf_last) for the scan-to-scan LM from two consecutive
+    feature-stage outputs (oracle/product result dicts), as runFeatureAssociation builds them:
+    flat += shadow points (FA:1310-1314); last clouds = TransformToEnd(prev less-sharp / less-flat)
+    + shadow points on the surf side (FA:2666-2707)."""
+    sh = shadow_points()
+    tp = np.zeros(6, np.float32) if transform_prev is None else transform_prev
+    sharp = cur["loam_xyzi"][cur["sharp_ind"]]
+    flat = np.concatenate([cur["loam_xyzi"][cur["flat_ind"]], sh])
+    corner_last = transform_to_end(tp, prev["loam_xyzi"][prev["less_sharp_ind"]])
+    surf_last = np.concatenate([transform_to_end(tp, prev["less_flat_xyzi"]), sh])
+    return sharp, flat, corner_last, surf_last

@@ -1,0 +1,121 @@
+"""GPU parity of the scan-to-scan LM (FeatureAssociation::updateTransformation, FA:2505-2535).
+
+HIP path (llsr_scan2scan / llsr_scan2scan_batch) against the oracle (oracle/oracle_fa_lm.cpp)
+on consecutive synthetic VLP-16 scans: the inputs are the oracle's own feature-stage outputs
+(bit-exact with the HIP feature stage, tests/test_gpu_parity.py) assembled as
+runFeatureAssociation does (oracle_py.fa_lm_inputs). The device sums the normal equations in
+the oracle's correspondence order, so the bar is bit-exact: transformCur, iteration counts,
+correspondence counts and the degeneracy flag all equal.
+"""
+import numpy as np
+import pytest
+
+import oracle_py
+from llsr import Pipeline, _abi, default_config, shadow_points, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _pairs(lidar, seeds, horizontal=None):
+    cfg = default_config(lidar, horizontal)
+    ora = oracle_py.Oracle(cfg)
+    prev = ora.process(synth.make_scan(seeds[0], lidar))
+    out = []
+    for s in seeds[1:]:
+        cur = ora.process(synth.make_scan(s, lidar))
+        out.append(oracle_py.fa_lm_inputs(prev, cur))
+        prev = cur
+    return cfg, out
+
+
+def _same(g, o):
+    errs = []
+    if not np.array_equal(g["transform_cur"], o["transform_cur"]):
+        errs.append(f"transform_cur {g['transform_cur']} vs {o['transform_cur']} "
+                    f"(max |d| {np.abs(g['transform_cur'] - o['transform_cur']).max():.3g})")
+    for k in ("surf_iterations", "corner_iterations", "n_surf_corr", "n_corner_corr", "degenerate", "skipped"):
+        if g[k] != o[k]:
+            errs.append(f"{k} {g[k]} vs {o[k]}")
+    return errs
+
+
+def test_shadow_points_match_oracle(require_gpu):
+    np.testing.assert_array_equal(shadow_points(), oracle_py.shadow_points())
+
+
+@pytest.mark.parametrize("lidar,seeds,horizontal", [("vlp16", [1, 2, 3, 4, 5, 70], None),
+                                                    ("hdl64e", [5, 6, 7], 2048)])
+def test_scan2scan_bit_exact(require_gpu, lidar, seeds, horizontal):
+    cfg, pairs = _pairs(lidar, seeds, horizontal)
+    pipe = Pipeline(cfg)
+    errs = []
+    t = np.zeros(6, np.float32)
+    for k, (sharp, flat, cl, sl) in enumerate(pairs):
+        g = pipe.scan2scan(sharp, flat, cl, sl, t, 0)
+        o = oracle_py.scan2scan(cfg, sharp, flat, cl, sl, t, 0)
+        errs += [f"pair {k}: {e}" for e in _same(g, o)]
+        t = o["transform_cur"] * np.float32(0.5)  # a non-zero initial guess for the next pair
+    pipe.close()
+    assert not errs, "\n".join(errs)
+
+
+def test_scan2scan_batch_and_skip(require_gpu):
+    import torch
+    cfg, pairs = _pairs("vlp16", [11, 12, 13, 14, 15])
+    # problem 4: a last corner cloud below the FA:2506 guard -> skipped, transform untouched
+    pairs.append((pairs[0][0], pairs[0][1], pairs[0][2][:9], pairs[0][3]))
+    P = len(pairs)
+    t0 = np.random.default_rng(3).uniform(-0.01, 0.01, (P, 6)).astype(np.float32)
+
+    def pack(k):
+        arrs = [pr[k] for pr in pairs]
+        off = np.zeros(P + 1, np.int64)
+        off[1:] = np.cumsum([len(a) for a in arrs])
+        return torch.from_numpy(np.concatenate(arrs)).cuda(), torch.from_numpy(off).cuda()
+
+    (sh, sho), (fl, flo), (cl, clo), (sl, slo) = (pack(k) for k in range(4))
+    tc = torch.from_numpy(t0.copy()).cuda()
+    deg = torch.zeros(P, dtype=torch.int32).cuda()
+    import ctypes
+    rep = torch.zeros(P * ctypes.sizeof(_abi.S2SReport) // 4, dtype=torch.float32).cuda()
+    pipe = Pipeline(cfg)
+    pipe.scan2scan_reserve(P, *(max(len(pr[k]) for pr in pairs) for k in range(4)))
+    torch.cuda.synchronize()
+    pipe.scan2scan_batch(dict(sharp=sh.data_ptr(), sharp_off=sho.data_ptr(), flat=fl.data_ptr(), flat_off=flo.data_ptr(),
+                              corner_last=cl.data_ptr(), corner_last_off=clo.data_ptr(), surf_last=sl.data_ptr(),
+                              surf_last_off=slo.data_ptr(), transform_cur=tc.data_ptr(),
+                              is_degenerate=deg.data_ptr(), report=rep.data_ptr()), P)
+    pipe.scan2scan_check()
+    tg = tc.cpu().numpy()
+    raw = rep.cpu().numpy().tobytes()
+    n = ctypes.sizeof(_abi.S2SReport)
+    pipe.close()
+    for p, pr in enumerate(pairs):
+        o = oracle_py.scan2scan(cfg, *pr, t0[p], 0)
+        g = _abi.S2SReport.from_buffer_copy(raw[p * n:(p + 1) * n]).as_dict()
+        g["transform_cur"] = tg[p]
+        assert not _same(g, o), (p, _same(g, o))
+    assert _abi.S2SReport.from_buffer_copy(raw[(P - 1) * n:P * n]).skipped == 1
+    np.testing.assert_array_equal(tg[P - 1], t0[P - 1])
+
+
+def test_scan2scan_capacity_error(require_gpu):
+    import torch
+    from llsr import LlsrError
+    cfg, pairs = _pairs("vlp16", [21, 22])
+    sharp, flat, cl, sl = pairs[0]
+    pipe = Pipeline(cfg)
+    pipe.scan2scan_reserve(1, 8, 8, 8, 8)
+    d = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (sharp, flat, cl, sl)]
+    o = [torch.tensor([0, len(a)], dtype=torch.int64).cuda() for a in (sharp, flat, cl, sl)]
+    tc = torch.zeros(6).cuda()
+    deg = torch.zeros(1, dtype=torch.int32).cuda()
+    rep = torch.zeros(64).cuda()
+    torch.cuda.synchronize()
+    pipe.scan2scan_batch(dict(sharp=d[0].data_ptr(), sharp_off=o[0].data_ptr(), flat=d[1].data_ptr(),
+                              flat_off=o[1].data_ptr(), corner_last=d[2].data_ptr(), corner_last_off=o[2].data_ptr(),
+                              surf_last=d[3].data_ptr(), surf_last_off=o[3].data_ptr(), transform_cur=tc.data_ptr(),
+                              is_degenerate=deg.data_ptr(), report=rep.data_ptr()), 1)
+    with pytest.raises(LlsrError):
+        pipe.scan2scan_check()
+    pipe.close()
