@@ -122,11 +122,12 @@ def scan2map_leg(dev, mode_name: str, P: int, steps: int, warmup: int, dist, run
                 surf_q_off=sqo.data_ptr(), corner_map=dcm.data_ptr(), corner_map_off=cmo.data_ptr(),
                 surf_map=dsm.data_ptr(), surf_map_off=smo.data_ptr(), pose=pose.data_ptr(),
                 report=rep.data_ptr())
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)  # the pose reset and the batch on one (non-default) stream
 
     def step():
-        pose.copy_(pose0)  # every step solves the same P problems from their start poses
-        pipe.scan2map_batch(ptrs, P, stream.cuda_stream)
+        with torch.cuda.stream(stream):
+            pose.copy_(pose0)  # every step solves the same P problems from their start poses
+            pipe.scan2map_batch(ptrs, P, stream.cuda_stream)
 
     for _ in range(warmup):
         step()
@@ -210,6 +211,85 @@ def scan2map_leg(dev, mode_name: str, P: int, steps: int, warmup: int, dist, run
     return out
 
 
+def scan2map_allreduce_leg(dev, P: int, steps: int, warmup: int, dist, check: bool) -> dict:
+    """configs[4]: B = P scans per step, every scan's scan-to-map correspondences split over all
+    ranks (llsr_scan2map_shard_*), ONE RCCL all-reduce of the [P][32] int64 normal equations per
+    LM iteration (llsr.dist.sharded_scan2map); every rank solves the same 6x6 systems. The total
+    work is fixed as N grows (strong scaling of one batch); at N = 1 no collective runs."""
+    import torch
+    from llsr import Pipeline, _abi, default_config
+    from llsr.dist import HipShardEngine, allreduce_latency_us, max_over_ranks, sharded_scan2map
+    z = np.load(os.path.join(REPO, "tests", "golden", "mo_map_vlp16.npz"))
+    nq = int(z["n_queries"])
+    cfg = default_config("vlp16")
+    cfg.mode = _abi.LLSR_MODE_LM_APPLIED
+    rng = np.random.default_rng(7)
+    probs = []
+    for p in range(P):
+        q = p % nq
+        pose = z[f"q{q}_true"] + np.concatenate([rng.uniform(-0.05, 0.05, 3), rng.uniform(-0.2, 0.2, 3)])
+        probs.append((z[f"q{q}_corner"], z[f"q{q}_surf"], z["corner_map"], z["surf_map"], pose.astype(np.float32)))
+
+    def pack(k):
+        arrs = [pr[k] for pr in probs]
+        off = np.zeros(P + 1, np.int64)
+        off[1:] = np.cumsum([len(a) for a in arrs])
+        return torch.from_numpy(np.concatenate(arrs)).to(dev), torch.from_numpy(off).to(dev)
+
+    (cq, cqo), (sq, sqo), (dcm, cmo), (dsm, smo) = (pack(k) for k in range(4))
+    pose0 = torch.from_numpy(np.stack([pr[4] for pr in probs])).to(dev)
+    pose = pose0.clone()
+    rep = torch.zeros((P, ctypes_sizeof_report() // 4), dtype=torch.float32, device=dev)
+    pipe = Pipeline(cfg, device=dev)
+    pipe.scan2map_reserve(P, len(z["corner_map"]), len(z["surf_map"]), max(len(pr[0]) for pr in probs),
+                          max(len(pr[1]) for pr in probs))
+    ptrs = dict(corner_q=cq.data_ptr(), corner_q_off=cqo.data_ptr(), surf_q=sq.data_ptr(),
+                surf_q_off=sqo.data_ptr(), corner_map=dcm.data_ptr(), corner_map_off=cmo.data_ptr(),
+                surf_map=dsm.data_ptr(), surf_map_off=smo.data_ptr(), pose=pose.data_ptr(),
+                report=rep.data_ptr())
+    side = torch.cuda.Stream(dev)  # torch's ops, the library's kernels and RCCL on one stream
+    ctx = torch.cuda.stream(side)
+    ctx.__enter__()
+    eng = HipShardEngine(pipe, ptrs, P, side.cuda_stream)
+    ne = eng.new_ne(dev)
+    iters = []
+
+    def step():
+        pose.copy_(pose0)
+        iters.append(sharded_scan2map(eng, ne, cfg.iterCountThres, poll=2))
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    el = max_over_ranks(time.perf_counter() - t0, dev)
+    lat = allreduce_latency_us(ne)
+    ctx.__exit__(None, None, None)
+    out = {"workload": f"configs[4]: {P} scans per step, each scan's scan-to-map correspondences split over "
+                       "all ranks, one all-reduce of the [P][32] int64 normal equations per LM iteration "
+                       "(lm_applied, ~76k-point local map)",
+           "value": round(P * steps / el, 1), "unit": "scans/s", "scaling": "strong",
+           "scans_per_step": P, "steps": steps, "ms_per_step": round(el / steps * 1e3, 3),
+           "lm_iterations_per_step": float(np.mean(iters[warmup:] if len(iters) > warmup else iters)),
+           "allreduce_bytes": P * 32 * 8, "allreduce_us": round(lat, 2)}
+    if check:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle_py
+        poses = pose.cpu().numpy()
+        out["pose_delta_max"] = max(float(np.abs(poses[p] - oracle_py.scan2map(cfg, *probs[p])["pose"]).max())
+                                    for p in range(min(P, nq)))
+    pipe.close()
+    return out
+
+
 def ctypes_sizeof_report() -> int:
     import ctypes
     from llsr import _abi
@@ -230,6 +310,8 @@ def main():
     ap.add_argument("--s2m-problems", type=int, default=256, help="scan-to-map problems per GPU per step")
     ap.add_argument("--s2m-steps", type=int, default=5)
     ap.add_argument("--s2m-modes", default="lm_applied,faithful", help="comma list; empty = skip the leg")
+    ap.add_argument("--allreduce-scans", type=int, default=8,
+                    help="configs[4] leg: scans per step split over all ranks (0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -331,6 +413,11 @@ def main():
                                       rank == 0 and not args.no_cpu and world == 1,
                                       min(args.cpu_seconds, 12.0))
 
+    allred = None
+    if args.allreduce_scans > 0:
+        allred = scan2map_allreduce_leg(dev, args.allreduce_scans, args.s2m_steps, 1, dist,
+                                        rank == 0 and not args.no_cpu)
+
     if rank == 0:
         out = {
             "metric": "scans/sec (VLP-16 1800x16) at 1/2/4/8 GPUs; pose delta vs CPU ref",
@@ -360,6 +447,7 @@ def main():
             "parity_spot_check_slot0": parity,
             "pose_delta": s2m.get("lm_applied", {}).get("pose_delta_max"),
             "scan2map": s2m,
+            "scan2map_allreduce": allred,
         }
         if not args.no_cpu and world == 1:
             scans = [pts[off[k]:off[k + 1]] for k in range(min(args.distinct, B))]

@@ -252,6 +252,31 @@ typedef struct llsr_s2m_stats {
   float iterate_ms;            /* first to last LM launch incl. the host's convergence polls, summed */
 } llsr_s2m_stats;
 int32_t llsr_scan2map_stats(llsr_handle* h, llsr_s2m_stats* out);
+/* ---- Split-correspondence scan-to-map for multi-GPU (BASELINE.json configs[4]) ----
+ * The optimisation of llsr_scan2map_batch driven one LM iteration at a time, so that the
+ * per-problem normal equations can be summed across GPUs between the Jacobian build and the
+ * solve. Rank r of W evaluates only its share of every problem's queries (256-query blocks b of
+ * each kind with b % W == r) and writes int64 fixed-point partial sums, LLSR_NE_WORDS per
+ * problem: AtA upper triangle (21, row-major), AtB (6), sum |coeff.intensity|, #corner, #surf
+ * correspondences, 2 spare; every term is rounded once to a multiple of 2^-30 before it is
+ * added. Integer sums are associative, so the summed words, and therefore every pose, are
+ * bit-identical for any W and any all-reduce order (they differ from llsr_scan2map_batch's float
+ * sums only by that rounding: well inside the 1e-4 pose tolerance). Per batch:
+ *   llsr_scan2map_shard_begin(h, batch, stream)              (reserve as for llsr_scan2map_batch)
+ *   up to iterCountThres times:
+ *     llsr_scan2map_shard_partial(h, r, W, d_ne, stream)     d_ne: int64 [P][LLSR_NE_WORDS], device
+ *     the caller sums d_ne over the W ranks in place (e.g. an RCCL all-reduce on `stream`)
+ *     llsr_scan2map_shard_step(h, d_ne, &n_active, stream)   n_active NULL: no host sync
+ *     stop once n_active == 0 (every rank sees the same count: no extra collective)
+ *   llsr_scan2map_shard_end(h, stream)                        pose + report into the batch arrays
+ * A handle holds one scan-to-map batch at a time (llsr_scan2map_batch / llsr_scan2map close an
+ * open shard batch). */
+#define LLSR_NE_WORDS 32
+int32_t llsr_scan2map_shard_begin(llsr_handle* h, const llsr_s2m_batch* batch, void* hip_stream);
+int32_t llsr_scan2map_shard_partial(llsr_handle* h, int32_t rank, int32_t world, int64_t* d_ne, void* hip_stream);
+int32_t llsr_scan2map_shard_step(llsr_handle* h, const int64_t* d_ne, int32_t* n_active, void* hip_stream);
+int32_t llsr_scan2map_shard_end(llsr_handle* h, void* hip_stream);
+
 /* One problem from host buffers (the reference's call shape: scan2MapOptimization on the
  * member clouds); reserves as needed; `pose` in/out; rep->ms = device time. */
 int32_t llsr_scan2map(llsr_handle* h, const float* corner_q, int32_t n_corner_q, const float* surf_q,

@@ -80,6 +80,8 @@ struct llsr_handle {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     hipEvent_t p0 = nullptr, p1 = nullptr, p2 = nullptr;  // profiling: start, grid built, LM done
     llsr_s2m_stats stats{};
+    S2MArgs sh{};                // the open split-correspondence batch (llsr_scan2map_shard_*)
+    bool sh_live = false;
   } mo;
   // scan-to-scan (llsr_scan2scan_*)
   struct {
@@ -544,6 +546,7 @@ extern "C" int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t P, int32_t mc, 
     HIP_OK(h, hipFree(m.pool));
     m.pool = nullptr;
   }
+  m.sh_live = false;
   m.P = P; m.mc = mc; m.ms = ms; m.qc = qc; m.qs = qs;
   m.log2T_c = grid_log2_table(mc);
   m.log2T_s = grid_log2_table(ms);
@@ -591,17 +594,15 @@ extern "C" int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t P, int32_t mc, 
   return LLSR_OK;
 }
 
-extern "C" int32_t llsr_scan2map_batch(llsr_handle* h, const llsr_s2m_batch* b, void* hip_stream) {
-  if (!h || !b) return fail(h, LLSR_EINVAL, "null argument");
+// Validate a scan-to-map batch and enqueue the per-problem setup and both cell-grid builds.
+static int32_t s2m_prepare(llsr_handle* h, const llsr_s2m_batch* b, hipStream_t s, S2MArgs& a) {
   auto& m = h->mo;
   if (!m.pool) return fail(h, LLSR_EINVAL, "llsr_scan2map_reserve not called");
   const int P = b->n_problems;
   if (P < 1 || P > m.P) return fail(h, LLSR_ERANGE, "n_problems outside [1, reserved]");
   if (!b->corner_q_off || !b->surf_q_off || !b->corner_map_off || !b->surf_map_off || !b->pose || !b->report)
     return fail(h, LLSR_EINVAL, "null batch array");
-  HIP_OK(h, hipSetDevice(h->device));
-  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
-  S2MArgs a = m.a;
+  a = m.a;
   a.P = P;
   a.applied = h->cfg.mode == LLSR_MODE_LM_APPLIED;
   a.iter_max = h->cfg.iterCountThres;
@@ -613,7 +614,9 @@ extern "C" int32_t llsr_scan2map_batch(llsr_handle* h, const llsr_s2m_batch* b, 
   a.sm = b->surf_map; a.sm_off = b->surf_map_off;
   a.pose = b->pose;
   a.report = b->report;
-  if (h->profiling) HIP_OK(h, hipEventRecord(m.p0, s));
+  a.rank = 0;
+  a.world = 1;
+  a.ne = nullptr;
   HIP_OK(h, hipMemsetAsync(a.n_active, 0, 2 * sizeof(int), s));
   a.grids.P = P;
   a.grids.g[0].src = reinterpret_cast<const float4*>(b->corner_map);
@@ -623,6 +626,20 @@ extern "C" int32_t llsr_scan2map_batch(llsr_handle* h, const llsr_s2m_batch* b, 
   k_s2m_setup<<<(P + 63) / 64, 64, 0, s>>>(a);
   grid_build(a.grids, s);
   HIP_OK(h, hipGetLastError());
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_scan2map_batch(llsr_handle* h, const llsr_s2m_batch* b, void* hip_stream) {
+  if (!h || !b) return fail(h, LLSR_EINVAL, "null argument");
+  auto& m = h->mo;
+  HIP_OK(h, hipSetDevice(h->device));
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+  if (h->profiling && m.pool) HIP_OK(h, hipEventRecord(m.p0, s));
+  S2MArgs a{};
+  m.sh_live = false;  // one scan-to-map batch per handle at a time: this one replaces a shard batch
+  int32_t rc = s2m_prepare(h, b, s, a);
+  if (rc != LLSR_OK) return rc;
+  const int P = a.P;
   if (h->profiling) HIP_OK(h, hipEventRecord(m.p1, s));
   // LM iterations; poll the active count every `poll` launches
   const int poll = 4;
@@ -654,6 +671,74 @@ extern "C" int32_t llsr_scan2map_batch(llsr_handle* h, const llsr_s2m_batch* b, 
     m.stats.grid_ms += g;
     m.stats.iterate_ms += it;
   }
+  return LLSR_OK;
+}
+
+// ---- split-correspondence scan-to-map (llsr_scan2map_shard_*): the LM loop is the caller's,
+// so the per-problem normal equations can be all-reduced across GPUs between the Jacobian build
+// (llsr_scan2map_shard_partial) and the solve (llsr_scan2map_shard_step).
+
+extern "C" int32_t llsr_scan2map_shard_begin(llsr_handle* h, const llsr_s2m_batch* b, void* hip_stream) {
+  if (!h || !b) return fail(h, LLSR_EINVAL, "null argument");
+  HIP_OK(h, hipSetDevice(h->device));
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+  auto& m = h->mo;
+  m.sh_live = false;
+  int32_t rc = s2m_prepare(h, b, s, m.sh);
+  if (rc != LLSR_OK) return rc;
+  m.sh_live = true;
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_scan2map_shard_partial(llsr_handle* h, int32_t rank, int32_t world, int64_t* d_ne,
+                                               void* hip_stream) {
+  if (!h || !d_ne) return fail(h, LLSR_EINVAL, "null argument");
+  auto& m = h->mo;
+  if (!m.sh_live) return fail(h, LLSR_EINVAL, "llsr_scan2map_shard_begin not called");
+  if (world < 1 || rank < 0 || rank >= world) return fail(h, LLSR_EINVAL, "rank outside [0, world)");
+  HIP_OK(h, hipSetDevice(h->device));
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+  S2MArgs a = m.sh;
+  a.rank = rank;
+  a.world = world;
+  a.ne = reinterpret_cast<long long*>(d_ne);
+  HIP_OK(h, hipMemsetAsync(d_ne, 0, sizeof(int64_t) * LLSR_NE_WORDS * (size_t)a.P, s));
+  const int bs = m.blocks - m.blocks_c;
+  const int nb = (m.blocks_c + world - 1) / world + (bs + world - 1) / world;
+  if (nb > 0) k_s2m_iter_fx<<<dim3(nb, a.P), 256, 0, s>>>(a);
+  HIP_OK(h, hipGetLastError());
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_scan2map_shard_step(llsr_handle* h, const int64_t* d_ne, int32_t* n_active,
+                                            void* hip_stream) {
+  if (!h || !d_ne) return fail(h, LLSR_EINVAL, "null argument");
+  auto& m = h->mo;
+  if (!m.sh_live) return fail(h, LLSR_EINVAL, "llsr_scan2map_shard_begin not called");
+  HIP_OK(h, hipSetDevice(h->device));
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+  S2MArgs a = m.sh;
+  a.ne = const_cast<long long*>(reinterpret_cast<const long long*>(d_ne));
+  k_s2m_solve_fx<<<(a.P + 63) / 64, 64, 0, s>>>(a);
+  HIP_OK(h, hipGetLastError());
+  if (n_active) {
+    HIP_OK(h, hipMemcpyAsync(m.host_flags, a.n_active, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_OK(h, hipStreamSynchronize(s));
+    if (m.host_flags[1]) return fail(h, LLSR_ERANGE, "a scan2map cloud exceeds the reserved capacity or has bad offsets");
+    *n_active = m.host_flags[0];
+  }
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_scan2map_shard_end(llsr_handle* h, void* hip_stream) {
+  if (!h) return LLSR_EINVAL;
+  auto& m = h->mo;
+  if (!m.sh_live) return fail(h, LLSR_EINVAL, "llsr_scan2map_shard_begin not called");
+  HIP_OK(h, hipSetDevice(h->device));
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+  k_s2m_finish<<<(m.sh.P + 63) / 64, 64, 0, s>>>(m.sh);
+  HIP_OK(h, hipGetLastError());
+  m.sh_live = false;
   return LLSR_OK;
 }
 

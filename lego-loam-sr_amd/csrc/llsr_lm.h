@@ -1,0 +1,101 @@
+// llsr_lm.h — LMOptimization's solve / degeneracy / pose update / stop test (MO:1453-1568) on
+// already-summed normal equations, and the int64 fixed-point words that the split-correspondence
+// scan-to-map sums across GPUs.
+//
+// Shared by the device (llsr_mo.hip: every scan-to-map path) and the oracle's split-sum
+// restatement (oracle/oracle_mo.cpp), so the step after the sums is one piece of code.
+#pragma once
+#include <stdint.h>
+
+#include "llsr_eigen.h"
+#include "llsr_libm.h"
+
+namespace llsr_lm {
+
+// Words per problem of the reduced normal equations: AtA upper triangle (21, row-major r <= c),
+// AtB (6), sum |coeff.intensity| (1), #corner, #surf correspondences (2), 2 spare.
+constexpr int kNeWords = 32;
+constexpr int kRed = 30;
+
+// Fixed point for the exchanged sums: every per-correspondence term is rounded once to a
+// multiple of 2^-30 and the sums are plain int64 additions — associative, so any split of the
+// correspondences over blocks / GPUs and any all-reduce order give identical words. Headroom:
+// sum |term| < 2^33 (e.g. 20k correspondences with |J|^2 up to 4e5, points ~600 m away).
+constexpr double kNeScale = 1073741824.0;  // 2^30
+
+LLSR_HD long long ne_fix(float v) { return (long long)__builtin_rint((double)v * kNeScale); }
+LLSR_HD float ne_unfix(long long w) { return (float)((double)w / kNeScale); }
+// Word k of one correspondence: the counts (28, 29) stay plain integers.
+LLSR_HD long long ne_term(int k, float v) { return k >= 28 ? (long long)v : ne_fix(v); }
+
+// Summed words -> the float reduction vector lm_update consumes.
+LLSR_HD void ne_to_red(const long long* w, float* red) {
+  for (int k = 0; k < 28; ++k) red[k] = ne_unfix(w[k]);
+  red[28] = (float)w[28];
+  red[29] = (float)w[29];
+}
+
+// One LMOptimization after the Jacobian build (MO:1453-1568) for a problem whose N = nc + ns
+// >= 50 (the caller checks MO:1453). St provides pose[6], cR/sR/cP/sP/cY/sY (cached cos / sin
+// of pose[0..2]), matP[36], matX0[6], min_lambda, cf_mean, degenerate. `red`: AtA upper
+// triangle (21), AtB (6), sum |d|, #corner, #surf. Returns the stop test (MO:1562-1566).
+template <class St>
+LLSR_HD bool lm_update(St& st, const float* red, int iterCount, bool applied, float stop_thres) {
+  using llsr_libm::cosf_;
+  using llsr_libm::sinf_;
+  const int N = (int)red[28] + (int)red[29];
+  float AtA[36], AtB[6];
+  int q = 0;
+  for (int r = 0; r < 6; ++r)
+    for (int c = r; c < 6; ++c, ++q) { AtA[r + 6 * c] = red[q]; AtA[c + 6 * r] = red[q]; }
+  for (int c = 0; c < 6; ++c) AtB[c] = red[21 + c];
+  float X[6];
+  llsr_eigen::colpiv_qr_solve<6, 6>(AtA, AtB, X);
+  if (iterCount == 0) {  // MO:1507-1537
+    float E[6], V[36], V2[36];
+    llsr_eigen::eig_sym<6>(AtA, E, V);
+    st.min_lambda = E[0];
+    for (int k = 0; k < 36; ++k) V2[k] = V[k];
+    bool deg = false;
+    for (int i = 5; i >= 0; --i) {
+      if (E[i] < 100) {
+        for (int j = 0; j < 6; ++j) V2[i + 6 * j] = 0;
+        deg = true;
+      } else {
+        break;
+      }
+    }
+    st.degenerate = deg ? 1 : 0;
+    for (int r = 0; r < 6; ++r)  // matV.inverse() * matV2, V orthonormal: V^T * V2
+      for (int c = 0; c < 6; ++c) {
+        float acc = 0;
+        for (int k = 0; k < 6; ++k) acc += V[k + 6 * r] * V2[k + 6 * c];
+        st.matP[r + 6 * c] = acc;
+      }
+    for (int k = 0; k < 6; ++k) st.matX0[k] = X[k];
+  }
+  if (st.degenerate) {
+    float X2[6];
+    for (int k = 0; k < 6; ++k) X2[k] = X[k];
+    for (int r = 0; r < 6; ++r) {
+      float acc = 0;
+      for (int k = 0; k < 6; ++k) acc += st.matP[r + 6 * k] * X2[k];
+      X[r] = acc;
+    }
+  }
+  if (applied) {  // MO:1539-1545 (commented out in the reference: faithful mode skips it)
+    for (int k = 0; k < 6; ++k) st.pose[k] += X[k];
+    st.cR = cosf_(st.pose[0]); st.sR = sinf_(st.pose[0]);
+    st.cP = cosf_(st.pose[1]); st.sP = sinf_(st.pose[1]);
+    st.cY = cosf_(st.pose[2]); st.sY = sinf_(st.pose[2]);
+  }
+  const float r2d = 57.29577951308232f;  // pcl::rad2deg(float)
+  const double e0 = (double)(X[0] * r2d), e1 = (double)(X[1] * r2d), e2 = (double)(X[2] * r2d);
+  const double t0 = (double)(X[3] * 100), t1 = (double)(X[4] * 100), t2 = (double)(X[5] * 100);
+  const float deltaR = (float)__builtin_sqrt(e0 * e0 + e1 * e1 + e2 * e2);
+  const float deltaT = (float)__builtin_sqrt(t0 * t0 + t1 * t1 + t2 * t2);
+  st.cf_mean = red[27] / (float)N;
+  return deltaR < stop_thres && deltaT < stop_thres;
+}
+
+}  // namespace llsr_lm

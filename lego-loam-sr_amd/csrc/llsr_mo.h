@@ -39,11 +39,16 @@ struct S2MArgs {
   float* partial;              // [P][blocks][32] block sums
   int* n_active;               // problems still iterating
   int* error;                  // capacity / offset violations
+  // split-correspondence mode (llsr_scan2map_shard_*): this rank's share of the query blocks
+  int rank, world;
+  long long* ne;               // [P][llsr_lm::kNeWords] int64 fixed-point sums
 };
 
 __global__ void k_s2m_setup(S2MArgs a);
 __global__ void k_s2m_iter(S2MArgs a);
 __global__ void k_s2m_solve(S2MArgs a);
 __global__ void k_s2m_finish(S2MArgs a);
+__global__ void k_s2m_iter_fx(S2MArgs a);
+__global__ void k_s2m_solve_fx(S2MArgs a);
 
 }  // namespace llsr

@@ -33,6 +33,7 @@
 #include "llsr_device.h"
 #include "llsr_eigen.h"
 #include "llsr_grid.h"
+#include "llsr_lm.h"
 #include "llsr_mo.h"
 
 namespace llsr {
@@ -199,72 +200,18 @@ __global__ void k_s2m_setup(S2MArgs a) {
   if (st.active) atomicAdd(a.n_active, 1);
 }
 
-// Values reduced per block: AtA upper triangle (21), AtB (6), sum |coeff.intensity|, #corner,
-// #surf.
-constexpr int kRed = 30;
+using llsr_lm::kRed;
 
 __device__ void lm_step(const S2MArgs& a, S2MProb& st, const float* red) {
-  // LMOptimization (MO:1444-1570) after the Jacobian build.
+  // LMOptimization (MO:1444-1570) after the Jacobian build; the solve / update / stop test is
+  // llsr_lm::lm_update (shared with the oracle's split-sum restatement).
   st.iter += 1;
   const int iterCount = st.iter - 1;
-  const int nc = (int)red[28], ns = (int)red[29];
-  st.nc = nc; st.ns = ns;
-  const int N = nc + ns;
+  st.nc = (int)red[28];
+  st.ns = (int)red[29];
   bool conv = false;
-  if (N >= 50) {  // MO:1453
-    float AtA[36], AtB[6];
-    int q = 0;
-    for (int r = 0; r < 6; ++r)
-      for (int c = r; c < 6; ++c, ++q) { AtA[r + 6 * c] = red[q]; AtA[c + 6 * r] = red[q]; }
-    for (int c = 0; c < 6; ++c) AtB[c] = red[21 + c];
-    float X[6];
-    llsr_eigen::colpiv_qr_solve<6, 6>(AtA, AtB, X);
-    if (iterCount == 0) {
-      float E[6], V[36], V2[36];
-      llsr_eigen::eig_sym<6>(AtA, E, V);
-      st.min_lambda = E[0];
-      for (int k = 0; k < 36; ++k) V2[k] = V[k];
-      bool deg = false;
-      for (int i = 5; i >= 0; --i) {
-        if (E[i] < 100) {
-          for (int j = 0; j < 6; ++j) V2[i + 6 * j] = 0;
-          deg = true;
-        } else {
-          break;
-        }
-      }
-      st.degenerate = deg ? 1 : 0;
-      for (int r = 0; r < 6; ++r)  // matV.inverse() * matV2, V orthonormal: V^T * V2
-        for (int c = 0; c < 6; ++c) {
-          float acc = 0;
-          for (int k = 0; k < 6; ++k) acc += V[k + 6 * r] * V2[k + 6 * c];
-          st.matP[r + 6 * c] = acc;
-        }
-      for (int k = 0; k < 6; ++k) st.matX0[k] = X[k];
-    }
-    if (st.degenerate) {
-      float X2[6];
-      for (int k = 0; k < 6; ++k) X2[k] = X[k];
-      for (int r = 0; r < 6; ++r) {
-        float acc = 0;
-        for (int k = 0; k < 6; ++k) acc += st.matP[r + 6 * k] * X2[k];
-        X[r] = acc;
-      }
-    }
-    if (a.applied) {
-      for (int k = 0; k < 6; ++k) st.pose[k] += X[k];
-      st.cR = cosf_(st.pose[0]); st.sR = sinf_(st.pose[0]);
-      st.cP = cosf_(st.pose[1]); st.sP = sinf_(st.pose[1]);
-      st.cY = cosf_(st.pose[2]); st.sY = sinf_(st.pose[2]);
-    }
-    const float r2d = 57.29577951308232f;
-    const double e0 = (double)(X[0] * r2d), e1 = (double)(X[1] * r2d), e2 = (double)(X[2] * r2d);
-    const double t0 = (double)(X[3] * 100), t1 = (double)(X[4] * 100), t2 = (double)(X[5] * 100);
-    const float deltaR = (float)sqrt(e0 * e0 + e1 * e1 + e2 * e2);
-    const float deltaT = (float)sqrt(t0 * t0 + t1 * t1 + t2 * t2);
-    st.cf_mean = red[27] / (float)N;
-    conv = deltaR < a.stop_thres && deltaT < a.stop_thres;
-  }
+  if (st.nc + st.ns >= 50)  // MO:1453
+    conv = llsr_lm::lm_update(st, red, iterCount, a.applied != 0, a.stop_thres);
   if (conv) st.converged = 1;
   if (conv || st.iter >= a.iter_max) {
     st.active = 0;
@@ -272,60 +219,65 @@ __device__ void lm_step(const S2MArgs& a, S2MProb& st, const float* red) {
   }
 }
 
+// What one query contributes (cornerOptimization MO:1274-1375 / surfOptimization MO:1383-1440,
+// then the Jacobian row of LMOptimization MO:1465-1490): v[0..20] the AtA upper triangle,
+// v[21..26] AtB, v[27] |coeff.intensity|, v[28] / v[29] = 1 for a corner / surf
+// correspondence; all zero without one.
+template <bool kCorner>
+__device__ __forceinline__ void query_terms(const S2MArgs& a, const S2MProb& st, int p, int qi, float* v) {
+#pragma unroll
+  for (int k = 0; k < kRed; ++k) v[k] = 0.0f;
+  const int Q = kCorner ? st.Qc : st.Qs;
+  if (qi >= Q) return;
+  const float4 q = reinterpret_cast<const float4*>(kCorner ? a.cq : a.sq)[(kCorner ? st.qc0 : st.qs0) + qi];
+  Assoc as{st.cR, st.sR, st.cP, st.sP, st.cY, st.sY, st.pose[3], st.pose[4], st.pose[5]};
+  float x0, y0, z0;
+  as.apply(q.x, q.y, q.z, x0, y0, z0);
+  float la, lb, lc, ld;
+  bool ok;
+  if constexpr (kCorner) {
+    const float4* mp = reinterpret_cast<const float4*>(a.cm) + st.mc0;
+    ok = corner_coeff(a.grids.g[0].table(p), a.grids.g[0].log2T, a.grids.g[0].cells(p), mp,
+                      x0, y0, z0, la, lb, lc, ld);
+  } else {
+    const float4* mp = reinterpret_cast<const float4*>(a.sm) + st.ms0;
+    ok = surf_coeff(a.grids.g[1].table(p), a.grids.g[1].log2T, a.grids.g[1].cells(p), mp,
+                    x0, y0, z0, la, lb, lc, ld);
+  }
+  if (!ok) return;
+  // Jacobian row (MO:1465-1490) at the current pose; srx.. are the same sin/cos values
+  const float srx = st.sR, crx = st.cR, sry = st.sP, cry = st.cP, srz = st.sY, crz = st.cY;
+  const float px = q.x, py = q.y, pz = q.z;
+  const float arx = (crx * sry * srz * px + crx * crz * sry * py - srx * sry * pz) * la +
+                    (-srx * srz * px - crz * srx * py - crx * pz) * lb +
+                    (crx * cry * srz * px + crx * cry * crz * py - cry * srx * pz) * lc;
+  const float ary = ((cry * srx * srz - crz * sry) * px + (sry * srz + cry * crz * srx) * py + crx * cry * pz) * la +
+                    ((-cry * crz - srx * sry * srz) * px + (cry * srz - crz * srx * sry) * py - crx * sry * pz) * lc;
+  const float arz = ((crz * srx * sry - cry * srz) * px + (-cry * crz - srx * sry * srz) * py) * la +
+                    (crx * crz * px - crx * srz * py) * lb +
+                    ((sry * srz + cry * crz * srx) * px + (crz * sry - cry * srx * srz) * py) * lc;
+  const float J[6] = {arx, ary, arz, la, lb, lc};
+  const float bb = -a.step_size * ld;
+  int k = 0;
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int c = r; c < 6; ++c, ++k) v[k] = J[r] * J[c];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) v[21 + c] = J[c] * bb;
+  v[27] = fabs_(ld);
+  v[kCorner ? 28 : 29] = 1.0f;
+}
+
 // One block of queries: kCorner = corner queries (partial slots [0, blocks_c)), else surf queries
 // (partial slots [blocks_c, blocks)).
 template <bool kCorner>
 __device__ __forceinline__ void s2m_block(const S2MArgs& a, int p, int qb) {
-  S2MProb& st = a.prob[p];
+  const S2MProb& st = a.prob[p];
   if (!st.active) return;
   __shared__ float wsum[4][kRed];
-  constexpr bool corner = kCorner;
-  const int qi = qb * 256 + threadIdx.x;
   float v[kRed];
-#pragma unroll
-  for (int k = 0; k < kRed; ++k) v[k] = 0.0f;
-  const int Q = corner ? st.Qc : st.Qs;
-  if (qi < Q) {
-    const float4 q = reinterpret_cast<const float4*>(corner ? a.cq : a.sq)[(corner ? st.qc0 : st.qs0) + qi];
-    Assoc as{st.cR, st.sR, st.cP, st.sP, st.cY, st.sY, st.pose[3], st.pose[4], st.pose[5]};
-    float x0, y0, z0;
-    as.apply(q.x, q.y, q.z, x0, y0, z0);
-    float la, lb, lc, ld;
-    bool ok;
-    if constexpr (kCorner) {
-      const float4* mp = reinterpret_cast<const float4*>(a.cm) + st.mc0;
-      ok = corner_coeff(a.grids.g[0].table(p), a.grids.g[0].log2T, a.grids.g[0].cells(p), mp,
-                        x0, y0, z0, la, lb, lc, ld);
-    } else {
-      const float4* mp = reinterpret_cast<const float4*>(a.sm) + st.ms0;
-      ok = surf_coeff(a.grids.g[1].table(p), a.grids.g[1].log2T, a.grids.g[1].cells(p), mp,
-                      x0, y0, z0, la, lb, lc, ld);
-    }
-    if (ok) {
-      // Jacobian row (MO:1465-1490) at the current pose; srx.. are the same sin/cos values
-      const float srx = st.sR, crx = st.cR, sry = st.sP, cry = st.cP, srz = st.sY, crz = st.cY;
-      const float px = q.x, py = q.y, pz = q.z;
-      const float arx = (crx * sry * srz * px + crx * crz * sry * py - srx * sry * pz) * la +
-                        (-srx * srz * px - crz * srx * py - crx * pz) * lb +
-                        (crx * cry * srz * px + crx * cry * crz * py - cry * srx * pz) * lc;
-      const float ary = ((cry * srx * srz - crz * sry) * px + (sry * srz + cry * crz * srx) * py + crx * cry * pz) * la +
-                        ((-cry * crz - srx * sry * srz) * px + (cry * srz - crz * srx * sry) * py - crx * sry * pz) * lc;
-      const float arz = ((crz * srx * sry - cry * srz) * px + (-cry * crz - srx * sry * srz) * py) * la +
-                        (crx * crz * px - crx * srz * py) * lb +
-                        ((sry * srz + cry * crz * srx) * px + (crz * sry - cry * srx * srz) * py) * lc;
-      const float J[6] = {arx, ary, arz, la, lb, lc};
-      const float bb = -a.step_size * ld;
-      int k = 0;
-#pragma unroll
-      for (int r = 0; r < 6; ++r)
-#pragma unroll
-        for (int c = r; c < 6; ++c, ++k) v[k] = J[r] * J[c];
-#pragma unroll
-      for (int c = 0; c < 6; ++c) v[21 + c] = J[c] * bb;
-      v[27] = fabs_(ld);
-      v[corner ? 28 : 29] = 1.0f;
-    }
-  }
+  query_terms<kCorner>(a, st, p, qb * 256 + threadIdx.x, v);
   // fixed-order block reduction: wave butterfly, then waves 0..3 in order
   const int w = threadIdx.x >> 6;
 #pragma unroll
@@ -358,6 +310,55 @@ __global__ __launch_bounds__(64) void k_s2m_solve(S2MArgs a) {
   const float* pp = a.partial + (size_t)p * a.blocks * 32;
   for (int b = 0; b < a.blocks; ++b)
     for (int k = 0; k < kRed; ++k) red[k] += pp[(size_t)b * 32 + k];
+  lm_step(a, st, red);
+}
+
+// ---- split-correspondence mode (llsr_scan2map_shard_*) ----------------------
+// Every term is rounded once to int64 fixed point (llsr_lm::ne_term) and summed with integer
+// adds: the wave / block sums and the global atomics are exact, so the words do not depend on
+// how the queries are split over blocks or ranks, nor on the order the atomics land.
+template <bool kCorner>
+__device__ __forceinline__ void s2m_block_fx(const S2MArgs& a, int p, int qb) {
+  const S2MProb& st = a.prob[p];
+  if (!st.active) return;
+  __shared__ long long wsum[4][kRed];
+  float v[kRed];
+  query_terms<kCorner>(a, st, p, qb * 256 + threadIdx.x, v);
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < kRed; ++k) {
+    const long long s = wave_reduce_add(llsr_lm::ne_term(k, v[k]));
+    if (lane_id() == 0) wsum[w][k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < kRed) {
+    const int k = threadIdx.x;
+    const long long t = wsum[0][k] + wsum[1][k] + wsum[2][k] + wsum[3][k];
+    if (t != 0)
+      atomicAdd(reinterpret_cast<unsigned long long*>(a.ne + (size_t)p * llsr_lm::kNeWords + k),
+                (unsigned long long)t);
+  }
+}
+
+// grid (ceil(blocks_c / world) + ceil(blocks_s / world), P): rank r takes the corner blocks
+// r, r + world, ... and likewise the surf blocks.
+__global__ __launch_bounds__(256) void k_s2m_iter_fx(S2MArgs a) {
+  const int bcw = (a.blocks_c + a.world - 1) / a.world;
+  const int bx = blockIdx.x;
+  if (bx < bcw)
+    s2m_block_fx<true>(a, blockIdx.y, bx * a.world + a.rank);
+  else
+    s2m_block_fx<false>(a, blockIdx.y, (bx - bcw) * a.world + a.rank);
+}
+
+// One thread per problem: the summed words (all ranks) -> the LM step.
+__global__ __launch_bounds__(64) void k_s2m_solve_fx(S2MArgs a) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.P) return;
+  S2MProb& st = a.prob[p];
+  if (!st.active) return;
+  float red[kRed];
+  llsr_lm::ne_to_red(a.ne + (size_t)p * llsr_lm::kNeWords, red);
   lm_step(a, st, red);
 }
 

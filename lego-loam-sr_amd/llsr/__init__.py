@@ -35,7 +35,8 @@ EXPORTS = [
     "llsr_batch_counts", "llsr_kernel_times_ms", "llsr_kernel_name", "llsr_set_profiling",
     "llsr_scan2map_reserve", "llsr_scan2map_batch", "llsr_scan2map", "llsr_scan2map_stats",
     "llsr_shadow_points", "llsr_scan2scan_reserve", "llsr_scan2scan_batch", "llsr_scan2scan_check",
-    "llsr_scan2scan",
+    "llsr_scan2scan", "llsr_scan2map_shard_begin", "llsr_scan2map_shard_partial",
+    "llsr_scan2map_shard_step", "llsr_scan2map_shard_end",
 ]
 
 
@@ -78,6 +79,10 @@ def lib():
                                      C.POINTER(_abi.S2SReport)]
         L.llsr_scan2map.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p,
                                     C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(_abi.LmReport)]
+        L.llsr_scan2map_shard_begin.argtypes = [C.c_void_p, C.POINTER(_abi.S2MBatch), C.c_void_p]
+        L.llsr_scan2map_shard_partial.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
+        L.llsr_scan2map_shard_step.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int32), C.c_void_p]
+        L.llsr_scan2map_shard_end.argtypes = [C.c_void_p, C.c_void_p]
         for fn in EXPORTS:
             if fn not in ("llsr_last_error", "llsr_kernel_name", "llsr_destroy"):
                 getattr(L, fn).restype = C.c_int32
@@ -181,13 +186,39 @@ class Pipeline:
         d["pose"] = pose
         return d
 
-    def scan2map_batch(self, ptrs: dict, P: int, stream: int = 0):
-        """Device-resident batch: ptrs maps the llsr_s2m_batch field names to device pointers."""
+    @staticmethod
+    def _s2m_batch(ptrs: dict, P: int) -> _abi.S2MBatch:
         b = _abi.S2MBatch()
         b.n_problems = P
         for k, v in ptrs.items():
             setattr(b, k, v)
+        return b
+
+    def scan2map_batch(self, ptrs: dict, P: int, stream: int = 0):
+        """Device-resident batch: ptrs maps the llsr_s2m_batch field names to device pointers."""
+        b = self._s2m_batch(ptrs, P)
         self._check(lib().llsr_scan2map_batch(self._h, C.byref(b), C.c_void_p(stream)), "llsr_scan2map_batch")
+
+    # split-correspondence mode (llsr_scan2map_shard_*): the LM loop is the caller's (llsr.dist)
+    def scan2map_shard_begin(self, ptrs: dict, P: int, stream: int = 0):
+        b = self._s2m_batch(ptrs, P)
+        self._check(lib().llsr_scan2map_shard_begin(self._h, C.byref(b), C.c_void_p(stream)),
+                    "llsr_scan2map_shard_begin")
+
+    def scan2map_shard_partial(self, rank: int, world: int, d_ne: int, stream: int = 0):
+        self._check(lib().llsr_scan2map_shard_partial(self._h, rank, world, C.c_void_p(d_ne), C.c_void_p(stream)),
+                    "llsr_scan2map_shard_partial")
+
+    def scan2map_shard_step(self, d_ne: int, poll: bool, stream: int = 0) -> int:
+        """Solve from the summed words; with poll, sync and return the problems still active
+        (else -1)."""
+        n = C.c_int32(-1)
+        self._check(lib().llsr_scan2map_shard_step(self._h, C.c_void_p(d_ne), C.byref(n) if poll else None,
+                                                    C.c_void_p(stream)), "llsr_scan2map_shard_step")
+        return int(n.value)
+
+    def scan2map_shard_end(self, stream: int = 0):
+        self._check(lib().llsr_scan2map_shard_end(self._h, C.c_void_p(stream)), "llsr_scan2map_shard_end")
 
 
     def scan2map_stats(self) -> dict:

@@ -10,6 +10,7 @@ LLSR_LIDAR_VLP16 = 0
 LLSR_LIDAR_HDL64E = 2
 LLSR_MODE_FAITHFUL = 0
 LLSR_MODE_LM_APPLIED = 1
+NE_WORDS = 32  # LLSR_NE_WORDS: int64 words per problem exchanged by llsr_scan2map_shard_*
 
 
 class Config(C.Structure):

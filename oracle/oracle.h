@@ -47,6 +47,17 @@ int32_t oracle_scan2scan(const llsr_config* cfg, const float* sharp, int32_t n_s
                          int32_t n_flat, const float* corner_last, int32_t n_corner_last,
                          const float* surf_last, int32_t n_surf_last, float* transform_cur,
                          int32_t* is_degenerate, llsr_s2s_report* rep);
+/* Split-correspondence scan-to-map with int64 fixed-point normal equations: the CPU statement of
+ * llsr_scan2map_shard_* for one problem (see oracle_mo.cpp). partial() writes LLSR_NE_WORDS words
+ * for rank/world; step() takes the words summed over every rank and returns 1 while active. */
+typedef struct oracle_s2m_shard oracle_s2m_shard;
+oracle_s2m_shard* oracle_s2m_shard_create(const llsr_config* cfg, const float* corner_q, int32_t Qc,
+                                          const float* surf_q, int32_t Qs, const float* corner_map, int32_t Mc,
+                                          const float* surf_map, int32_t Ms, const float* pose);
+void oracle_s2m_shard_destroy(oracle_s2m_shard* s);
+void oracle_s2m_shard_partial(oracle_s2m_shard* s, int32_t rank, int32_t world, int64_t* ne);
+int32_t oracle_s2m_shard_step(oracle_s2m_shard* s, const int64_t* ne);
+void oracle_s2m_shard_result(const oracle_s2m_shard* s, float* pose, llsr_lm_report* rep);
 /* TransformToEnd (FA:1414-1490, no-IMU branch) of n float4 points in place. */
 void oracle_transform_to_end(const float* transform_cur, float* xyzi, int32_t n);
 /* GenerateShadowPoint (FA:412-439). */

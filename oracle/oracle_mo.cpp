@@ -24,6 +24,7 @@
 
 #include "../include/llsr.h"
 #include "../lego-loam-sr_amd/csrc/llsr_eigen.h"
+#include "../lego-loam-sr_amd/csrc/llsr_lm.h"
 #include "oracle.h"
 #ifdef LLSR_ORACLE_NANOFLANN
 #include "nanoflann.hpp"
@@ -114,6 +115,109 @@ using Knn = Grid;
 
 struct Coeff { P4 ori; float cx, cy, cz, ci; };
 
+// cornerOptimization body (MO:1274-1375) for one map-frame query point; false when rejected.
+bool corner_coeff(const Knn& gc, const P4* cornerM, const P4& sel_p, float& la_, float& lb_, float& lc_,
+                  float& ld_) {
+  using namespace llsr_eigen;
+  int idx[5];
+  float d2[5];
+  if (gc.knn5(sel_p, idx, d2) < 5) return false;
+  float cx = 0, cy = 0, cz = 0;
+  for (int j = 0; j < 5; ++j) { cx += cornerM[idx[j]].x; cy += cornerM[idx[j]].y; cz += cornerM[idx[j]].z; }
+  cx /= 5; cy /= 5; cz /= 5;
+  float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
+  for (int j = 0; j < 5; ++j) {
+    const float ax = cornerM[idx[j]].x - cx, ay = cornerM[idx[j]].y - cy, az = cornerM[idx[j]].z - cz;
+    a11 += ax * ax; a12 += ax * ay; a13 += ax * az; a22 += ay * ay; a23 += ay * az; a33 += az * az;
+  }
+  a11 /= 5; a12 /= 5; a13 /= 5; a22 /= 5; a23 /= 5; a33 /= 5;
+  const float A1[9] = {a11, a12, a13, a12, a22, a23, a13, a23, a33};  // column-major
+  float D1[3], V1[9];
+  eig3(A1, D1, V1);
+  if (!(D1[2] > 3 * D1[1])) return false;
+  const float x0 = sel_p.x, y0 = sel_p.y, z0 = sel_p.z;
+  // ROW 0 of matV1: V(0,0), V(0,1), V(0,2) (column-major: [0], [3], [6])
+  const float x1 = (float)(cx + 0.1 * V1[0]), y1 = (float)(cy + 0.1 * V1[3]), z1 = (float)(cz + 0.1 * V1[6]);
+  const float x2 = (float)(cx - 0.1 * V1[0]), y2 = (float)(cy - 0.1 * V1[3]), z2 = (float)(cz - 0.1 * V1[6]);
+  const float a012 = std::sqrt(((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1)) * ((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1)) +
+                               ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1)) * ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1)) +
+                               ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1)) * ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1)));
+  const float l12 = std::sqrt((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2));
+  const float la = ((y1 - y2) * ((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1)) +
+                    (z1 - z2) * ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1))) / a012 / l12;
+  const float lb = -((x1 - x2) * ((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1)) -
+                     (z1 - z2) * ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1))) / a012 / l12;
+  const float lc = -((x1 - x2) * ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1)) +
+                     (y1 - y2) * ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1))) / a012 / l12;
+  const float ld2 = a012 / l12;
+  const float s = (float)(1 - 0.9 * std::fabs(ld2));
+  if (!(s > 0.1)) return false;
+  la_ = s * la; lb_ = s * lb; lc_ = s * lc; ld_ = s * ld2;
+  return true;
+}
+
+// surfOptimization body (MO:1383-1440) for one map-frame query point; false when rejected.
+bool surf_coeff(const Knn& gs, const P4* surfM, const P4& sel_p, float& la_, float& lb_, float& lc_, float& ld_) {
+  using namespace llsr_eigen;
+  int idx[5];
+  float d2[5];
+  if (gs.knn5(sel_p, idx, d2) < 5) return false;
+  float A0[15];  // 5x3 column-major
+  for (int j = 0; j < 5; ++j) { A0[j] = surfM[idx[j]].x; A0[5 + j] = surfM[idx[j]].y; A0[10 + j] = surfM[idx[j]].z; }
+  const float B0[5] = {-1, -1, -1, -1, -1};
+  float X0[3];
+  colpiv_qr_solve<5, 3>(A0, B0, X0);
+  float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1;
+  const float ps = std::sqrt(pa * pa + pb * pb + pc * pc);
+  pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+  for (int j = 0; j < 5; ++j)
+    if (std::fabs(pa * surfM[idx[j]].x + pb * surfM[idx[j]].y + pc * surfM[idx[j]].z + pd) > 0.2) return false;
+  const float pd2 = pa * sel_p.x + pb * sel_p.y + pc * sel_p.z + pd;
+  const float s = (float)(1 - 0.9 * std::fabs(pd2) /
+                                 std::sqrt(std::sqrt(sel_p.x * sel_p.x + sel_p.y * sel_p.y + sel_p.z * sel_p.z)));
+  if (!(s > 0.1)) return false;
+  la_ = s * pa; lb_ = s * pb; lc_ = s * pc; ld_ = s * pd2;
+  return true;
+}
+
+// pointAssociateToMap (MO:606-620) with the sin/cos of updatePointAssociateToMapSinCos (MO:591-604).
+P4 associate(const float* t, const P4& pi) {
+  const float cRoll = std::cos(t[0]), sRoll = std::sin(t[0]);
+  const float cPitch = std::cos(t[1]), sPitch = std::sin(t[1]);
+  const float cYaw = std::cos(t[2]), sYaw = std::sin(t[2]);
+  const float x1 = cYaw * pi.x - sYaw * pi.y;
+  const float y1 = sYaw * pi.x + cYaw * pi.y;
+  const float z1 = pi.z;
+  const float x2 = x1;
+  const float y2 = cRoll * y1 - sRoll * z1;
+  const float z2 = sRoll * y1 + cRoll * z1;
+  P4 po;
+  po.x = cPitch * x2 + sPitch * z2 + t[3];
+  po.y = y2 + t[4];
+  po.z = -sPitch * x2 + cPitch * z2 + t[5];
+  po.i = pi.i;
+  return po;
+}
+
+// Jacobian row of LMOptimization (MO:1465-1490) at pose t; a[6] = (arx, ary, arz, cx, cy, cz).
+void jacobian_row(const float* t, const Coeff& co, float* a) {
+  const float srx = std::sin(t[0]), crx = std::cos(t[0]);
+  const float sry = std::sin(t[1]), cry = std::cos(t[1]);
+  const float srz = std::sin(t[2]), crz = std::cos(t[2]);
+  const P4& p = co.ori;
+  a[0] = (crx * sry * srz * p.x + crx * crz * sry * p.y - srx * sry * p.z) * co.cx +
+         (-srx * srz * p.x - crz * srx * p.y - crx * p.z) * co.cy +
+         (crx * cry * srz * p.x + crx * cry * crz * p.y - cry * srx * p.z) * co.cz;
+  a[1] = ((cry * srx * srz - crz * sry) * p.x + (sry * srz + cry * crz * srx) * p.y + crx * cry * p.z) * co.cx +
+         ((-cry * crz - srx * sry * srz) * p.x + (cry * srz - crz * srx * sry) * p.y - crx * sry * p.z) * co.cz;
+  a[2] = ((crz * srx * sry - cry * srz) * p.x + (-cry * crz - srx * sry * srz) * p.y) * co.cx +
+         (crx * crz * p.x - crx * srz * p.y) * co.cy +
+         ((sry * srz + cry * crz * srx) * p.x + (crz * sry - cry * srx * srz) * p.y) * co.cz;
+  a[3] = co.cx;
+  a[4] = co.cy;
+  a[5] = co.cz;
+}
+
 }  // namespace
 
 extern "C" int32_t ORACLE_FN(scan2map)(const llsr_config* cfg, const float* cq, int32_t Qc, const float* sq,
@@ -145,108 +249,27 @@ extern "C" int32_t ORACLE_FN(scan2map)(const llsr_config* cfg, const float* cq, 
   for (int iterCount = 0; iterCount < cfg->iterCountThres; ++iterCount) {
     sel.clear();
     ++iters;
-    // updatePointAssociateToMapSinCos (MO:591-604)
-    const float cRoll = std::cos(t[0]), sRoll = std::sin(t[0]);
-    const float cPitch = std::cos(t[1]), sPitch = std::sin(t[1]);
-    const float cYaw = std::cos(t[2]), sYaw = std::sin(t[2]);
-    auto assoc = [&](const P4& pi) {  // pointAssociateToMap (MO:606-620)
-      const float x1 = cYaw * pi.x - sYaw * pi.y;
-      const float y1 = sYaw * pi.x + cYaw * pi.y;
-      const float z1 = pi.z;
-      const float x2 = x1;
-      const float y2 = cRoll * y1 - sRoll * z1;
-      const float z2 = sRoll * y1 + cRoll * z1;
-      P4 po;
-      po.x = cPitch * x2 + sPitch * z2 + t[3];
-      po.y = y2 + t[4];
-      po.z = -sPitch * x2 + cPitch * z2 + t[5];
-      po.i = pi.i;
-      return po;
-    };
     // ---- cornerOptimization (MO:1269-1377) ----
     int ncor = 0;
     for (int i = 0; i < Qc; ++i) {
-      const P4 sel_p = assoc(cornerQ[i]);
-      int idx[5];
-      float d2[5];
-      if (gc.knn5(sel_p, idx, d2) < 5) continue;
-      float cx = 0, cy = 0, cz = 0;
-      for (int j = 0; j < 5; ++j) { cx += cornerM[idx[j]].x; cy += cornerM[idx[j]].y; cz += cornerM[idx[j]].z; }
-      cx /= 5; cy /= 5; cz /= 5;
-      float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
-      for (int j = 0; j < 5; ++j) {
-        const float ax = cornerM[idx[j]].x - cx, ay = cornerM[idx[j]].y - cy, az = cornerM[idx[j]].z - cz;
-        a11 += ax * ax; a12 += ax * ay; a13 += ax * az; a22 += ay * ay; a23 += ay * az; a33 += az * az;
-      }
-      a11 /= 5; a12 /= 5; a13 /= 5; a22 /= 5; a23 /= 5; a33 /= 5;
-      const float A1[9] = {a11, a12, a13, a12, a22, a23, a13, a23, a33};  // column-major
-      float D1[3], V1[9];
-      eig3(A1, D1, V1);
-      if (D1[2] > 3 * D1[1]) {
-        const float x0 = sel_p.x, y0 = sel_p.y, z0 = sel_p.z;
-        // ROW 0 of matV1: V(0,0), V(0,1), V(0,2) (column-major: [0], [3], [6])
-        const float x1 = (float)(cx + 0.1 * V1[0]), y1 = (float)(cy + 0.1 * V1[3]), z1 = (float)(cz + 0.1 * V1[6]);
-        const float x2 = (float)(cx - 0.1 * V1[0]), y2 = (float)(cy - 0.1 * V1[3]), z2 = (float)(cz - 0.1 * V1[6]);
-        const float a012 = std::sqrt(((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1)) * ((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1)) +
-                                     ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1)) * ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1)) +
-                                     ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1)) * ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1)));
-        const float l12 = std::sqrt((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2));
-        const float la = ((y1 - y2) * ((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1)) +
-                          (z1 - z2) * ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1))) / a012 / l12;
-        const float lb = -((x1 - x2) * ((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1)) -
-                           (z1 - z2) * ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1))) / a012 / l12;
-        const float lc = -((x1 - x2) * ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1)) +
-                           (y1 - y2) * ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1))) / a012 / l12;
-        const float ld2 = a012 / l12;
-        const float s = (float)(1 - 0.9 * std::fabs(ld2));
-        if (s > 0.1) { sel.push_back({cornerQ[i], s * la, s * lb, s * lc, s * ld2}); ++ncor; }
-      }
+      Coeff co{cornerQ[i], 0, 0, 0, 0};
+      if (corner_coeff(gc, cornerM, associate(t, cornerQ[i]), co.cx, co.cy, co.cz, co.ci)) { sel.push_back(co); ++ncor; }
     }
     // ---- surfOptimization (MO:1379-1442) ----
     int nsur = 0;
     for (int i = 0; i < Qs; ++i) {
-      const P4 sel_p = assoc(surfQ[i]);
-      int idx[5];
-      float d2[5];
-      if (gs.knn5(sel_p, idx, d2) < 5) continue;
-      float A0[15];  // 5x3 column-major
-      for (int j = 0; j < 5; ++j) { A0[j] = surfM[idx[j]].x; A0[5 + j] = surfM[idx[j]].y; A0[10 + j] = surfM[idx[j]].z; }
-      const float B0[5] = {-1, -1, -1, -1, -1};
-      float X0[3];
-      colpiv_qr_solve<5, 3>(A0, B0, X0);
-      float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1;
-      const float ps = std::sqrt(pa * pa + pb * pb + pc * pc);
-      pa /= ps; pb /= ps; pc /= ps; pd /= ps;
-      bool valid = true;
-      for (int j = 0; j < 5; ++j)
-        if (std::fabs(pa * surfM[idx[j]].x + pb * surfM[idx[j]].y + pc * surfM[idx[j]].z + pd) > 0.2) { valid = false; break; }
-      if (!valid) continue;
-      const float pd2 = pa * sel_p.x + pb * sel_p.y + pc * sel_p.z + pd;
-      const float s = (float)(1 - 0.9 * std::fabs(pd2) /
-                                     std::sqrt(std::sqrt(sel_p.x * sel_p.x + sel_p.y * sel_p.y + sel_p.z * sel_p.z)));
-      if (s > 0.1) { sel.push_back({surfQ[i], s * pa, s * pb, s * pc, s * pd2}); ++nsur; }
+      Coeff co{surfQ[i], 0, 0, 0, 0};
+      if (surf_coeff(gs, surfM, associate(t, surfQ[i]), co.cx, co.cy, co.cz, co.ci)) { sel.push_back(co); ++nsur; }
     }
     nc = ncor; ns = nsur;
     // ---- LMOptimization (MO:1444-1570) ----
-    const float srx = std::sin(t[0]), crx = std::cos(t[0]);
-    const float sry = std::sin(t[1]), cry = std::cos(t[1]);
-    const float srz = std::sin(t[2]), crz = std::cos(t[2]);
     const int N = (int)sel.size();
     if (N < 50) continue;  // returns false: not converged, no update
     float AtA[36] = {0}, AtB[6] = {0};
     for (int i = 0; i < N; ++i) {
-      const P4& p = sel[i].ori;
-      const Coeff& co = sel[i];
-      const float arx = (crx * sry * srz * p.x + crx * crz * sry * p.y - srx * sry * p.z) * co.cx +
-                        (-srx * srz * p.x - crz * srx * p.y - crx * p.z) * co.cy +
-                        (crx * cry * srz * p.x + crx * cry * crz * p.y - cry * srx * p.z) * co.cz;
-      const float ary = ((cry * srx * srz - crz * sry) * p.x + (sry * srz + cry * crz * srx) * p.y + crx * cry * p.z) * co.cx +
-                        ((-cry * crz - srx * sry * srz) * p.x + (cry * srz - crz * srx * sry) * p.y - crx * sry * p.z) * co.cz;
-      const float arz = ((crz * srx * sry - cry * srz) * p.x + (-cry * crz - srx * sry * srz) * p.y) * co.cx +
-                        (crx * crz * p.x - crx * srz * p.y) * co.cy +
-                        ((sry * srz + cry * crz * srx) * p.x + (crz * sry - cry * srx * srz) * p.y) * co.cz;
-      const float a[6] = {arx, ary, arz, co.cx, co.cy, co.cz};
-      const float bb = -cfg->step_size * co.ci;
+      float a[6];
+      jacobian_row(t, sel[i], a);
+      const float bb = -cfg->step_size * sel[i].ci;
       for (int c = 0; c < 6; ++c) {
         for (int r = 0; r < 6; ++r) AtA[r + 6 * c] += a[r] * a[c];
         AtB[c] += a[c] * bb;
@@ -309,6 +332,120 @@ extern "C" int32_t ORACLE_FN(scan2map)(const llsr_config* cfg, const float* cq, 
   std::memcpy(rep->pose, t, sizeof t);
   std::memcpy(pose, t, sizeof t);
   return LLSR_OK;
+}
+
+// ---- split-correspondence scan-to-map, int64 fixed-point sums (llsr_scan2map_shard_*) -------
+// The CPU statement of what the device's split mode computes: per LM iteration every rank sums
+// the fixed-point terms (llsr_lm::ne_term) of its 256-query blocks (block b of each kind goes to
+// rank b % world), the ranks' words are added, and llsr_lm::lm_update — the device's own step —
+// runs on the total. Used by the gloo tests as a rank's engine and by the GPU tests as the
+// bit-exact reference for the device's split mode.
+struct oracle_s2m_shard {
+  llsr_config cfg;
+  std::vector<P4> cq, sq, cm, sm;
+  Knn gc, gs;
+  struct State {
+    float pose[6];
+    float cR, sR, cP, sP, cY, sY;
+    float matP[36];
+    float matX0[6];
+    float min_lambda = 0.0f, cf_mean = 0.0f;
+    int degenerate = 0, iter = 0, active = 0, converged = 0, nc = 0, ns = 0;
+  } st;
+};
+
+extern "C" oracle_s2m_shard* ORACLE_FN(s2m_shard_create)(const llsr_config* cfg, const float* cq, int32_t Qc,
+                                                         const float* sq, int32_t Qs, const float* cm, int32_t Mc,
+                                                         const float* sm, int32_t Ms, const float* pose) {
+  if (!cfg || !pose || Qc < 0 || Qs < 0 || Mc < 0 || Ms < 0) return nullptr;
+  auto* s = new oracle_s2m_shard();
+  s->cfg = *cfg;
+  const P4* p4[4] = {reinterpret_cast<const P4*>(cq), reinterpret_cast<const P4*>(sq),
+                     reinterpret_cast<const P4*>(cm), reinterpret_cast<const P4*>(sm)};
+  s->cq.assign(p4[0], p4[0] + Qc);
+  s->sq.assign(p4[1], p4[1] + Qs);
+  s->cm.assign(p4[2], p4[2] + Mc);
+  s->sm.assign(p4[3], p4[3] + Ms);
+  auto& st = s->st;
+  std::memcpy(st.pose, pose, sizeof st.pose);
+  std::memset(st.matP, 0, sizeof st.matP);
+  std::memset(st.matX0, 0, sizeof st.matX0);
+  st.cR = std::cos(st.pose[0]); st.sR = std::sin(st.pose[0]);
+  st.cP = std::cos(st.pose[1]); st.sP = std::sin(st.pose[1]);
+  st.cY = std::cos(st.pose[2]); st.sY = std::sin(st.pose[2]);
+  st.active = (Mc > 10 && Ms > 100) ? 1 : 0;  // MO:1573
+  if (st.active) {
+    s->gc.build(s->cm.data(), Mc);
+    s->gs.build(s->sm.data(), Ms);
+  }
+  return s;
+}
+
+extern "C" void ORACLE_FN(s2m_shard_destroy)(oracle_s2m_shard* s) { delete s; }
+
+// Rank `rank` of `world`: the LLSR_NE_WORDS int64 words of this rank's query blocks.
+extern "C" void ORACLE_FN(s2m_shard_partial)(oracle_s2m_shard* s, int32_t rank, int32_t world, int64_t* ne) {
+  for (int k = 0; k < llsr_lm::kNeWords; ++k) ne[k] = 0;
+  if (!s->st.active || world < 1) return;
+  const float* t = s->st.pose;
+  auto add = [&](const Coeff& co, bool corner) {
+    float a[6];
+    jacobian_row(t, co, a);
+    const float bb = -s->cfg.step_size * co.ci;
+    float v[llsr_lm::kRed] = {0};
+    int k = 0;
+    for (int r = 0; r < 6; ++r)
+      for (int c = r; c < 6; ++c, ++k) v[k] = a[r] * a[c];
+    for (int c = 0; c < 6; ++c) v[21 + c] = a[c] * bb;
+    v[27] = std::fabs(co.ci);
+    v[corner ? 28 : 29] = 1.0f;
+    for (int q = 0; q < llsr_lm::kRed; ++q) ne[q] += llsr_lm::ne_term(q, v[q]);
+  };
+  for (int i = 0; i < (int)s->cq.size(); ++i) {
+    if ((i / 256) % world != rank) continue;
+    Coeff co{s->cq[i], 0, 0, 0, 0};
+    if (corner_coeff(s->gc, s->cm.data(), associate(t, s->cq[i]), co.cx, co.cy, co.cz, co.ci)) add(co, true);
+  }
+  for (int i = 0; i < (int)s->sq.size(); ++i) {
+    if ((i / 256) % world != rank) continue;
+    Coeff co{s->sq[i], 0, 0, 0, 0};
+    if (surf_coeff(s->gs, s->sm.data(), associate(t, s->sq[i]), co.cx, co.cy, co.cz, co.ci)) add(co, false);
+  }
+}
+
+// LMOptimization on the summed words of all ranks; returns 1 while the problem is still active.
+extern "C" int32_t ORACLE_FN(s2m_shard_step)(oracle_s2m_shard* s, const int64_t* ne) {
+  auto& st = s->st;
+  if (!st.active) return 0;
+  long long w[llsr_lm::kNeWords];
+  for (int k = 0; k < llsr_lm::kNeWords; ++k) w[k] = (long long)ne[k];
+  float red[llsr_lm::kRed];
+  llsr_lm::ne_to_red(w, red);
+  st.iter += 1;
+  const int iterCount = st.iter - 1;
+  st.nc = (int)red[28];
+  st.ns = (int)red[29];
+  bool conv = false;
+  if (st.nc + st.ns >= 50)
+    conv = llsr_lm::lm_update(st, red, iterCount, s->cfg.mode == LLSR_MODE_LM_APPLIED, s->cfg.stop_thres);
+  if (conv) st.converged = 1;
+  if (conv || st.iter >= s->cfg.iterCountThres) st.active = 0;
+  return st.active;
+}
+
+extern "C" void ORACLE_FN(s2m_shard_result)(const oracle_s2m_shard* s, float* pose, llsr_lm_report* rep) {
+  const auto& st = s->st;
+  std::memset(rep, 0, sizeof *rep);
+  rep->iterations = st.iter;
+  rep->converged = st.converged;
+  rep->degenerate = st.degenerate;
+  rep->min_lambda = st.min_lambda;
+  rep->cf_mean = st.cf_mean;
+  rep->n_corner_corr = st.nc;
+  rep->n_surf_corr = st.ns;
+  std::memcpy(rep->matX0, st.matX0, sizeof st.matX0);
+  std::memcpy(rep->pose, st.pose, sizeof st.pose);
+  std::memcpy(pose, st.pose, sizeof st.pose);
 }
 
 // kNN-5 of Q queries against one map (cross-check hook): idx/d2 [Q][5]; returns #accepted and

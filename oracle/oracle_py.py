@@ -50,6 +50,13 @@ def lib():
         _bind_mo(L, "oracle_")
         L.oracle_transform_to_end.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         L.oracle_shadow_points.argtypes = [C.c_void_p]
+        L.oracle_s2m_shard_create.restype = C.c_void_p
+        L.oracle_s2m_shard_create.argtypes = [C.POINTER(_abi.Config)] + [C.c_void_p, C.c_int32] * 4 + [C.c_void_p]
+        L.oracle_s2m_shard_destroy.argtypes = [C.c_void_p]
+        L.oracle_s2m_shard_partial.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]
+        L.oracle_s2m_shard_step.restype = C.c_int32
+        L.oracle_s2m_shard_step.argtypes = [C.c_void_p, C.c_void_p]
+        L.oracle_s2m_shard_result.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(_abi.LmReport)]
         _LIB = L
     return _LIB
 
@@ -236,3 +243,84 @@ def fa_lm_inputs(prev: dict, cur: dict, transform_prev=None):
     corner_last = transform_to_end(tp, prev["loam_xyzi"][prev["less_sharp_ind"]])
     surf_last = np.concatenate([transform_to_end(tp, prev["less_flat_xyzi"]), sh])
     return sharp, flat, corner_last, surf_last
+
+
+class OracleShardEngine:
+    """CPU statement of llsr_scan2map_shard_* for a batch of problems (llsr.dist engine protocol):
+    the gloo tests' per-rank engine and the bit-exact reference of the device's split mode.
+    problems: list of (corner_q, surf_q, corner_map, surf_map, pose0)."""
+
+    def __init__(self, cfg: _abi.Config, problems):
+        self.cfg = cfg
+        self._keep = []
+        self.h = []
+        for cq, sq, cm, sm, pose in problems:
+            arrs = [_f4(a) for a in (cq, sq, cm, sm)]
+            p = np.ascontiguousarray(pose, dtype=np.float32)
+            self._keep.append((arrs, p))
+            args = []
+            for a in arrs:
+                args += [a.ctypes.data, len(a)]
+            h = lib().oracle_s2m_shard_create(C.byref(cfg), *args, p.ctypes.data)
+            if not h:
+                raise ValueError("oracle_s2m_shard_create rejected the problem")
+            self.h.append(h)
+        self.P = len(self.h)
+
+    def __del__(self):
+        for h in getattr(self, "h", []):
+            lib().oracle_s2m_shard_destroy(h)
+        self.h = []
+
+    def new_ne(self, device=None):
+        import torch
+        return torch.zeros((self.P, _abi.NE_WORDS), dtype=torch.int64)
+
+    def begin(self):
+        pass
+
+    def partial(self, rank: int, world: int, ne):
+        a = ne.numpy() if hasattr(ne, "numpy") else ne
+        for p, h in enumerate(self.h):
+            lib().oracle_s2m_shard_partial(h, rank, world, a[p].ctypes.data)
+
+    def step(self, ne, poll: bool) -> int:
+        a = ne.numpy() if hasattr(ne, "numpy") else ne
+        active = sum(lib().oracle_s2m_shard_step(h, a[p].ctypes.data) for p, h in enumerate(self.h))
+        return active if poll else -1
+
+    def end(self):
+        pass
+
+    def results(self):
+        out = []
+        for h in self.h:
+            pose = np.zeros(6, np.float32)
+            rep = _abi.LmReport()
+            lib().oracle_s2m_shard_result(h, pose.ctypes.data, C.byref(rep))
+            d = rep.as_dict()
+            d["pose"] = pose
+            out.append(d)
+        return out
+
+
+def shard_run_local(cfg: _abi.Config, problems, world: int) -> list:
+    """The split scan-to-map with `world` ranks simulated in one process: each iteration sums
+    the ranks' words, exactly what an all-reduce delivers. Returns the per-problem reports."""
+    engines = [OracleShardEngine(cfg, problems) for _ in range(world)]
+    P = len(problems)
+    for it in range(cfg.iterCountThres):
+        tot = np.zeros((P, _abi.NE_WORDS), np.int64)
+        part = np.zeros_like(tot)
+        for r, e in enumerate(engines):
+            e.partial(r, world, part)
+            tot += part
+        active = [e.step(tot, True) for e in engines]
+        assert len(set(active)) == 1
+        if active[0] == 0:
+            break
+    res = [e.results() for e in engines]
+    for r in res[1:]:
+        for a, b in zip(res[0], r):
+            assert np.array_equal(a["pose"], b["pose"])
+    return res[0]

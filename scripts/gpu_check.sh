@@ -14,7 +14,7 @@ step() {  # name timeout cmd...
   if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then echo "stopping after $name rc=$rc" >> "$OUT/steps.log"; exit $rc; fi
   return 0
 }
-[ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 900 python -m pytest tests -q -m gpu -x
+[ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 900 python -u -m pytest tests -v -m gpu -x --timeout 120 --timeout-method thread
 [ "${SKIP_BENCH:-0}" = 1 ] || step bench 600 python bench.py ${BENCH_ARGS:-}
 if [ "${PROF:-1}" = 1 ]; then
   export TMPDIR=/tmp
