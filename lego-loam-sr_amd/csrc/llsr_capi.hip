@@ -62,6 +62,8 @@ struct llsr_handle {
   hipStream_t stream = nullptr;
   hipStream_t last_stream = nullptr;
   int last_B = 0;
+  const float4* last_pts = nullptr;  // inputs of the last batch (diagnostic re-launches only)
+  const int64_t* last_off = nullptr;
   bool profiling = false;
   // Event sets for up to kRing in-flight profiled batches; retired sets are summed into ksum.
   static constexpr int kRing = 64;
@@ -390,6 +392,8 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   }
   h->last_stream = s;
   h->last_B = B;
+  h->last_pts = pts;
+  h->last_off = d_offsets;
   return LLSR_OK;
 }
 
@@ -436,6 +440,10 @@ extern "C" float llsr_debug_phase_ms(llsr_handle* h, int32_t k, int32_t phase, i
         break;
       case 4: k_ground_elev_ransac<<<B, 1024, 0, s>>>(c, h->d); break;
       case 3: k_ground_add<<<dim3((c.H + 3) / 4, B), 256, 0, s>>>(c, h->d); break;
+      case 1:
+        if (!c.ccl_lds) return -2.f;
+        k_project_fused<<<B, 1024, c.HW * sizeof(int), s>>>(c, h->last_pts, h->last_off, h->d);
+        break;
       default: return -2.f;
     }
   }

@@ -148,9 +148,11 @@ __device__ __forceinline__ void ground_column(const DevCfg& c, const float4* __r
                                               int j) {
   bool haveRV = false, obs = false;
   float RVx = 0.f, RVy = 0.f, RVz = 0.f, lx = 0.f, ly = 0.f, lz = 0.f;
+  float4 fn = full[j];  // the next row's cell is loaded one step ahead of the serial test
   for (int i = 0; i < c.H; ++i) {
     const int cell = j + i * c.W;
-    const float4 f = full[cell];
+    const float4 f = fn;
+    if (i + 1 < c.H) fn = full[cell + c.W];
     int8_t g;
     if (f.w == 0.0f) {
       g = -1;
@@ -209,29 +211,42 @@ __global__ __launch_bounds__(1024) void k_project_fused(DevCfg c, const float4* 
     cnt[C_FIRST] = first;
     cnt[C_LAST] = last;
   }
-  // winners write their cell; then empty cells get the reset values
-  for (int i = tid; i < n; i += nt) {
-    const float4 p = pts[o0 + i];
-    if (!finite3(p)) continue;
-    float r;
-    const int cell = project_cell(c, p, &r);
-    if (cell < 0 || cidx[cell] != i) continue;
-    const int row = cell / c.W, col = cell - row * c.W;
-    d.range[base + cell] = r;
-    d.full[base + cell] = make_float4(p.x, p.y, p.z, (float)((double)(float)row + (double)(float)col / 10000.0));
-    d.vis[base + cell] = p.w;
-  }
+  if (c.dbg_phase <= 0) return;
+  // pass 2 over the cells: each cell's winner is re-read (the cells of a row hold neighbouring
+  // azimuths, so the gather stays within a few cache lines) and only its range is recomputed;
+  // row / column come from the cell. Empty cells get the resetParameters values (IP:170-179).
+  // Four cells per thread per step: every LDS read and gather is issued before the stores.
   const float qnan = __builtin_nanf("");
-  for (int q = tid; q < HW; q += nt) {
-    const int pi = cidx[q];
-    d.cell_pt[base + q] = pi;
-    if (pi < 0) {
-      d.range[base + q] = FLT_MAX;
-      d.full[base + q] = make_float4(qnan, qnan, qnan, 0.0f);
-      d.vis[base + q] = 0.0f;
+  constexpr int kU = 4;
+  for (int q0 = tid; q0 < HW; q0 += kU * nt) {
+    int pi[kU];
+    float4 p[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int q = q0 + u * nt;
+      pi[u] = q < HW ? cidx[q] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) p[u] = pi[u] >= 0 ? pts[o0 + pi[u]] : make_float4(qnan, qnan, qnan, 0.0f);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int q = q0 + u * nt;
+      if (q >= HW) continue;
+      d.cell_pt[base + q] = pi[u];
+      if (pi[u] >= 0) {
+        const int row = q / c.W, col = q - row * c.W;
+        d.range[base + q] = sqrt_(p[u].x * p[u].x + p[u].y * p[u].y + p[u].z * p[u].z);
+        d.full[base + q] = make_float4(p[u].x, p[u].y, p[u].z, (float)((double)(float)row + (double)(float)col / 10000.0));
+        d.vis[base + q] = p[u].w;
+      } else {
+        d.range[base + q] = FLT_MAX;
+        d.full[base + q] = p[u];
+        d.vis[base + q] = 0.0f;
+      }
     }
   }
   __syncthreads();
+  if (c.dbg_phase <= 1) return;
   for (int j = tid; j < c.W; j += nt) ground_column(c, d.full + base, d.ground + base, j);
 }
 
