@@ -290,6 +290,85 @@ def scan2map_allreduce_leg(dev, P: int, steps: int, warmup: int, dist, check: bo
     return out
 
 
+def odometry_leg(dev, lidar: str, B: int, seqs: int, frames: int, steps: int, warmup: int, dist,
+                 check: bool, cpu_seconds: float) -> dict:
+    """configs[3] (HDL-64E) / VLP-16: end-to-end odometry of B independent sequences, one scan per
+    sequence per step: IP + feature stage + scan-to-scan LM + integrateTransformation + the next
+    last clouds, all on the device (llsr_odometry_batch). `seqs` distinct synthetic sequences of
+    `frames` consecutive scans (0.5 m apart) are tiled over the slots and replayed in a loop."""
+    import torch
+    from llsr import Pipeline, _abi, default_config, synth
+    from llsr.dist import max_over_ranks
+    hdl = lidar == "hdl64e"
+    cfg = default_config(lidar, 2048 if hdl else None)
+    cfg.mode = _abi.LLSR_MODE_LM_APPLIED
+    H, W = cfg.num_vertical_scans, cfg.num_horizontal_scans
+    rank = dist.get_rank() if dist else 0
+    seq_scans = [[synth.make_scan(1 + 64 * (q + 4 * rank) + k, lidar) for k in range(frames)] for q in range(seqs)]
+    batches = []
+    for k in range(frames):
+        scans = [seq_scans[b % seqs][k] for b in range(B)]
+        off = np.zeros(B + 1, np.int64)
+        off[1:] = np.cumsum([len(a) for a in scans])
+        batches.append((torch.from_numpy(np.concatenate(scans)).to(dev), torch.from_numpy(off).to(dev)))
+    pipe = Pipeline(cfg, device=dev, max_batch=B, max_points=H * W)
+    torch.cuda.synchronize(dev)
+    n = 0
+
+    def step():
+        nonlocal n
+        d_pts, d_off = batches[n % frames]
+        pipe.odometry_batch(d_pts.data_ptr(), d_off.data_ptr(), B)
+        n += 1
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    el = max_over_ranks(time.perf_counter() - t0, dev)
+    world = dist.get_world_size() if dist else 1
+    s0 = pipe.odometry_fetch(0)
+    out = {"workload": f"{'configs[3]: HDL-64E 64x2048' if hdl else 'VLP-16 1800x16'} end-to-end odometry: "
+                       "projection + segmentation + features + scan-to-scan LM + transformSum + last clouds, "
+                       f"{B} sequences per GPU, one scan each per step",
+           "value": round(B * steps * world / el, 1), "unit": "scans/s", "scaling": "weak",
+           "sequences_per_gpu": B, "steps": steps, "ms_per_step": round(el / steps * 1e3, 3),
+           "slot0_frames": s0["frames"], "slot0_lm_iterations": [s0["lm"]["surf_iterations"], s0["lm"]["corner_iterations"]]}
+    if check:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle_py
+        # slot 0 replays sequence 0 frame (i % frames) for i = 0 .. n-1: the oracle does the same
+        od = oracle_py.OracleOdometry(cfg)
+        t_cpu = 0.0
+        for i in range(n):
+            t1 = time.perf_counter()
+            o = od.process(seq_scans[0][i % frames])
+            t_cpu += time.perf_counter() - t1
+        out["pose_delta_max"] = float(max(np.abs(s0["transform_cur"] - o["transform_cur"]).max(),
+                                          np.abs(s0["transform_sum"] - o["transform_sum"]).max()))
+        # CPU baseline: the same restatement, one core, continuing the sequence for ~cpu_seconds
+        k = n
+        while t_cpu < cpu_seconds and k < n + 1000:
+            t1 = time.perf_counter()
+            od.process(seq_scans[0][k % frames])
+            t_cpu += time.perf_counter() - t1
+            k += 1
+        out["cpu_baseline"] = {"value": round(k / t_cpu, 2), "unit": "scans/s", "cores": 1, "kind": "port",
+                               "sample": f"{k} scans of sequence 0 through the oracle (IP + features + "
+                                         f"scan-to-scan LM + integrate + TransformToEnd), 1 thread, {t_cpu:.1f} s"}
+        out["speedup_vs_cpu"] = round(out["value"] / world / out["cpu_baseline"]["value"], 1)
+    pipe.close()
+    return out
+
+
 def ctypes_sizeof_report() -> int:
     import ctypes
     from llsr import _abi
@@ -310,6 +389,8 @@ def main():
     ap.add_argument("--s2m-problems", type=int, default=256, help="scan-to-map problems per GPU per step")
     ap.add_argument("--s2m-steps", type=int, default=5)
     ap.add_argument("--s2m-modes", default="lm_applied,faithful", help="comma list; empty = skip the leg")
+    ap.add_argument("--odo", default="hdl64e:128,vlp16:1024",
+                    help="odometry legs lidar:sequences_per_gpu, comma list (empty = skip)")
     ap.add_argument("--allreduce-scans", type=int, default=8,
                     help="configs[4] leg: scans per step split over all ranks (0 = skip)")
     args = ap.parse_args()
@@ -413,6 +494,12 @@ def main():
                                       rank == 0 and not args.no_cpu and world == 1,
                                       min(args.cpu_seconds, 12.0))
 
+    odo = {}
+    for spec in [x for x in args.odo.split(",") if x]:
+        lid, nb = spec.split(":")
+        odo[lid] = odometry_leg(dev, lid, int(nb), 2, 4, args.s2m_steps, 2, dist,
+                                rank == 0 and not args.no_cpu and world == 1, min(args.cpu_seconds, 10.0))
+
     allred = None
     if args.allreduce_scans > 0:
         allred = scan2map_allreduce_leg(dev, args.allreduce_scans, args.s2m_steps, 1, dist,
@@ -448,6 +535,7 @@ def main():
             "pose_delta": s2m.get("lm_applied", {}).get("pose_delta_max"),
             "scan2map": s2m,
             "scan2map_allreduce": allred,
+            "odometry": odo,
         }
         if not args.no_cpu and world == 1:
             scans = [pts[off[k]:off[k + 1]] for k in range(min(args.distinct, B))]

@@ -284,6 +284,36 @@ int32_t llsr_scan2map(llsr_handle* h, const float* corner_q, int32_t n_corner_q,
                       const float* surf_map, int32_t n_surf_map, float* pose, llsr_lm_report* rep);
 
 
+/* ---- End-to-end odometry (runFeatureAssociation, featureAssociation.cpp:2742-2853) ----
+ * B independent sequences (slots). Each call consumes one device-resident scan per slot (as
+ * llsr_process_batch) and runs, without leaving the device: the ImageProjection + feature stage,
+ * then updateTransformation against the slot's last clouds (FA:2505-2535), integrateTransformation
+ * (FA:2537-2568, transformSum) and publishCloudsLast (FA:2660-2717): TransformToEnd of the
+ * less-sharp / less-flat clouds, which become the slot's last clouds (+ the 160 shadow points on
+ * the surf side), and of the sharp / flat clouds (MapOptimization's scan inputs). A slot's first
+ * scan runs checkSystemInitialization (FA:2291-2315) instead. transformCur carries over to the
+ * next scan as the LM's initial guess. Requires LLSR_MODE_LM_APPLIED (LLSR_ENOSYS otherwise): in
+ * the faithful mode updateInitialGuess (FA:2790) overwrites transformCur from the /odom2 topic,
+ * which has no input here. One host sync per call (the feature counts size the packed clouds). */
+typedef struct llsr_odom_slot {
+  int32_t frames;            /* scans this slot has consumed */
+  int32_t n_corner_last;     /* laserCloudCornerLastNum after the last scan */
+  int32_t n_surf_last;       /* laserCloudSurfLastNum (incl. the 160 shadow points) */
+  int32_t n_corner_scan;     /* laserCloudCornerScan = TransformToEnd(cornerPointsSharp); 0 on frame 1 */
+  int32_t n_surf_scan;       /* laserCloudSurfScan = TransformToEnd(surfPointsFlat + shadow); 0 on frame 1 */
+  float transform_cur[6];    /* transformCur after updateTransformation */
+  float transform_sum[6];    /* transformSum after integrateTransformation */
+  llsr_s2s_report lm;        /* the last scan's updateTransformation (skipped = 1 on frame 1) */
+} llsr_odom_slot;
+int32_t llsr_odometry_batch(llsr_handle* h, const float* d_xyzi, const int64_t* d_offsets, int32_t B,
+                            void* hip_stream);
+/* Slot b's state after the last call; the float4 cloud buffers (host, may be NULL) receive the
+ * last clouds and the scan clouds (capacity H*W + 160 points each). Synchronises. */
+int32_t llsr_odometry_fetch(llsr_handle* h, int32_t b, llsr_odom_slot* out, float* corner_last, float* surf_last,
+                            float* corner_scan, float* surf_scan);
+/* Start every slot over: transformCur / transformSum = 0, no last clouds, FA carry-over reset. */
+int32_t llsr_odometry_reset(llsr_handle* h);
+
 #ifdef __cplusplus
 }
 #endif

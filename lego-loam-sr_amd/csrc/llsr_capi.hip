@@ -14,6 +14,7 @@
 #include "llsr_device.h"
 #include "llsr_grid.h"
 #include "llsr_mo.h"
+#include "llsr_odo.h"
 #include "llsr_s2s.h"
 
 namespace llsr {
@@ -96,6 +97,25 @@ struct llsr_handle {
     hipStream_t last = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
   } s2s;
+  // end-to-end odometry (llsr_odometry_*): per-slot FA state + packed clouds, allocated lazily
+  struct {
+    void* pool = nullptr;
+    int B = 0;                    // slots
+    size_t cap = 0;               // points per packed buffer (B * (H*W + 160))
+    float* tcur = nullptr;        // [B][6]
+    float* tsum = nullptr;        // [B][6]
+    int* deg = nullptr;           // [B] isDegenerate
+    int* inited = nullptr;        // [B]
+    int* frames = nullptr;        // [B]
+    float4* shadow = nullptr;     // [160]
+    float4 *sharp = nullptr, *flat = nullptr, *scan_c = nullptr, *scan_s = nullptr;
+    float4 *last_c[2] = {nullptr, nullptr}, *last_s[2] = {nullptr, nullptr};
+    int64_t* off = nullptr;       // device [6][B+1]: sharp, flat, last_c[0], last_c[1], last_s[0], last_s[1]
+    int64_t* h_off = nullptr;     // pinned host copy
+    int* h_counts = nullptr;      // pinned [B][kCnt]
+    llsr_s2s_report* report = nullptr;  // [B]
+    int cur = 0;                  // last_c/s[cur] hold the current last clouds
+  } odo;
   std::string err;
 };
 
@@ -280,6 +300,9 @@ extern "C" void llsr_destroy(llsr_handle* h) {
   if (h->s2s.host_flag) (void)hipHostFree(h->s2s.host_flag);
   if (h->s2s.e0) (void)hipEventDestroy(h->s2s.e0);
   if (h->s2s.e1) (void)hipEventDestroy(h->s2s.e1);
+  if (h->odo.pool) (void)hipFree(h->odo.pool);
+  if (h->odo.h_off) (void)hipHostFree(h->odo.h_off);
+  if (h->odo.h_counts) (void)hipHostFree(h->odo.h_counts);
   if (h->mo.stage) (void)hipFree(h->mo.stage);
   if (h->mo.host_flags) (void)hipHostFree(h->mo.host_flags);
   if (h->mo.e0) (void)hipEventDestroy(h->mo.e0);
@@ -998,5 +1021,184 @@ extern "C" int32_t llsr_scan2scan(llsr_handle* h, const float* sharp, int32_t Ms
   float ms_ = 0.f;
   HIP_OK(h, hipEventElapsedTime(&ms_, m.e0, m.e1));
   rep->ms = ms_;
+  return LLSR_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// End-to-end odometry (runFeatureAssociation, FA:2742-2853): see llsr_odo.hip.
+
+static int32_t odo_alloc(llsr_handle* h) {
+  auto& o = h->odo;
+  if (o.pool) return LLSR_OK;
+  const int B = h->max_batch;
+  const size_t per = (size_t)h->dc.HW + kShadow;
+  o.B = B;
+  o.cap = (size_t)B * per;
+  const size_t bytes = sizeof(float) * 12 * B + sizeof(int) * 3 * B + sizeof(float4) * kShadow +
+                       sizeof(float4) * 8 * o.cap + sizeof(int64_t) * 6 * (B + 1) + sizeof(llsr_s2s_report) * B +
+                       16 * 256;
+  if (hipMalloc(&o.pool, bytes) != hipSuccess) {
+    o.pool = nullptr;
+    return fail(h, LLSR_ENOMEM, "odometry buffers");
+  }
+  char* q = (char*)o.pool;
+  o.tcur = carve<float>(q, 6 * (size_t)B);
+  o.tsum = carve<float>(q, 6 * (size_t)B);
+  o.deg = carve<int>(q, B);
+  o.inited = carve<int>(q, B);
+  o.frames = carve<int>(q, B);
+  o.shadow = carve<float4>(q, kShadow);
+  o.sharp = carve<float4>(q, o.cap);
+  o.flat = carve<float4>(q, o.cap);
+  o.scan_c = carve<float4>(q, o.cap);
+  o.scan_s = carve<float4>(q, o.cap);
+  for (int k = 0; k < 2; ++k) {
+    o.last_c[k] = carve<float4>(q, o.cap);
+    o.last_s[k] = carve<float4>(q, o.cap);
+  }
+  o.off = carve<int64_t>(q, 6 * (size_t)(B + 1));
+  o.report = carve<llsr_s2s_report>(q, B);
+  if (hipHostMalloc((void**)&o.h_off, sizeof(int64_t) * 6 * (B + 1)) != hipSuccess ||
+      hipHostMalloc((void**)&o.h_counts, sizeof(int) * kCnt * B) != hipSuccess)
+    return fail(h, LLSR_ENOMEM, "pinned odometry staging");
+  float sh[4 * kShadow];
+  llsr_shadow_points(sh);
+  HIP_OK(h, hipMemcpy(o.shadow, sh, sizeof sh, hipMemcpyHostToDevice));
+  return llsr_odometry_reset(h);
+}
+
+extern "C" int32_t llsr_odometry_reset(llsr_handle* h) {
+  if (!h) return LLSR_EINVAL;
+  auto& o = h->odo;
+  int32_t rc = llsr_reset_state(h);  // FA carry-over arrays (FA:167-198) of every slot
+  if (rc != LLSR_OK || !o.pool) return rc;
+  HIP_OK(h, hipSetDevice(h->device));
+  const int B = o.B;
+  HIP_OK(h, hipMemset(o.tcur, 0, sizeof(float) * 6 * B));
+  HIP_OK(h, hipMemset(o.tsum, 0, sizeof(float) * 6 * B));
+  HIP_OK(h, hipMemset(o.deg, 0, sizeof(int) * B));
+  HIP_OK(h, hipMemset(o.inited, 0, sizeof(int) * B));
+  HIP_OK(h, hipMemset(o.frames, 0, sizeof(int) * B));
+  HIP_OK(h, hipMemset(o.off, 0, sizeof(int64_t) * 6 * (B + 1)));
+  HIP_OK(h, hipMemset(o.report, 0, sizeof(llsr_s2s_report) * B));
+  std::memset(o.h_off, 0, sizeof(int64_t) * 6 * (B + 1));
+  o.cur = 0;
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_odometry_batch(llsr_handle* h, const float* d_xyzi, const int64_t* d_offsets, int32_t B,
+                                       void* hip_stream) {
+  if (!h) return LLSR_EINVAL;
+  if (h->cfg.mode != LLSR_MODE_LM_APPLIED)
+    return fail(h, LLSR_ENOSYS, "odometry needs LLSR_MODE_LM_APPLIED: faithful mode overwrites transformCur "
+                                "from the /odom2 topic (updateInitialGuess, FA:2790), which has no input here");
+  if (B < 1 || B > h->max_batch) return fail(h, LLSR_ERANGE, "batch size outside [1, max_batch]");
+  HIP_OK(h, hipSetDevice(h->device));
+  int32_t rc = odo_alloc(h);
+  if (rc != LLSR_OK) return rc;
+  auto& o = h->odo;
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+  rc = llsr_process_batch(h, d_xyzi, d_offsets, B, s);
+  if (rc != LLSR_OK) return rc;
+  // the feature counts size the packed clouds: one host sync per batch
+  HIP_OK(h, hipMemcpyAsync(o.h_counts, h->d.counts, sizeof(int) * kCnt * B, hipMemcpyDeviceToHost, s));
+  HIP_OK(h, hipStreamSynchronize(s));
+  const int nb = o.B + 1;
+  int64_t* hs = o.h_off;                       // sharp
+  int64_t* hf = o.h_off + nb;                  // flat
+  const int cur = o.cur, nxt = cur ^ 1;
+  int64_t* hlc = o.h_off + (2 + cur) * nb;     // current last corner (from the previous batch)
+  int64_t* hls = o.h_off + (4 + cur) * nb;
+  int64_t* hnc = o.h_off + (2 + nxt) * nb;     // next last clouds
+  int64_t* hns = o.h_off + (4 + nxt) * nb;
+  int mMs = 0, mF = 0, mNc = 0, mNs = 0;
+  hs[0] = hf[0] = hnc[0] = hns[0] = 0;
+  for (int b = 0; b < B; ++b) {
+    const int* c = o.h_counts + (size_t)b * kCnt;
+    const int Ms = c[C_SHARP], F = c[C_F] + kShadow, M = c[C_M], L = c[C_L] + kShadow;
+    hs[b + 1] = hs[b] + Ms;
+    hf[b + 1] = hf[b] + F;
+    hnc[b + 1] = hnc[b] + M;
+    hns[b + 1] = hns[b] + L;
+    mMs = Ms > mMs ? Ms : mMs;
+    mF = F > mF ? F : mF;
+    const int Nc = (int)(hlc[b + 1] - hlc[b]), Ns = (int)(hls[b + 1] - hls[b]);
+    mNc = Nc > mNc ? Nc : mNc;
+    mNs = Ns > mNs ? Ns : mNs;
+  }
+  // slots beyond B keep their (empty) ranges: offsets stay at the B-th value
+  for (int b = B; b < o.B; ++b) {
+    hs[b + 1] = hs[B]; hf[b + 1] = hf[B]; hnc[b + 1] = hnc[B]; hns[b + 1] = hns[B];
+  }
+  HIP_OK(h, hipMemcpyAsync(o.off, hs, sizeof(int64_t) * nb, hipMemcpyHostToDevice, s));
+  HIP_OK(h, hipMemcpyAsync(o.off + nb, hf, sizeof(int64_t) * nb, hipMemcpyHostToDevice, s));
+  HIP_OK(h, hipMemcpyAsync(o.off + (2 + nxt) * nb, hnc, sizeof(int64_t) * nb, hipMemcpyHostToDevice, s));
+  HIP_OK(h, hipMemcpyAsync(o.off + (4 + nxt) * nb, hns, sizeof(int64_t) * nb, hipMemcpyHostToDevice, s));
+  rc = llsr_scan2scan_reserve(h, o.B, mMs > 1 ? mMs : 1, mF, mNc > 1 ? mNc : 1, mNs > 1 ? mNs : 1);
+  if (rc != LLSR_OK) return rc;
+  OdoArgs a{};
+  a.B = B;
+  a.HW = h->dc.HW;
+  a.counts = h->d.counts;
+  a.loam = h->d.loam;
+  a.sharp_ind = h->d.sharp;
+  a.flat_ind = h->d.flat;
+  a.less_sharp = h->d.less_sharp;
+  a.lflat = h->d.lflat;
+  a.shadow = o.shadow;
+  a.sharp_off = o.off; a.sharp = o.sharp;
+  a.flat_off = o.off + nb; a.flat = o.flat;
+  a.nlast_c_off = o.off + (2 + nxt) * nb; a.nlast_c = o.last_c[nxt];
+  a.nlast_s_off = o.off + (4 + nxt) * nb; a.nlast_s = o.last_s[nxt];
+  a.scan_c = o.scan_c; a.scan_s = o.scan_s;
+  a.tcur = o.tcur; a.tsum = o.tsum; a.inited = o.inited; a.frames = o.frames;
+  k_odo_inputs<<<B, 256, 0, s>>>(a);
+  HIP_OK(h, hipGetLastError());
+  llsr_s2s_batch sb{};
+  sb.n_problems = B;
+  sb.sharp = (const float*)o.sharp; sb.sharp_off = o.off;
+  sb.flat = (const float*)o.flat; sb.flat_off = o.off + nb;
+  sb.corner_last = (const float*)o.last_c[cur]; sb.corner_last_off = o.off + (2 + cur) * nb;
+  sb.surf_last = (const float*)o.last_s[cur]; sb.surf_last_off = o.off + (4 + cur) * nb;
+  sb.transform_cur = o.tcur;
+  sb.is_degenerate = o.deg;
+  sb.report = o.report;
+  rc = llsr_scan2scan_batch(h, &sb, s);
+  if (rc != LLSR_OK) return rc;
+  k_odo_finish<<<B, 256, 0, s>>>(a);
+  HIP_OK(h, hipGetLastError());
+  o.cur = nxt;
+  h->last_stream = s;
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_odometry_fetch(llsr_handle* h, int32_t b, llsr_odom_slot* out, float* corner_last,
+                                       float* surf_last, float* corner_scan, float* surf_scan) {
+  if (!h || !out) return LLSR_EINVAL;
+  auto& o = h->odo;
+  if (!o.pool) return fail(h, LLSR_EINVAL, "llsr_odometry_batch not called");
+  if (b < 0 || b >= o.B) return fail(h, LLSR_ERANGE, "slot outside [0, max_batch)");
+  int32_t rc = sync_last(h);
+  if (rc) return rc;
+  rc = llsr_scan2scan_check(h);
+  if (rc) return rc;
+  const int nb = o.B + 1;
+  const int cur = o.cur;
+  const int64_t* hlc = o.h_off + (2 + cur) * nb;
+  const int64_t* hls = o.h_off + (4 + cur) * nb;
+  std::memset(out, 0, sizeof *out);
+  HIP_OK(h, d2h(&out->frames, o.frames + b, 1));
+  HIP_OK(h, d2h(out->transform_cur, o.tcur + 6 * b, 6));
+  HIP_OK(h, d2h(out->transform_sum, o.tsum + 6 * b, 6));
+  HIP_OK(h, d2h(&out->lm, o.report + b, 1));
+  out->n_corner_last = (int)(hlc[b + 1] - hlc[b]);
+  out->n_surf_last = (int)(hls[b + 1] - hls[b]);
+  const bool scans = out->frames > 1;  // the first scan of a slot publishes no scan clouds
+  out->n_corner_scan = scans ? (int)(o.h_off[b + 1] - o.h_off[b]) : 0;
+  out->n_surf_scan = scans ? (int)(o.h_off[nb + b + 1] - o.h_off[nb + b]) : 0;
+  HIP_OK(h, d2h(corner_last, (const float*)(o.last_c[cur] + hlc[b]), 4 * (size_t)out->n_corner_last));
+  HIP_OK(h, d2h(surf_last, (const float*)(o.last_s[cur] + hls[b]), 4 * (size_t)out->n_surf_last));
+  HIP_OK(h, d2h(corner_scan, (const float*)(o.scan_c + o.h_off[b]), 4 * (size_t)out->n_corner_scan));
+  HIP_OK(h, d2h(surf_scan, (const float*)(o.scan_s + o.h_off[nb + b]), 4 * (size_t)out->n_surf_scan));
   return LLSR_OK;
 }

@@ -36,7 +36,8 @@ EXPORTS = [
     "llsr_scan2map_reserve", "llsr_scan2map_batch", "llsr_scan2map", "llsr_scan2map_stats",
     "llsr_shadow_points", "llsr_scan2scan_reserve", "llsr_scan2scan_batch", "llsr_scan2scan_check",
     "llsr_scan2scan", "llsr_scan2map_shard_begin", "llsr_scan2map_shard_partial",
-    "llsr_scan2map_shard_step", "llsr_scan2map_shard_end",
+    "llsr_scan2map_shard_step", "llsr_scan2map_shard_end", "llsr_odometry_batch", "llsr_odometry_fetch",
+    "llsr_odometry_reset",
 ]
 
 
@@ -83,6 +84,9 @@ def lib():
         L.llsr_scan2map_shard_partial.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
         L.llsr_scan2map_shard_step.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int32), C.c_void_p]
         L.llsr_scan2map_shard_end.argtypes = [C.c_void_p, C.c_void_p]
+        L.llsr_odometry_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
+        L.llsr_odometry_fetch.argtypes = [C.c_void_p, C.c_int32, C.POINTER(_abi.OdomSlot)] + [C.c_void_p] * 4
+        L.llsr_odometry_reset.argtypes = [C.c_void_p]
         for fn in EXPORTS:
             if fn not in ("llsr_last_error", "llsr_kernel_name", "llsr_destroy"):
                 getattr(L, fn).restype = C.c_int32
@@ -256,6 +260,32 @@ class Pipeline:
 
     def scan2scan_check(self):
         self._check(lib().llsr_scan2scan_check(self._h), "llsr_scan2scan_check")
+
+
+    # ---- end-to-end odometry (runFeatureAssociation) -------------------------------------------
+    def odometry_batch(self, d_xyzi: int, d_offsets: int, B: int, stream: int = 0):
+        """One device-resident scan per slot through features + scan-to-scan LM + last clouds."""
+        self._check(lib().llsr_odometry_batch(self._h, C.c_void_p(d_xyzi), C.c_void_p(d_offsets), B,
+                                              C.c_void_p(stream)), "llsr_odometry_batch")
+
+    def odometry_fetch(self, b: int, clouds: bool = False) -> dict:
+        st = _abi.OdomSlot()
+        cap = self.cfg.num_vertical_scans * self.cfg.num_horizontal_scans + 160
+        bufs = [np.zeros((cap, 4), np.float32) for _ in range(4)] if clouds else [None] * 4
+        ptrs = [C.c_void_p(a.ctypes.data) if a is not None else None for a in bufs]
+        self._check(lib().llsr_odometry_fetch(self._h, b, C.byref(st), *ptrs), "llsr_odometry_fetch")
+        d = {k: getattr(st, k) for k in ("frames", "n_corner_last", "n_surf_last", "n_corner_scan", "n_surf_scan")}
+        d["transform_cur"] = np.array(st.transform_cur[:], np.float32)
+        d["transform_sum"] = np.array(st.transform_sum[:], np.float32)
+        d["lm"] = st.lm.as_dict()
+        if clouds:
+            for name, a, n in zip(("corner_last", "surf_last", "corner_scan", "surf_scan"), bufs,
+                                  (st.n_corner_last, st.n_surf_last, st.n_corner_scan, st.n_surf_scan)):
+                d[name] = a[:n].copy()
+        return d
+
+    def odometry_reset(self):
+        self._check(lib().llsr_odometry_reset(self._h), "llsr_odometry_reset")
 
 
 def shadow_points() -> np.ndarray:

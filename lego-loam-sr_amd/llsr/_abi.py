@@ -156,6 +156,20 @@ class S2SReport(C.Structure):
         return d
 
 
+class OdomSlot(C.Structure):
+    """llsr_odom_slot (include/llsr.h): one sequence's odometry state after the last scan."""
+    _fields_ = [
+        ("frames", C.c_int32),
+        ("n_corner_last", C.c_int32),
+        ("n_surf_last", C.c_int32),
+        ("n_corner_scan", C.c_int32),
+        ("n_surf_scan", C.c_int32),
+        ("transform_cur", C.c_float * 6),
+        ("transform_sum", C.c_float * 6),
+        ("lm", S2SReport),
+    ]
+
+
 class S2SBatch(C.Structure):
     """llsr_s2s_batch (include/llsr.h): device pointers of one scan-to-scan batch."""
     _fields_ = [

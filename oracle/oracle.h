@@ -60,6 +60,8 @@ int32_t oracle_s2m_shard_step(oracle_s2m_shard* s, const int64_t* ne);
 void oracle_s2m_shard_result(const oracle_s2m_shard* s, float* pose, llsr_lm_report* rep);
 /* TransformToEnd (FA:1414-1490, no-IMU branch) of n float4 points in place. */
 void oracle_transform_to_end(const float* transform_cur, float* xyzi, int32_t n);
+/* integrateTransformation (FA:2537-2568, no IMU): transform_sum in place. */
+void oracle_integrate_transformation(float* transform_sum, const float* transform_cur);
 /* GenerateShadowPoint (FA:412-439). */
 void oracle_shadow_points(float* out_xyzi);
 /* Test hooks for the Eigen restatements (llsr_eigen.h): column-major inputs. */

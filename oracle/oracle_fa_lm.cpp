@@ -426,6 +426,45 @@ extern "C" void oracle_transform_to_end(const float* tc, float* xyzi, int32_t n)
   }
 }
 
+// AccumulateRotation (FA:1552-1578): float sin / cos / asin / atan2 overloads.
+static void accumulate_rotation(float cx, float cy, float cz, float lx, float ly, float lz, float& ox, float& oy,
+                                float& oz) {
+  float srx = std::cos(lx) * std::cos(cx) * std::sin(ly) * std::sin(cz) -
+              std::cos(cx) * std::cos(cz) * std::sin(lx) - std::cos(lx) * std::cos(ly) * std::sin(cx);
+  ox = -std::asin(srx);
+  float srycrx = std::sin(lx) * (std::cos(cy) * std::sin(cz) - std::cos(cz) * std::sin(cx) * std::sin(cy)) +
+                 std::cos(lx) * std::sin(ly) * (std::cos(cy) * std::cos(cz) + std::sin(cx) * std::sin(cy) * std::sin(cz)) +
+                 std::cos(lx) * std::cos(ly) * std::cos(cx) * std::sin(cy);
+  float crycrx = std::cos(lx) * std::cos(ly) * std::cos(cx) * std::cos(cy) -
+                 std::cos(lx) * std::sin(ly) * (std::cos(cz) * std::sin(cy) - std::cos(cy) * std::sin(cx) * std::sin(cz)) -
+                 std::sin(lx) * (std::sin(cy) * std::sin(cz) + std::cos(cy) * std::cos(cz) * std::sin(cx));
+  oy = std::atan2(srycrx / std::cos(ox), crycrx / std::cos(ox));
+  float srzcrx = std::sin(cx) * (std::cos(lz) * std::sin(ly) - std::cos(ly) * std::sin(lx) * std::sin(lz)) +
+                 std::cos(cx) * std::sin(cz) * (std::cos(ly) * std::cos(lz) + std::sin(lx) * std::sin(ly) * std::sin(lz)) +
+                 std::cos(lx) * std::cos(cx) * std::cos(cz) * std::sin(lz);
+  float crzcrx = std::cos(lx) * std::cos(lz) * std::cos(cx) * std::cos(cz) -
+                 std::cos(cx) * std::sin(cz) * (std::cos(ly) * std::sin(lz) - std::cos(lz) * std::sin(lx) * std::sin(ly)) -
+                 std::sin(cx) * (std::sin(ly) * std::sin(lz) + std::cos(ly) * std::cos(lz) * std::sin(lx));
+  oz = std::atan2(srzcrx / std::cos(ox), crzcrx / std::cos(ox));
+}
+
+// integrateTransformation (FA:2537-2568), use_imu_undistortion == false: transformSum in place.
+extern "C" void oracle_integrate_transformation(float* ts, const float* tc) {
+  float rx, ry, rz;
+  accumulate_rotation(ts[0], ts[1], ts[2], -tc[0], -tc[1], -tc[2], rx, ry, rz);
+  const float x1 = std::cos(rz) * (tc[3]) - std::sin(rz) * (tc[4]);
+  const float y1 = std::sin(rz) * (tc[3]) + std::cos(rz) * (tc[4]);
+  const float z1 = tc[5];
+  const float x2 = x1;
+  const float y2 = std::cos(rx) * y1 - std::sin(rx) * z1;
+  const float z2 = std::sin(rx) * y1 + std::cos(rx) * z1;
+  const float tx = ts[3] - (std::cos(ry) * x2 + std::sin(ry) * z2);
+  const float ty = ts[4] - y2;
+  const float tz = ts[5] - (-std::sin(ry) * x2 + std::cos(ry) * z2);
+  ts[0] = rx; ts[1] = ry; ts[2] = rz;
+  ts[3] = tx; ts[4] = ty; ts[5] = tz;
+}
+
 // GenerateShadowPoint (FA:412-439): 16 x 10 virtual points, lidar_to_body_centor (FA:300).
 extern "C" void oracle_shadow_points(float* out) {
   const double c0 = 0.008, c1 = 0.0, c2 = -0.035;

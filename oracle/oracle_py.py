@@ -50,6 +50,7 @@ def lib():
         _bind_mo(L, "oracle_")
         L.oracle_transform_to_end.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         L.oracle_shadow_points.argtypes = [C.c_void_p]
+        L.oracle_integrate_transformation.argtypes = [C.c_void_p, C.c_void_p]
         L.oracle_s2m_shard_create.restype = C.c_void_p
         L.oracle_s2m_shard_create.argtypes = [C.POINTER(_abi.Config)] + [C.c_void_p, C.c_int32] * 4 + [C.c_void_p]
         L.oracle_s2m_shard_destroy.argtypes = [C.c_void_p]
@@ -324,3 +325,53 @@ def shard_run_local(cfg: _abi.Config, problems, world: int) -> list:
         for a, b in zip(res[0], r):
             assert np.array_equal(a["pose"], b["pose"])
     return res[0]
+
+
+def integrate_transformation(transform_sum, transform_cur) -> np.ndarray:
+    ts = np.ascontiguousarray(transform_sum, dtype=np.float32).copy()
+    tc = np.ascontiguousarray(transform_cur, dtype=np.float32)
+    lib().oracle_integrate_transformation(ts.ctypes.data, tc.ctypes.data)
+    return ts
+
+
+class OracleOdometry:
+    """runFeatureAssociation (FA:2742-2853) in the lm_applied mode for one sequence: the IP +
+    feature stage, then updateTransformation against the last clouds, integrateTransformation and
+    publishCloudsLast's TransformToEnd (first scan: checkSystemInitialization)."""
+
+    def __init__(self, cfg: _abi.Config):
+        self.cfg = cfg
+        self.ora = Oracle(cfg)
+        self.shadow = shadow_points()
+        self.tcur = np.zeros(6, np.float32)
+        self.tsum = np.zeros(6, np.float32)
+        self.deg = 0
+        self.corner_last = None
+        self.surf_last = None
+        self.frames = 0
+
+    def process(self, xyzi: np.ndarray) -> dict:
+        r = self.ora.process(xyzi)
+        loam = r["loam_xyzi"]
+        sharp = loam[r["sharp_ind"]]
+        flat = np.concatenate([loam[r["flat_ind"]], self.shadow])
+        less_sharp, less_flat = loam[r["less_sharp_ind"]], r["less_flat_xyzi"]
+        out = {"features": r}
+        if self.corner_last is None:  # checkSystemInitialization (FA:2291-2315)
+            self.corner_last = less_sharp.copy()
+            self.surf_last = np.concatenate([less_flat, self.shadow])
+            out["lm"] = None
+            out["corner_scan"] = out["surf_scan"] = None
+        else:
+            lm = scan2scan(self.cfg, sharp, flat, self.corner_last, self.surf_last, self.tcur, self.deg)
+            self.tcur, self.deg = lm["transform_cur"], lm["is_degenerate"]
+            self.tsum = integrate_transformation(self.tsum, self.tcur)
+            self.corner_last = transform_to_end(self.tcur, less_sharp)
+            self.surf_last = np.concatenate([transform_to_end(self.tcur, less_flat), self.shadow])
+            out["lm"] = lm
+            out["corner_scan"] = transform_to_end(self.tcur, sharp)
+            out["surf_scan"] = transform_to_end(self.tcur, flat)
+        self.frames += 1
+        out.update(frames=self.frames, transform_cur=self.tcur.copy(), transform_sum=self.tsum.copy(),
+                   corner_last=self.corner_last, surf_last=self.surf_last)
+        return out

@@ -1,0 +1,80 @@
+"""GPU parity of the end-to-end odometry (llsr_odometry_*, runFeatureAssociation FA:2742-2853).
+
+B independent sequences advance one scan per call through IP + features + scan-to-scan LM +
+integrateTransformation + publishCloudsLast on the device; each slot is compared after every
+scan with the oracle's sequence restatement (oracle_py.OracleOdometry).
+
+Bar: frame counts, LM skip flag and cloud sizes equal; transformCur / transformSum and the last /
+scan clouds within 1e-4 (the surf-last cloud carries the VoxelGrid centroids, which may differ in
+the last bits because PCL sums a voxel in std::sort's tie order — tests/_compare.py — so the LM
+inputs are not always bit-identical; every other input is).
+"""
+import numpy as np
+import pytest
+
+import oracle_py
+from llsr import Pipeline, _abi, default_config, synth
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+def _sequence(lidar, horizontal, slots, frames):
+    import torch
+    cfg = default_config(lidar, horizontal)
+    cfg.mode = _abi.LLSR_MODE_LM_APPLIED
+    H, W = cfg.num_vertical_scans, cfg.num_horizontal_scans
+    pipe = Pipeline(cfg, max_batch=len(slots), max_points=H * W)
+    oras = [oracle_py.OracleOdometry(cfg) for _ in slots]
+    errs = []
+    for k in range(frames):
+        scans = [synth.make_scan(s0 + k, lidar) for s0 in slots]
+        off = np.zeros(len(scans) + 1, np.int64)
+        off[1:] = np.cumsum([len(s) for s in scans])
+        d_pts = torch.from_numpy(np.concatenate(scans)).cuda()
+        d_off = torch.from_numpy(off).cuda()
+        torch.cuda.synchronize()
+        pipe.odometry_batch(d_pts.data_ptr(), d_off.data_ptr(), len(scans))
+        for b, ora in enumerate(oras):
+            g = pipe.odometry_fetch(b, clouds=True)
+            o = ora.process(scans[b])
+            tag = f"{lidar} slot {b} frame {k}"
+            if g["frames"] != o["frames"]:
+                errs.append(f"{tag}: frames {g['frames']} vs {o['frames']}")
+            if (g["lm"]["skipped"] == 1) != (o["lm"] is None):
+                errs.append(f"{tag}: skipped {g['lm']['skipped']} vs oracle lm {o['lm'] is not None}")
+            for key in ("transform_cur", "transform_sum"):
+                if np.abs(g[key] - o[key]).max() > TOL:
+                    errs.append(f"{tag}: {key} {g[key]} vs {o[key]}")
+            for key in ("corner_last", "surf_last", "corner_scan", "surf_scan"):
+                ref = o[key] if o[key] is not None else np.zeros((0, 4), np.float32)
+                if g[key].shape != ref.shape:
+                    errs.append(f"{tag}: {key} shape {g[key].shape} vs {ref.shape}")
+                elif g[key].size and np.abs(g[key] - ref).max() > TOL * max(1.0, np.abs(ref).max()):
+                    errs.append(f"{tag}: {key} max |d| {np.abs(g[key] - ref).max():.3g}")
+    pipe.close()
+    return errs
+
+
+def test_odometry_vlp16_sequences(require_gpu):
+    errs = _sequence("vlp16", None, [1, 65, 130], 5)
+    assert not errs, "\n".join(errs)
+
+
+def test_odometry_hdl64e_sequence(require_gpu):
+    errs = _sequence("hdl64e", 2048, [5, 70], 3)
+    assert not errs, "\n".join(errs)
+
+
+def test_odometry_needs_lm_applied(require_gpu):
+    import torch
+    from llsr import LlsrError
+    cfg = default_config("vlp16")
+    pipe = Pipeline(cfg, max_batch=1, max_points=28800)
+    pts = synth.make_scan(1, "vlp16")
+    d_pts = torch.from_numpy(pts).cuda()
+    d_off = torch.tensor([0, len(pts)], dtype=torch.int64).cuda()
+    torch.cuda.synchronize()
+    with pytest.raises(LlsrError):
+        pipe.odometry_batch(d_pts.data_ptr(), d_off.data_ptr(), 1)
+    pipe.close()
