@@ -38,6 +38,8 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kMaxShell = 4;  // grid shells searched before the exact brute-force fallback
+constexpr int kLdsRows = 2048;    // Jacobian rows kept in LDS (32 KB); larger phases use the HBM buffer
+constexpr int kLdsCorner = 2048;  // laserCloudCornerLast kept in LDS (32 KB) for a brute-force kNN-1
 
 // TransformToStart (FA:1389-1412)
 __device__ __forceinline__ float4 to_start(const float* t, float4 pi) {
@@ -117,11 +119,24 @@ __device__ void nn1(const CellGrid& g, int p, float4 q, float dist_sqr, int& bi,
 
 // findCorrespondingCornerFeatures search (FA:1587-1648); `fwd` = the reference's forward bound
 // (cornerPointsSharpNum), clamped to the last cloud.
+// Exact nearest neighbour by a scan in index order with strict '<' (ties -> lower index, as nn1).
+__device__ __forceinline__ void nn1_scan(const float4* pts, int n, float4 q, int& bi, float& bd) {
+  bd = INFINITY;
+  bi = INT_MAX;
+  for (int k = 0; k < n; ++k) {
+    const float d = l2(q, pts[k]);
+    if (d < bd) { bd = d; bi = k; }
+  }
+}
+
+// `brute`: cl is the LDS copy of the whole (small) cloud — scanning it beats probing up to 9^3
+// sparse grid cells in HBM for the corner cloud's far-apart points.
 __device__ void corner_search(const CellGrid& g, int p, const float4* cl, int Nc, int fwd, float4 sel,
-                              float dist_sqr, int& i1, int& i2) {
+                              float dist_sqr, bool brute, int& i1, int& i2) {
   int nn;
   float nd;
-  nn1(g, p, sel, dist_sqr, nn, nd);
+  if (brute) nn1_scan(cl, Nc, sel, nn, nd);
+  else nn1(g, p, sel, dist_sqr, nn, nd);
   i1 = -1;
   i2 = -1;
   if (!(nd < dist_sqr)) return;
@@ -186,6 +201,7 @@ __device__ void surf_search(const CellGrid& g, int p, const float4* sl, int Ns, 
 // Jacobian constants of calculateTransformationSurf (FA:1858-1891) / ...Corner (FA:2025-2043)
 struct JacSurf {
   float a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11, crx, b2, b6, c1, c2, c3, c4, c5, c6, c7, c8, c9;
+  JacSurf() = default;
   __device__ explicit JacSurf(const float* t) {
     const float srx = sinf_(t[0]), crx_ = cosf_(t[0]);
     const float sry = sinf_(t[1]), cry = cosf_(t[1]);
@@ -215,6 +231,7 @@ struct JacSurf {
 
 struct JacCorner {
   float b1, b2, b3, b4, b5, b6, b7, b8, c5, srx;
+  JacCorner() = default;
   __device__ explicit JacCorner(const float* t) {
     srx = sinf_(t[0]);
     const float crx = cosf_(t[0]);
@@ -247,6 +264,8 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
   __shared__ float matP[9];
   __shared__ float sums[12];
   __shared__ int cnt, isDeg, stop, n_corr[2], iters[2];
+  __shared__ float4 lrows[kLdsRows];
+  __shared__ float4 lcl[kLdsCorner];
   const CellGrid& gc = a.grids.g[0];
   const CellGrid& gs = a.grids.g[1];
   const int64_t ms0 = a.sharp_off[p], ms1 = a.sharp_off[p + 1], f0 = a.flat_off[p], f1 = a.flat_off[p + 1];
@@ -265,15 +284,22 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
   __syncthreads();
   const bool skipped = bad || Nc < 10 || Ns < 100;  // FA:2506
   if (!skipped) {
+    const bool corner_lds = Nc <= kLdsCorner;
     const float4* cl = gc.src + gc.off[p];
+    if (corner_lds) {
+      for (int k = tid; k < Nc; k += kThreads) lcl[k] = cl[k];
+      cl = lcl;  // visible to every thread after the barrier at the top of the first phase
+    }
     const float4* sl = gs.src + gs.off[p];
     const int capq = a.cap_sharp > a.cap_flat ? a.cap_sharp : a.cap_flat;
     int* idx = a.idx + (size_t)p * capq * 3;
-    float4* rows = a.rows + (size_t)p * capq;
+    float4* grows = a.rows + (size_t)p * capq;
     for (int phase = 0; phase < 2; ++phase) {  // 0: surf (FA:2508-2516), 1: corner (FA:2519-2527)
       const bool surf = phase == 0;
       const float4* qry = surf ? a.flat + f0 : a.sharp + ms0;
       const int Q = surf ? F : Ms;
+      // the rows of this phase: LDS when they fit (phase B re-reads them serially every iteration)
+      float4* rows = Q <= kLdsRows ? lrows : grows;
       if (tid == 0)
         for (int k = 0; k < 9; ++k) matP[k] = (k % 4 == 0) ? 1.0f : 0.0f;
       __syncthreads();
@@ -282,6 +308,11 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
         // ---- A: correspondences + Jacobian rows at the current transformCur ----
         float tl[6];
         for (int k = 0; k < 6; ++k) tl[k] = t[k];
+        // the Jacobian constants depend only on transformCur: once per iteration, not per query
+        JacSurf js;
+        JacCorner jc;
+        if (surf) js = JacSurf(tl);
+        else jc = JacCorner(tl);
         for (int q = tid; q < Q; q += kThreads) {
           const float4 pi = qry[q];
           const float4 sel = to_start(tl, pi);
@@ -291,7 +322,7 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
             if (surf)
               surf_search(gs, p, sl, Ns, F, sel, a.dist_sqr, i1, i2, i3);
             else
-              corner_search(gc, p, cl, Nc, Ms, sel, a.dist_sqr, i1, i2);
+              corner_search(gc, p, cl, Nc, Ms, sel, a.dist_sqr, corner_lds, i1, i2);
             ix[0] = i1; ix[1] = i2; ix[2] = i3;
           }
           float4 row = make_float4(0.f, 0.f, 0.f, __uint_as_float(0x7fc00000u));
@@ -311,7 +342,7 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
                                     (double)sqrt_(sqrt_(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z)));
               if ((double)s > 0.1 && pd2 != 0) {
                 float J[3];
-                JacSurf(tl).row(pi, s * pa, s * pb, s * pc, J);
+                js.row(pi, s * pa, s * pb, s * pc, J);
                 row = make_float4(J[0], J[1], J[2], (float)(-0.05 * (double)(s * pd2)));
               }
             }
@@ -332,7 +363,7 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
             if (it >= 5) s = (float)(1 - 1.8 * (double)fabs_(ld2));
             if ((double)s > 0.1 && ld2 != 0) {
               float J[3];
-              JacCorner(tl).row(pi, s * la, s * lb, s * lc, J);
+              jc.row(pi, s * la, s * lb, s * lc, J);
               row = make_float4(J[0], J[1], J[2], (float)(-0.05 * (double)(s * ld2)));
             }
           }
@@ -344,6 +375,7 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
           const int r = tid % 3, c = (tid / 3) % 3;
           float acc = 0.0f;
           int n = 0;
+#pragma unroll 8
           for (int q = 0; q < Q; ++q) {
             const float4 w = rows[q];
             if (w.w != w.w) continue;  // no correspondence

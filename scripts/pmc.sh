@@ -1,12 +1,14 @@
 #!/bin/bash
 # HBM traffic per kernel from PMC counters, one counter group per rocprofv3 pass (FETCH_SIZE and
-# WRITE_SIZE do not fit one TCC pass), kernel-trace only (no sys/runtime trace with --pmc).
+# WRITE_SIZE do not fit one TCC pass), kernel-trace only (no sys/runtime trace with --pmc). The
+# bench runs 1 stream and no side legs so every dispatch is one whole batch of B scans.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${TAG:-pmc}
+B=${B:-1024}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS="--steps 4 --warmup 1 --no-cpu --streams 1"
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$PWD/$OUT/fetch" -o run -- python3 bench.py $ARGS > "$OUT/fetch.log" 2>&1 || exit $?
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$PWD/$OUT/write" -o run -- python3 bench.py $ARGS > "$OUT/write.log" 2>&1 || exit $?
-python3 scripts/pmc_parse.py "$OUT" > "$OUT/traffic.json"
+ARGS="--steps 3 --warmup 1 --no-cpu --streams 1 --batch $B --s2m-modes= --allreduce-scans 0 --odo="
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$PWD/$OUT/fetch" -o run -- python3 bench.py $ARGS > "$OUT/fetch.log" 2>&1 || exit $?
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$PWD/$OUT/write" -o run -- python3 bench.py $ARGS > "$OUT/write.log" 2>&1 || exit $?
+python3 scripts/pmc_parse.py "$OUT" "$B" > "$OUT/traffic.json"

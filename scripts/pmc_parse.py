@@ -2,7 +2,12 @@
 
 MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half
 the bytes of a wide coalesced streaming read, so it is doubled here (an upper bound for kernels
-whose reads are not 16 B/lane streams; uncalibrated for other widths)."""
+whose reads are not 16 B/lane streams; uncalibrated for other widths). Output: {"batch": B,
+"kernels": {name: {fetch_bytes_x2, write_bytes, hbm_bytes, launches}}} — bench.py scales
+hbm_bytes by its own batch size into roofline.traffic.
+
+    python scripts/pmc_parse.py <dir with fetch/ and write/ passes> <batch>
+"""
 import csv
 import glob
 import json
@@ -11,6 +16,7 @@ import sys
 from collections import defaultdict
 
 d = sys.argv[1]
+batch = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
 
 
 def load(sub, counter):
@@ -22,12 +28,17 @@ def load(sub, counter):
             name = row["Kernel_Name"].split("(")[0].replace("void ", "").replace("llsr::", "")
             name = name.split("<")[0]
             acc[name].append(float(row["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in acc.items()}
+    return acc
 
 
 fetch, write = load("fetch", "FETCH_SIZE"), load("write", "WRITE_SIZE")
 out = {}
 for k in sorted(set(fetch) | set(write)):
-    f, w = fetch.get(k, 0.0) * 1024 * 2, write.get(k, 0.0) * 1024
-    out[k] = {"fetch_bytes_x2": f, "write_bytes": w, "hbm_bytes": f + w}
-print(json.dumps(out, indent=1))
+    fv, wv = fetch.get(k, []), write.get(k, [])
+    f = (sum(fv) / len(fv) if fv else 0.0) * 1024 * 2
+    w = (sum(wv) / len(wv) if wv else 0.0) * 1024
+    out[k] = {"fetch_bytes_x2": f, "write_bytes": w, "hbm_bytes": f + w, "launches": max(len(fv), len(wv))}
+# the fused VLP-16 projection is reported under the bench's kernel name
+if "k_project_fused" in out:
+    out["k_project"] = out["k_project_fused"]
+print(json.dumps({"batch": batch, "kernels": out}, indent=1))
