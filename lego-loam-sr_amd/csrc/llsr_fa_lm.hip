@@ -4,14 +4,16 @@
 // k_s2s_lm: one 256-thread workgroup per scan runs the whole two-phase optimisation in-kernel
 // (no host round trips): surf phase (FA:2508-2516) then corner phase (FA:2519-2527), each up to
 // 100 iterations. Per iteration:
-//   A  every thread takes queries q = tid, tid + 256, ...: TransformToStart (FA:1389-1412); on
-//      iterations % 5 == 0 the kNN-1 in the last cloud (exact shell search over its 1 m cell
-//      grid, llsr_grid.h, brute force beyond kMaxShell) and the ring-constrained scans for the
-//      second / third tripod point in the last cloud's own order (FA:1588-1647, 1737-1803);
-//      then the line / plane coefficient (FA:1650-1695, 1806-1842) and the Jacobian row of
-//      calculateTransformation{Surf,Corner} (FA:1893-1913, 2046-2062), written to a row buffer;
-//   B  13 lanes of wave 0 sum the rows in correspondence order — one lane per entry of the
-//      3x3 AtA / 3-vector AtB, plus the count — the oracle's summation order exactly;
+//   A  on iterations % 5 == 0 the kNN-1 of every query (q = tid, tid + 256, ...) after
+//      TransformToStart (FA:1389-1412) in the last cloud: the sparse corner cloud is scanned from
+//      LDS, the surf cloud searched over shells of its 1 m cell grid (llsr_grid.h), and queries
+//      the shells leave open are resolved by a block-wide scan; then the ring-constrained scans
+//      for the second / third tripod point in the last cloud's own order (FA:1588-1647,
+//      1737-1803). Every iteration: the line / plane coefficient (FA:1650-1695, 1806-1842) and
+//      the Jacobian row of calculateTransformation{Surf,Corner} (FA:1893-1913, 2046-2062) into an
+//      LDS row buffer (zeros without a correspondence; the valid rows are counted);
+//   B  12 lanes of wave 0 sum the rows in correspondence order — one lane per entry of the
+//      3x3 AtA / 3-vector AtB — the oracle's summation order exactly;
 //   C  thread 0: ColPivHouseholderQR solve, SelfAdjointEigenSolver degeneracy test at
 //      iteration 0, projection, pose update, NaN reset, stop test (FA:1915-2009, 2064-2142).
 // Float / double typing follows each reference line, sin/cos are the glibc ports, so results
@@ -40,6 +42,7 @@ constexpr int kThreads = 256;
 constexpr int kMaxShell = 4;  // grid shells searched before the exact brute-force fallback
 constexpr int kLdsRows = 2048;    // Jacobian rows kept in LDS (32 KB); larger phases use the HBM buffer
 constexpr int kLdsCorner = 2048;  // laserCloudCornerLast kept in LDS (32 KB) for a brute-force kNN-1
+constexpr int kFbMax = 256;       // queries per kNN iteration whose shells did not settle (block scan)
 
 // TransformToStart (FA:1389-1412)
 __device__ __forceinline__ float4 to_start(const float* t, float4 pi) {
@@ -72,10 +75,11 @@ __device__ __forceinline__ float l2(float4 q, float4 p) {
   return d;
 }
 
-// Exact nearest neighbour of q in grid g of problem p (KdTreeFLANN::nearestKSearch, k = 1;
-// ties -> lower index). Stops once the searched shells provably contain the nearest point or
-// nothing nearer than dist_sqr can remain outside them.
-__device__ void nn1(const CellGrid& g, int p, float4 q, float dist_sqr, int& bi, float& bd) {
+// Nearest neighbour of q in grid g of problem p (KdTreeFLANN::nearestKSearch, k = 1; ties ->
+// lower index) over growing shells of 1 m cells. Returns true once the searched shells provably
+// contain the nearest point or nothing nearer than dist_sqr can remain outside them; false when
+// kMaxShell shells do not settle it (the caller then scans the whole cloud, nn1_block).
+__device__ bool nn1_shells(const CellGrid& g, int p, float4 q, float dist_sqr, int& bi, float& bd) {
   const CellSlot* tab = g.table(p);
   const float4* pts = g.cells(p);
   bd = INFINITY;
@@ -105,21 +109,13 @@ __device__ void nn1(const CellGrid& g, int p, float4 q, float dist_sqr, int& bi,
     r = fminf(r, q.z - (float)(cz - h));
     r = fminf(r, (float)(cz + h + 1) - q.z);
     const float r2 = r * r * (1.0f - 1e-5f);
-    if (bd < r2 || r2 >= dist_sqr) return;
+    if (bd < r2 || r2 >= dist_sqr) return true;
   }
-  const float4* src = g.src + g.off[p];
-  const int n = g.count(p);
-  bd = INFINITY;
-  bi = INT_MAX;
-  for (int k = 0; k < n; ++k) {
-    const float d = l2(q, src[k]);
-    if (d < bd) { bd = d; bi = k; }
-  }
+  return false;
 }
 
-// findCorrespondingCornerFeatures search (FA:1587-1648); `fwd` = the reference's forward bound
-// (cornerPointsSharpNum), clamped to the last cloud.
-// Exact nearest neighbour by a scan in index order with strict '<' (ties -> lower index, as nn1).
+// Exact nearest neighbour by a scan in index order with strict '<' (ties -> lower index, as the
+// shells).
 __device__ __forceinline__ void nn1_scan(const float4* pts, int n, float4 q, int& bi, float& bd) {
   bd = INFINITY;
   bi = INT_MAX;
@@ -129,14 +125,36 @@ __device__ __forceinline__ void nn1_scan(const float4* pts, int n, float4 q, int
   }
 }
 
-// `brute`: cl is the LDS copy of the whole (small) cloud — scanning it beats probing up to 9^3
-// sparse grid cells in HBM for the corner cloud's far-apart points.
-__device__ void corner_search(const CellGrid& g, int p, const float4* cl, int Nc, int fwd, float4 sel,
-                              float dist_sqr, bool brute, int& i1, int& i2) {
-  int nn;
-  float nd;
-  if (brute) nn1_scan(cl, Nc, sel, nn, nd);
-  else nn1(g, p, sel, dist_sqr, nn, nd);
+// The same scan by the whole block: each thread scans an interleaved slice in index order, then
+// the (d, index) minima are reduced with the index tie-break — equal to nn1_scan. Contains
+// barriers: every thread of the block must call it.
+__device__ void nn1_block(const float4* pts, int n, float4 q, int& bi, float& bd, float* red_d, int* red_i) {
+  float d = INFINITY;
+  int i = INT_MAX;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    const float dd = l2(q, pts[k]);
+    if (dd < d) { d = dd; i = k; }
+  }
+  for (int off = 32; off; off >>= 1) {
+    const float od = __shfl_xor(d, off, 64);
+    const int oi = __shfl_xor(i, off, 64);
+    if (nn_before(od, oi, d, i)) { d = od; i = oi; }
+  }
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane_id() == 0) { red_d[w] = d; red_i[w] = i; }
+  __syncthreads();
+  bd = red_d[0];
+  bi = red_i[0];
+  for (int k = 1; k < nw; ++k)
+    if (nn_before(red_d[k], red_i[k], bd, bi)) { bd = red_d[k]; bi = red_i[k]; }
+  __syncthreads();
+}
+
+// findCorrespondingCornerFeatures search (FA:1587-1648) around the nearest neighbour nn (squared
+// distance nd); `fwd` = the reference's forward bound (cornerPointsSharpNum), clamped to the last
+// cloud.
+__device__ void corner_finish(const float4* cl, int Nc, int fwd, float4 sel, float dist_sqr, int nn, float nd,
+                              int& i1, int& i2) {
   i1 = -1;
   i2 = -1;
   if (!(nd < dist_sqr)) return;
@@ -161,11 +179,8 @@ __device__ void corner_search(const CellGrid& g, int p, const float4* cl, int Nc
 }
 
 // findCorrespondingSurfFeatures search (FA:1724-1809)
-__device__ void surf_search(const CellGrid& g, int p, const float4* sl, int Ns, int fwd, float4 sel,
-                            float dist_sqr, int& i1, int& i2, int& i3) {
-  int nn;
-  float nd;
-  nn1(g, p, sel, dist_sqr, nn, nd);
+__device__ void surf_finish(const float4* sl, int Ns, int fwd, float4 sel, float dist_sqr, int nn, float nd,
+                            int& i1, int& i2, int& i3) {
   i1 = -1;
   i2 = -1;
   i3 = -1;
@@ -257,15 +272,36 @@ struct JacCorner {
 
 }  // namespace
 
+// Diagnostic build only (make prof -> libllsr_prof.so): thread 0 accumulates the wall clock of
+// each phase and the report's transform_cur carries {A with kNN, A, B, C} in 10 ns ticks.
+#ifdef LLSR_S2S_PROF
+#define LLSR_STAMP(acc)                                    \
+  do {                                                     \
+    if (tid == 0) {                                        \
+      const unsigned long long t1_ = wall_clock64();       \
+      acc += t1_ - tprev;                                  \
+      tprev = t1_;                                         \
+    }                                                      \
+  } while (0)
+#else
+#define LLSR_STAMP(acc) do {} while (0)
+#endif
+
 __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
   const int p = blockIdx.x;
   const int tid = threadIdx.x;
+#ifdef LLSR_S2S_PROF
+  unsigned long long tprev = wall_clock64(), tAks = 0, tAkc = 0, tA = 0, tB = 0, tC = 0;
+#endif
   __shared__ float t[6];
   __shared__ float matP[9];
   __shared__ float sums[12];
-  __shared__ int cnt, isDeg, stop, n_corr[2], iters[2];
+  __shared__ int isDeg, stop, n_corr[2], iters[2];
   __shared__ float4 lrows[kLdsRows];
   __shared__ float4 lcl[kLdsCorner];
+  __shared__ int fbq[kFbMax], nfb, nvalid;
+  __shared__ float red_d[kThreads / 64];
+  __shared__ int red_i[kThreads / 64];
   const CellGrid& gc = a.grids.g[0];
   const CellGrid& gs = a.grids.g[1];
   const int64_t ms0 = a.sharp_off[p], ms1 = a.sharp_off[p + 1], f0 = a.flat_off[p], f1 = a.flat_off[p + 1];
@@ -279,13 +315,16 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
     isDeg = a.degen[p];
     n_corr[0] = n_corr[1] = 0;
     iters[0] = iters[1] = 0;
+    nfb = 0;
+    nvalid = 0;
     if (bad) atomicOr(a.error, 1);
   }
   __syncthreads();
   const bool skipped = bad || Nc < 10 || Ns < 100;  // FA:2506
   if (!skipped) {
     const bool corner_lds = Nc <= kLdsCorner;
-    const float4* cl = gc.src + gc.off[p];
+    const float4* clg = gc.src + gc.off[p];
+    const float4* cl = clg;
     if (corner_lds) {
       for (int k = tid; k < Nc; k += kThreads) lcl[k] = cl[k];
       cl = lcl;  // visible to every thread after the barrier at the top of the first phase
@@ -313,19 +352,57 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
         JacCorner jc;
         if (surf) js = JacSurf(tl);
         else jc = JacCorner(tl);
+        const bool knn = it % 5 == 0;
+        // the ring-constrained tripod search around a found nearest neighbour (FA:1588-1647 /
+        // FA:1737-1803) and the correspondence indices it leaves in idx
+        auto finish = [&](int q, float4 sel, int nn, float nd) {
+          int i1, i2, i3 = -1;
+          if (surf) surf_finish(sl, Ns, F, sel, a.dist_sqr, nn, nd, i1, i2, i3);
+          else corner_finish(cl, Nc, Ms, sel, a.dist_sqr, nn, nd, i1, i2);
+          int* ix = idx + 3 * q;
+          ix[0] = i1; ix[1] = i2; ix[2] = i3;
+        };
+        if (knn) {  // kNN-1 every 5th iteration (FA:1588 / 1724)
+          for (int q = tid; q < Q; q += kThreads) {
+            const float4 sel = to_start(tl, qry[q]);
+            int nn;
+            float nd;
+            bool ok = true;
+            if (!surf && corner_lds) nn1_scan(cl, Nc, sel, nn, nd);  // the sparse corner cloud, from LDS
+            else ok = nn1_shells(surf ? gs : gc, p, sel, a.dist_sqr, nn, nd);
+            if (ok) {
+              finish(q, sel, nn, nd);
+            } else {
+              const int k = atomicAdd(&nfb, 1);
+              if (k < kFbMax) {
+                fbq[k] = q;
+              } else {  // overflow of the queue: the serial scan (same result)
+                nn1_scan(surf ? sl : clg, surf ? Ns : Nc, sel, nn, nd);
+                finish(q, sel, nn, nd);
+              }
+            }
+          }
+          __syncthreads();
+          // queries the shells left open: the whole block scans the cloud for each of them
+          const int nq = nfb < kFbMax ? nfb : kFbMax;
+          for (int k = 0; k < nq; ++k) {
+            const int q = fbq[k];
+            const float4 sel = to_start(tl, qry[q]);
+            int nn;
+            float nd;
+            nn1_block(surf ? sl : clg, surf ? Ns : Nc, sel, nn, nd, red_d, red_i);
+            if (tid == (k & (kThreads - 1))) finish(q, sel, nn, nd);
+          }
+          if (tid == 0) nfb = 0;
+          __syncthreads();
+        }
+        int nval = 0;
         for (int q = tid; q < Q; q += kThreads) {
           const float4 pi = qry[q];
           const float4 sel = to_start(tl, pi);
-          int* ix = idx + 3 * q;
-          if (it % 5 == 0) {
-            int i1, i2, i3 = -1;
-            if (surf)
-              surf_search(gs, p, sl, Ns, F, sel, a.dist_sqr, i1, i2, i3);
-            else
-              corner_search(gc, p, cl, Nc, Ms, sel, a.dist_sqr, corner_lds, i1, i2);
-            ix[0] = i1; ix[1] = i2; ix[2] = i3;
-          }
-          float4 row = make_float4(0.f, 0.f, 0.f, __uint_as_float(0x7fc00000u));
+          const int* ix = idx + 3 * q;
+          float4 row = make_float4(0.f, 0.f, 0.f, 0.f);  // no correspondence: adds exact zeros
+          bool valid = false;
           if (surf) {
             if (ix[1] >= 0 && ix[2] >= 0) {
               const float4 t1 = sl[ix[0]], t2 = sl[ix[1]], t3 = sl[ix[2]];
@@ -344,6 +421,7 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
                 float J[3];
                 js.row(pi, s * pa, s * pb, s * pc, J);
                 row = make_float4(J[0], J[1], J[2], (float)(-0.05 * (double)(s * pd2)));
+                valid = true;
               }
             }
           } else if (ix[1] >= 0) {
@@ -365,32 +443,44 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
               float J[3];
               jc.row(pi, s * la, s * lb, s * lc, J);
               row = make_float4(J[0], J[1], J[2], (float)(-0.05 * (double)(s * ld2)));
+              valid = true;
             }
           }
           rows[q] = row;
+          nval += valid ? 1 : 0;
         }
+        if (nval) atomicAdd(&nvalid, nval);
         __syncthreads();
+        if (it % 5 == 0 && surf) LLSR_STAMP(tAks);
+        else if (it % 5 == 0) LLSR_STAMP(tAkc);
+        else LLSR_STAMP(tA);
         // ---- B: AtA / AtB summed in correspondence order, one lane per entry ----
-        if (tid < 13) {
-          const int r = tid % 3, c = (tid / 3) % 3;
+        if (tid < 12) {
+          // lane r + 3c sums AtA(r, c), lanes 9..11 AtB: the products of two components of each
+          // row in correspondence order (FA:1915-1923 / 2064-2072). A row without a correspondence
+          // is all zeros, and adding +0 leaves the sum bit-identical (a sum started at +0 is never
+          // -0), so the loop needs no test; rows are read 8 at a time.
+          const int ra = tid < 9 ? tid % 3 : tid - 9, rb = tid < 9 ? tid / 3 : 3;
+          const float* rf = reinterpret_cast<const float*>(rows);
           float acc = 0.0f;
-          int n = 0;
-#pragma unroll 8
-          for (int q = 0; q < Q; ++q) {
-            const float4 w = rows[q];
-            if (w.w != w.w) continue;  // no correspondence
-            const float J[3] = {w.x, w.y, w.z};
-            if (tid < 9) acc += J[r] * J[c];
-            else if (tid < 12) acc += J[tid - 9] * w.w;
-            else ++n;
+          int q = 0;
+          for (; q + 8 <= Q; q += 8) {
+            float u0[8], u1[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) { u0[u] = rf[4 * (q + u) + ra]; u1[u] = rf[4 * (q + u) + rb]; }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc += u0[u] * u1[u];
           }
-          if (tid < 12) sums[tid] = acc;
-          else cnt = n;
+          for (; q < Q; ++q) acc += rf[4 * q + ra] * rf[4 * q + rb];
+          sums[tid] = acc;
         }
         __syncthreads();
+        LLSR_STAMP(tB);
         // ---- C: solve and update (thread 0) ----
         if (tid == 0) {
           stop = 0;
+          const int cnt = nvalid;
+          nvalid = 0;  // counted again by the next phase A (after the end-of-iteration barrier)
           n_corr[phase] = cnt;
           if (cnt >= 10) {  // FA:2514 / 2525
             float AtA[9], AtB[3], X[3];
@@ -441,6 +531,7 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
           }
         }
         __syncthreads();
+        LLSR_STAMP(tC);
         if (stop) break;
       }
       if (tid == 0) iters[phase] = it;
@@ -460,6 +551,10 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
       a.tcur[6 * p + k] = t[k];
     }
     r.ms = 0.0f;
+#ifdef LLSR_S2S_PROF
+    r.transform_cur[0] = (float)tAks; r.transform_cur[1] = (float)tAkc; r.transform_cur[2] = (float)tA;
+    r.transform_cur[3] = (float)tB; r.transform_cur[4] = (float)tC;
+#endif
     a.degen[p] = isDeg;
   }
 }
