@@ -39,7 +39,7 @@ using llsr_libm::sqrt_;
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kMaxShell = 4;  // grid shells searched before the exact brute-force fallback
+constexpr int kMaxShell = 2;  // grid shells searched before the exact block-wide scan (queries in sparse regions)
 constexpr int kLdsRows = 2048;    // Jacobian rows kept in LDS (32 KB); larger phases use the HBM buffer
 constexpr int kLdsCorner = 2048;  // laserCloudCornerLast kept in LDS (32 KB) for a brute-force kNN-1
 constexpr int kFbMax = 256;       // queries per kNN iteration whose shells did not settle (block scan)
@@ -125,29 +125,90 @@ __device__ __forceinline__ void nn1_scan(const float4* pts, int n, float4 q, int
   }
 }
 
-// The same scan by the whole block: each thread scans an interleaved slice in index order, then
-// the (d, index) minima are reduced with the index tie-break — equal to nn1_scan. Contains
-// barriers: every thread of the block must call it.
-__device__ void nn1_block(const float4* pts, int n, float4 q, int& bi, float& bd, float* red_d, int* red_i) {
-  float d = INFINITY;
-  int i = INT_MAX;
+// nn1_scan for up to kMulti queries at once by the whole block: each thread scans an interleaved
+// slice of the cloud in index order against every query, then each query's (d, index) minima are
+// reduced with the index tie-break — equal to nn1_scan per query, with one pass over the cloud
+// for kMulti queries. Contains barriers: every thread of the block must call it.
+constexpr int kMulti = 4;
+__device__ void nn1_block_multi(const float4* pts, int n, const float4* qs, int nq, int* bi, float* bd,
+                                float (*red_d)[kThreads / 64], int (*red_i)[kThreads / 64]) {
+  float d[kMulti];
+  int id[kMulti];
+#pragma unroll
+  for (int j = 0; j < kMulti; ++j) { d[j] = INFINITY; id[j] = INT_MAX; }
   for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    const float dd = l2(q, pts[k]);
-    if (dd < d) { d = dd; i = k; }
-  }
-  for (int off = 32; off; off >>= 1) {
-    const float od = __shfl_xor(d, off, 64);
-    const int oi = __shfl_xor(i, off, 64);
-    if (nn_before(od, oi, d, i)) { d = od; i = oi; }
+    const float4 p = pts[k];
+#pragma unroll
+    for (int j = 0; j < kMulti; ++j)
+      if (j < nq) {
+        const float dd = l2(qs[j], p);
+        if (dd < d[j]) { d[j] = dd; id[j] = k; }
+      }
   }
   const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  if (lane_id() == 0) { red_d[w] = d; red_i[w] = i; }
+#pragma unroll
+  for (int j = 0; j < kMulti; ++j) {
+    for (int off = 32; off; off >>= 1) {
+      const float od = __shfl_xor(d[j], off, 64);
+      const int oi = __shfl_xor(id[j], off, 64);
+      if (nn_before(od, oi, d[j], id[j])) { d[j] = od; id[j] = oi; }
+    }
+    if (lane_id() == 0) { red_d[j][w] = d[j]; red_i[j][w] = id[j]; }
+  }
   __syncthreads();
-  bd = red_d[0];
-  bi = red_i[0];
-  for (int k = 1; k < nw; ++k)
-    if (nn_before(red_d[k], red_i[k], bd, bi)) { bd = red_d[k]; bi = red_i[k]; }
+  for (int j = 0; j < nq; ++j) {
+    float bdj = red_d[j][0];
+    int bij = red_i[j][0];
+    for (int k = 1; k < nw; ++k)
+      if (nn_before(red_d[j][k], red_i[j][k], bdj, bij)) { bdj = red_d[j][k]; bij = red_i[j][k]; }
+    bd[j] = bdj;
+    bi[j] = bij;
+  }
   __syncthreads();
+}
+
+// findCorrespondingCornerFeatures search (FA:1587-1648) around the nearest neighbour nn (squared
+// distance nd); `fwd` = the reference's forward bound (cornerPointsSharpNum), clamped to the last
+// cloud.
+// The two linear scans of the tripod searches walk the last cloud away from the nearest neighbour
+// until the ring leaves [cs - 2.5, cs + 2.5]; they read 8 points per step (all loads in flight at
+// once) and replay the serial test on them in order, so the result is the serial loop's.
+constexpr int kScan = 4;
+
+template <class Visit>
+__device__ __forceinline__ void scan_up(const float4* pts, int from, int end, int cs, Visit visit) {
+  for (int j0 = from; j0 < end; j0 += kScan) {
+    float4 c[kScan];
+#pragma unroll
+    for (int u = 0; u < kScan; ++u) c[u] = j0 + u < end ? pts[j0 + u] : make_float4(0.f, 0.f, 0.f, 0.f);
+    bool stop = false;
+#pragma unroll
+    for (int u = 0; u < kScan; ++u) {
+      if (stop || j0 + u >= end) continue;
+      const int rj = trunc_i32(c[u].w);
+      if ((double)rj > (double)cs + 2.5) stop = true;
+      else visit(j0 + u, c[u], rj);
+    }
+    if (stop) return;
+  }
+}
+
+template <class Visit>
+__device__ __forceinline__ void scan_down(const float4* pts, int from, int cs, Visit visit) {
+  for (int j0 = from; j0 >= 0; j0 -= kScan) {
+    float4 c[kScan];
+#pragma unroll
+    for (int u = 0; u < kScan; ++u) c[u] = j0 - u >= 0 ? pts[j0 - u] : make_float4(0.f, 0.f, 0.f, 0.f);
+    bool stop = false;
+#pragma unroll
+    for (int u = 0; u < kScan; ++u) {
+      if (stop || j0 - u < 0) continue;
+      const int rj = trunc_i32(c[u].w);
+      if ((double)rj < (double)cs - 2.5) stop = true;
+      else visit(j0 - u, c[u], rj);
+    }
+    if (stop) return;
+  }
 }
 
 // findCorrespondingCornerFeatures search (FA:1587-1648) around the nearest neighbour nn (squared
@@ -161,21 +222,17 @@ __device__ void corner_finish(const float4* cl, int Nc, int fwd, float4 sel, flo
   i1 = nn;
   const int cs = trunc_i32(cl[nn].w);
   float m2 = dist_sqr;
+  int b2 = -1;
   const int end = fwd < Nc ? fwd : Nc;
-  for (int j = nn + 1; j < end; j++) {
-    const float4 c = cl[j];
-    const int rj = trunc_i32(c.w);
-    if ((double)rj > (double)cs + 2.5) break;
+  scan_up(cl, nn + 1, end, cs, [&](int j, float4 c, int rj) {
     const float d = sqdis(c, sel);
-    if (rj > cs && d < m2) { m2 = d; i2 = j; }
-  }
-  for (int j = nn - 1; j >= 0; j--) {
-    const float4 c = cl[j];
-    const int rj = trunc_i32(c.w);
-    if ((double)rj < (double)cs - 2.5) break;
+    if (rj > cs && d < m2) { m2 = d; b2 = j; }
+  });
+  scan_down(cl, nn - 1, cs, [&](int j, float4 c, int rj) {
     const float d = sqdis(c, sel);
-    if (rj < cs && d < m2) { m2 = d; i2 = j; }
-  }
+    if (rj < cs && d < m2) { m2 = d; b2 = j; }
+  });
+  i2 = b2;
 }
 
 // findCorrespondingSurfFeatures search (FA:1724-1809)
@@ -188,29 +245,26 @@ __device__ void surf_finish(const float4* sl, int Ns, int fwd, float4 sel, float
   i1 = nn;
   const int cs = trunc_i32(sl[nn].w);
   float m2 = dist_sqr, m3 = dist_sqr;
+  int b2 = -1, b3 = -1;
   const int end = fwd < Ns ? fwd : Ns;
-  for (int j = nn + 1; j < end; j++) {
-    const float4 c = sl[j];
-    const int rj = trunc_i32(c.w);
-    if ((double)rj > (double)cs + 2.5) break;
+  scan_up(sl, nn + 1, end, cs, [&](int j, float4 c, int rj) {
     const float d = sqdis(c, sel);
     if (rj <= cs) {
-      if (d < m2) { m2 = d; i2 = j; }
+      if (d < m2) { m2 = d; b2 = j; }
     } else {
-      if (d < m3) { m3 = d; i3 = j; }
+      if (d < m3) { m3 = d; b3 = j; }
     }
-  }
-  for (int j = nn - 1; j >= 0; j--) {
-    const float4 c = sl[j];
-    const int rj = trunc_i32(c.w);
-    if ((double)rj < (double)cs - 2.5) break;
+  });
+  scan_down(sl, nn - 1, cs, [&](int j, float4 c, int rj) {
     const float d = sqdis(c, sel);
     if (rj >= cs) {
-      if (d < m2) { m2 = d; i2 = j; }
+      if (d < m2) { m2 = d; b2 = j; }
     } else {
-      if (d < m3) { m3 = d; i3 = j; }
+      if (d < m3) { m3 = d; b3 = j; }
     }
-  }
+  });
+  i2 = b2;
+  i3 = b3;
 }
 
 // Jacobian constants of calculateTransformationSurf (FA:1858-1891) / ...Corner (FA:2025-2043)
@@ -300,8 +354,8 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
   __shared__ float4 lrows[kLdsRows];
   __shared__ float4 lcl[kLdsCorner];
   __shared__ int fbq[kFbMax], nfb, nvalid;
-  __shared__ float red_d[kThreads / 64];
-  __shared__ int red_i[kThreads / 64];
+  __shared__ float red_d[kMulti][kThreads / 64];
+  __shared__ int red_i[kMulti][kThreads / 64];
   const CellGrid& gc = a.grids.g[0];
   const CellGrid& gs = a.grids.g[1];
   const int64_t ms0 = a.sharp_off[p], ms1 = a.sharp_off[p + 1], f0 = a.flat_off[p], f1 = a.flat_off[p + 1];
@@ -363,13 +417,38 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
           ix[0] = i1; ix[1] = i2; ix[2] = i3;
         };
         if (knn) {  // kNN-1 every 5th iteration (FA:1588 / 1724)
-          for (int q = tid; q < Q; q += kThreads) {
+          if (!surf && corner_lds) {
+            // the sparse corner cloud from LDS: each thread scans it once for up to kMulti of its
+            // queries (index order, strict '<': nn1_scan per query)
+            for (int q0 = tid; q0 < Q; q0 += kThreads * kMulti) {
+              float4 qs[kMulti];
+              float bd[kMulti];
+              int bi[kMulti];
+#pragma unroll
+              for (int j = 0; j < kMulti; ++j) {
+                const int q = q0 + j * kThreads;
+                qs[j] = q < Q ? to_start(tl, qry[q]) : make_float4(0.f, 0.f, 0.f, 0.f);
+                bd[j] = INFINITY;
+                bi[j] = INT_MAX;
+              }
+              for (int k = 0; k < Nc; ++k) {
+                const float4 c = cl[k];
+#pragma unroll
+                for (int j = 0; j < kMulti; ++j) {
+                  const float d = l2(qs[j], c);
+                  if (d < bd[j]) { bd[j] = d; bi[j] = k; }
+                }
+              }
+#pragma unroll
+              for (int j = 0; j < kMulti; ++j)
+                if (q0 + j * kThreads < Q) finish(q0 + j * kThreads, qs[j], bi[j], bd[j]);
+            }
+          }
+          for (int q = tid; q < Q && !(!surf && corner_lds); q += kThreads) {
             const float4 sel = to_start(tl, qry[q]);
             int nn;
             float nd;
-            bool ok = true;
-            if (!surf && corner_lds) nn1_scan(cl, Nc, sel, nn, nd);  // the sparse corner cloud, from LDS
-            else ok = nn1_shells(surf ? gs : gc, p, sel, a.dist_sqr, nn, nd);
+            const bool ok = nn1_shells(surf ? gs : gc, p, sel, a.dist_sqr, nn, nd);
             if (ok) {
               finish(q, sel, nn, nd);
             } else {
@@ -383,15 +462,19 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
             }
           }
           __syncthreads();
-          // queries the shells left open: the whole block scans the cloud for each of them
+          // queries the shells left open: the whole block scans the cloud, kMulti queries per pass
           const int nq = nfb < kFbMax ? nfb : kFbMax;
-          for (int k = 0; k < nq; ++k) {
-            const int q = fbq[k];
-            const float4 sel = to_start(tl, qry[q]);
-            int nn;
-            float nd;
-            nn1_block(surf ? sl : clg, surf ? Ns : Nc, sel, nn, nd, red_d, red_i);
-            if (tid == (k & (kThreads - 1))) finish(q, sel, nn, nd);
+          for (int k0 = 0; k0 < nq; k0 += kMulti) {
+            const int m = nq - k0 < kMulti ? nq - k0 : kMulti;
+            float4 qs[kMulti];
+#pragma unroll
+            for (int j = 0; j < kMulti; ++j) qs[j] = j < m ? to_start(tl, qry[fbq[k0 + j]]) : make_float4(0.f, 0.f, 0.f, 0.f);
+            int nn[kMulti];
+            float nd[kMulti];
+            nn1_block_multi(surf ? sl : clg, surf ? Ns : Nc, qs, m, nn, nd, red_d, red_i);
+#pragma unroll
+            for (int j = 0; j < kMulti; ++j)
+              if (j < m && tid == j) finish(fbq[k0 + j], qs[j], nn[j], nd[j]);
           }
           if (tid == 0) nfb = 0;
           __syncthreads();
