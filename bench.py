@@ -465,7 +465,7 @@ def main():
     csum["M2"] = float((cnt[:, 3].astype(np.float64) ** 2).sum())  # DBSCAN pair count
     HWB = float(H * W * B)
     per = {k: kernel_bytes(k, csum, HWB) for k in ktimes}
-    if ktimes.get("k_gather_column", 1.0) == 0.0:  # fused projection kernel (H*W fits LDS)
+    if H <= 16 and H * W <= 32768:  # fused projection kernel (H*W fits LDS): one launch does both
         per["k_project"] += per["k_gather_column"]
         per["k_gather_column"] = 0.0
     dom = max((k for k in ktimes if k != "init"), key=lambda k: ktimes[k])

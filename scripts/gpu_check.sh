@@ -19,5 +19,6 @@ step() {  # name timeout cmd...
 if [ "${PROF:-1}" = 1 ]; then
   export TMPDIR=/tmp
   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof" -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu
+  python3 scripts/trace_prof_pass.py "$OUT/prof/run_kernel_trace.csv" 1 5 3 > "$OUT/prof_pass.json" 2>&1
 fi
 echo done >> "$OUT/steps.log"
