@@ -314,6 +314,70 @@ int32_t llsr_odometry_fetch(llsr_handle* h, int32_t b, llsr_odom_slot* out, floa
 /* Start every slot over: transformCur / transformSum = 0, no last clouds, FA carry-over reset. */
 int32_t llsr_odometry_reset(llsr_handle* h);
 
+/* ---- MapOptimization local map (llsr_map.hip) ----
+ * The keyframe store of saveKeyFramesAndFactor (MO:1686-1752) kept in HBM, the local-map assembly
+ * of extractSurroundingKeyFrames (MO:1151-1231, loop closure disabled as in every config block,
+ * CFG:23) and the downSizeFilter* VoxelGrids (MO:92-104; downsampleCurrentScan MO:1234-1267), on
+ * the device. A llsr_map is independent of any llsr_handle, one per mapped sequence; it owns a
+ * non-blocking stream used when hip_stream is NULL. Point clouds are float4 x, y, z, intensity.
+ * VoxelGrid = pcl::VoxelGrid<PointXYZI>::filter (downsample_all_data, 0 min points): same voxel
+ * set and output order (ascending voxel index) as PCL; each centroid sums its voxel's points in
+ * input order (PCL sums them in std::sort's order: float rounding only). */
+typedef struct llsr_map llsr_map;
+typedef struct llsr_map_config {
+  float surrounding_radius;  /* surrounding_keyframe_search_radius, 50 m (CFG:26) */
+  float keypose_leaf;        /* downSizeFilterSurroundingKeyPoses, 1.0 (MO:99) */
+  float corner_leaf;         /* downSizeFilterCorner, 0.2 (MO:92) */
+  float surf_leaf;           /* downSizeFilterSurf, 0.4 (MO:93) */
+  float outlier_leaf;        /* downSizeFilterOutlier, 0.4 (MO:94) */
+} llsr_map_config;
+int32_t llsr_map_config_default(llsr_map_config* cfg);
+llsr_map* llsr_map_create(const llsr_map_config* cfg, int32_t hip_device);
+void llsr_map_destroy(llsr_map* m);
+const char* llsr_map_last_error(const llsr_map* m);
+/* Drop every keyframe and the surrounding-keyframe list. */
+int32_t llsr_map_reset(llsr_map* m);
+/* VoxelGrid of S independent clouds packed in d_in (device float4); off[S+1] and leaf[S] are host
+ * arrays; d_out (device, capacity off[S] points) receives the S results packed, out_off[S+1]
+ * (host) their offsets. Synchronises hip_stream. */
+int32_t llsr_map_voxel_grid(llsr_map* m, const float* d_in, const int64_t* off, int32_t S, const float* leaf,
+                            float* d_out, int64_t* out_off, void* hip_stream);
+/* downsampleCurrentScan (MO:1234-1267). Inputs (device float4): laserCloudCornerLast, SurfLast,
+ * OutlierLast, CornerScan, SurfScan. d_out (capacity n_cl + n_sl + n_ol + n_cs + n_ss + n_sl +
+ * n_ol points) receives, packed in this order: CornerLastDS (corner leaf), SurfLastDS (surf leaf),
+ * OutlierLastDS (outlier leaf), CornerScanDS, SurfScanDS, SurfTotalLastDS (= surf leaf over
+ * SurfLastDS + OutlierLastDS); out_off[7] (host) their offsets. Synchronises. */
+int32_t llsr_map_downsample_scan(llsr_map* m, const float* corner_last, int32_t n_cl, const float* surf_last,
+                                 int32_t n_sl, const float* outlier_last, int32_t n_ol, const float* corner_scan,
+                                 int32_t n_cs, const float* surf_scan, int32_t n_ss, float* d_out, int64_t* out_off,
+                                 void* hip_stream);
+/* saveKeyFramesAndFactor's store (MO:1686-1752): key pose x, y, z, roll, pitch, yaw (PointTypePose;
+ * cloudKeyPoses3D = x, y, z with intensity = the returned keyframe index) and the keyframe's corner
+ * (laserCloudCornerScan), surf (SurfLastDS) and outlier (OutlierLastDS) clouds, copied into the
+ * store (device or host pointers). Returns the index (>= 0) or an error. */
+int32_t llsr_map_add_keyframe(llsr_map* m, const float pose[6], const float* corner, int32_t n_corner,
+                              const float* surf, int32_t n_surf, const float* outlier, int32_t n_outlier,
+                              void* hip_stream);
+int32_t llsr_map_num_keyframes(const llsr_map* m);
+typedef struct llsr_map_report {
+  int32_t n_in_radius;     /* key poses within surrounding_radius (MO:1157-1164) */
+  int32_t n_poses_ds;      /* surroundingKeyPosesDS size (MO:1166-1167) */
+  int32_t n_keyframes;     /* surroundingExistingKeyPosesID size after the update */
+  int32_t n_transformed;   /* keyframes newly added to the list this call (MO:1205-1220) */
+  int64_t n_corner_map;    /* laserCloudCornerFromMap before / after VoxelGrid */
+  int64_t n_surf_map;      /* laserCloudSurfFromMap (surf + outlier keyframe clouds) */
+  int64_t n_corner_ds;
+  int64_t n_surf_ds;
+  float ms;                /* wall time of the call */
+} llsr_map_report;
+/* extractSurroundingKeyFrames (MO:1096-1232) around robot_pos (currentRobotPosPoint = x, y, z of
+ * transformAftMapped): the corner / surf local maps (…FromMapDS) into d_corner / d_surf (device,
+ * capacities in points; LLSR_ERANGE with the sizes in rep when they do not fit). Synchronises. */
+int32_t llsr_map_extract(llsr_map* m, const float robot_pos[3], float* d_corner, int64_t cap_corner, float* d_surf,
+                         int64_t cap_surf, llsr_map_report* rep, void* hip_stream);
+/* surroundingExistingKeyPosesID after the last extract; returns its length. */
+int32_t llsr_map_keyframe_ids(const llsr_map* m, int32_t* out, int32_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,629 @@
+// llsr_map.hip — MapOptimization's local map on the device: the keyframe store
+// (saveKeyFramesAndFactor, mapOptmization.cpp:1686-1752), extractSurroundingKeyFrames with loop
+// closure disabled (MO:1151-1231), downsampleCurrentScan (MO:1234-1267), and the segmented
+// VoxelGrid they all run on.
+//
+// VoxelGrid (pcl::VoxelGrid<PointXYZI>::applyFilter, PCL 1.10, downsample_all_data) of S clouds at
+// once, every step a device pass over HBM:
+//   k_vg_minmax    per-chunk min / max of x, y, z, folded into the cloud's bounds with order-
+//                  preserving uint atomics (min / max are order independent, so exact);
+//   k_vg_params    per cloud: the (max - min) * inv + 1 product check (over INT32_MAX: PCL returns
+//                  the input unchanged — here every point becomes its own voxel, idx = its index,
+//                  which reproduces that bit for bit), min_b = floor(min * inv), the div products;
+//   k_vg_keys      64-bit key (cloud << 32 | idx), value = index in the cloud;
+//   radix sort     hipcub::DeviceRadixSort (rocPRIM onesweep; stable, so a voxel's points stay in
+//                  input order); bits = 32 + ceil(log2 S);
+//   k_vg_heads     run heads, exclusive scan -> output slot of every voxel (ascending idx per
+//                  cloud, the PCL output order; the per-cloud output offsets fall out of the scan);
+//   k_vg_centroid  one lane per voxel sums its run in float (x, y, z, intensity) and divides by
+//                  the run length, as PCL does for its sorted run.
+// Host work per call is bookkeeping (block tables, the key-pose radius test over K poses, the
+// surroundingExistingKeyPosesID list); every point of every cloud is touched only on the device.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cfloat>
+#include <chrono>
+#include <cstdint>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/llsr.h"
+#include "llsr_libm.h"
+
+namespace {
+
+using llsr_libm::cosf_;
+using llsr_libm::sinf_;
+
+struct VgSeg {            // one cloud of a VoxelGrid call
+  const float4* src;
+  long long n;
+  float inv;              // 1.0f / leaf (PCL: inverse_leaf_size_ = 1 / leaf_size_, float)
+  int pad;
+};
+struct VgPar {            // per-cloud PCL parameters
+  int minb[3];
+  unsigned mul1, mul2;
+  int pass;               // product check failed: input returned unchanged
+};
+struct Chunk {            // a block's share: points [b, e) of cloud seg
+  int seg, pad;
+  long long b, e;
+};
+constexpr int kChunk = 4096;  // points per block in the chunked passes (256 lanes x 16)
+
+__device__ __forceinline__ unsigned ord(float f) {
+  const unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unord(unsigned o) {
+  return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+
+__global__ void k_vg_init(unsigned* mm, int S) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  for (int a = 0; a < 3; ++a) {
+    mm[6 * s + a] = 0xffffffffu;
+    mm[6 * s + 3 + a] = 0u;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_vg_minmax(const Chunk* ch, const VgSeg* segs, unsigned* mm) {
+  const Chunk c = ch[blockIdx.x];
+  const float4* p = segs[c.seg].src;
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (long long i = c.b + threadIdx.x; i < c.e; i += blockDim.x) {
+    const float4 q = p[i];
+    mn[0] = fminf(mn[0], q.x); mx[0] = fmaxf(mx[0], q.x);
+    mn[1] = fminf(mn[1], q.y); mx[1] = fmaxf(mx[1], q.y);
+    mn[2] = fminf(mn[2], q.z); mx[2] = fmaxf(mx[2], q.z);
+  }
+  for (int o = 32; o > 0; o >>= 1)
+    for (int a = 0; a < 3; ++a) {
+      mn[a] = fminf(mn[a], __shfl_xor(mn[a], o));
+      mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], o));
+    }
+  __shared__ float red[4][6];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+    for (int a = 0; a < 3; ++a) { red[w][a] = mn[a]; red[w][3 + a] = mx[a]; }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int a = threadIdx.x;
+    float v = red[0][a];
+    for (int k = 1; k < 4; ++k) v = a < 3 ? fminf(v, red[k][a]) : fmaxf(v, red[k][a]);
+    if (a < 3) atomicMin(&mm[6 * c.seg + a], ord(v));
+    else atomicMax(&mm[6 * c.seg + a], ord(v));
+  }
+}
+
+__global__ void k_vg_params(const VgSeg* segs, const unsigned* mm, VgPar* par, int S) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  VgPar q{};
+  if (segs[s].n > 0) {
+    const float inv = segs[s].inv;
+    float mn[3], mx[3];
+    for (int a = 0; a < 3; ++a) { mn[a] = unord(mm[6 * s + a]); mx[a] = unord(mm[6 * s + 3 + a]); }
+    // PCL: int64(float) + 1 per axis, product > INT32_MAX. Truncated in double (exact for these
+    // magnitudes; an f32 -> i64 conversion here crashes the gfx950 instruction selector), and the
+    // product in double is exact wherever it is near the INT32_MAX threshold.
+    const float ex = (mx[0] - mn[0]) * inv, ey = (mx[1] - mn[1]) * inv, ez = (mx[2] - mn[2]) * inv;
+    const double dx = trunc((double)ex) + 1, dy = trunc((double)ey) + 1, dz = trunc((double)ez) + 1;
+    q.pass = dx * dy * dz > 2147483647.0;
+    int div[3];
+    for (int a = 0; a < 3; ++a) {
+      q.minb[a] = (int)floorf(mn[a] * inv);
+      div[a] = (int)floorf(mx[a] * inv) - q.minb[a] + 1;
+    }
+    q.mul1 = (unsigned)div[0];
+    q.mul2 = (unsigned)div[0] * (unsigned)div[1];
+  }
+  par[s] = q;
+}
+
+__global__ __launch_bounds__(256) void k_vg_keys(const Chunk* ch, const VgSeg* segs, const VgPar* par,
+                                                 const long long* base, unsigned long long* key, int* val) {
+  const Chunk c = ch[blockIdx.x];
+  const float4* p = segs[c.seg].src;
+  const float inv = segs[c.seg].inv;
+  const VgPar q = par[c.seg];
+  const long long o = base[c.seg];
+  for (long long i = c.b + threadIdx.x; i < c.e; i += blockDim.x) {
+    unsigned idx;
+    if (q.pass) {
+      idx = (unsigned)i;
+    } else {
+      const float4 v = p[i];
+      const int i0 = (int)(floorf(v.x * inv) - (float)q.minb[0]);
+      const int i1 = (int)(floorf(v.y * inv) - (float)q.minb[1]);
+      const int i2 = (int)(floorf(v.z * inv) - (float)q.minb[2]);
+      idx = (unsigned)i0 + (unsigned)i1 * q.mul1 + (unsigned)i2 * q.mul2;
+    }
+    key[o + i] = ((unsigned long long)c.seg << 32) | idx;
+    val[o + i] = (int)i;
+  }
+}
+
+__global__ void k_vg_heads(const unsigned long long* key, int* flag, long long N) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  flag[i] = (i == 0 || key[i] != key[i - 1]) ? 1 : 0;
+}
+
+__global__ void k_vg_centroid(const unsigned long long* key, const int* val, const int* flag, const int* rank,
+                              const VgSeg* segs, float4* out, long long N) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N || !flag[i]) return;
+  const unsigned long long k = key[i];
+  const float4* p = segs[(int)(k >> 32)].src;
+  float sx = 0, sy = 0, sz = 0, si = 0;
+  long long j = i;
+  do {
+    const float4 v = p[val[j]];
+    sx += v.x; sy += v.y; sz += v.z; si += v.w;
+    ++j;
+  } while (j < N && key[j] == k);
+  const float n = (float)(j - i);
+  out[rank[i]] = make_float4(sx / n, sy / n, sz / n, si / n);
+}
+
+// out_off[s] = output slot of cloud s's first voxel (= rank at its first sorted position, which
+// for an empty cloud is the next cloud's first slot); out_off[S] = voxel total.
+__global__ void k_vg_offsets(const long long* base, const int* flag, const int* rank, long long N, int S,
+                             long long* out_off) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > S) return;
+  const long long total = N > 0 ? (long long)rank[N - 1] + flag[N - 1] : 0;
+  const long long b = base[s];
+  out_off[s] = b < N ? (long long)rank[b] : total;
+}
+
+// transformPointCloud(cloudIn, transformIn) (MO:671-701) of one keyframe chunk per block.
+struct XfChunk {
+  long long src, dst;  // store / map offsets (points)
+  int n, pad;
+  float t[6];          // x, y, z, roll, pitch, yaw
+};
+
+__global__ __launch_bounds__(256) void k_map_transform(const XfChunk* ch, const float4* store, float4* map) {
+  const XfChunk c = ch[blockIdx.x];
+  const float tx = c.t[0], ty = c.t[1], tz = c.t[2], roll = c.t[3], pitch = c.t[4], yaw = c.t[5];
+  const float cy = cosf_(yaw), sy = sinf_(yaw), cr = cosf_(roll), sr = sinf_(roll), cp = cosf_(pitch),
+              sp = sinf_(pitch);
+  for (int k = threadIdx.x; k < c.n; k += blockDim.x) {
+    const float4 q = store[c.src + k];
+    const float x1 = cy * q.x - sy * q.y;
+    const float y1 = sy * q.x + cy * q.y;
+    const float z1 = q.z;
+    const float x2 = x1;
+    const float y2 = cr * y1 - sr * z1;
+    const float z2 = sr * y1 + cr * z1;
+    map[c.dst + k] = make_float4(cp * x2 + sp * z2 + tx, y2 + ty, -sp * x2 + cp * z2 + tz, q.w);
+  }
+}
+
+template <class T>
+hipError_t grow(T*& p, size_t& cap, size_t need) {
+  if (need <= cap) return hipSuccess;
+  size_t n = cap ? cap : 1024;
+  while (n < need) n += n / 2 + 1;
+  if (p) {
+    hipError_t e = hipFree(p);
+    if (e != hipSuccess) return e;
+    p = nullptr;
+  }
+  cap = 0;
+  hipError_t e = hipMalloc(&p, n * sizeof(T));
+  if (e == hipSuccess) cap = n;
+  return e;
+}
+
+int ceil_log2(int s) {
+  int b = 0;
+  while ((1 << b) < s) ++b;
+  return b;
+}
+
+}  // namespace
+
+struct llsr_map {
+  llsr_map_config cfg{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  // keyframe store: packed points, host-side index
+  float4* store = nullptr;
+  size_t store_cap = 0, store_used = 0;
+  struct Kf { float pose[6]; long long off[3]; int n[3]; };  // corner, surf, outlier
+  std::vector<Kf> kf;
+  std::vector<int> existing;   // surroundingExistingKeyPosesID
+  // VoxelGrid scratch
+  unsigned long long *key = nullptr, *key2 = nullptr;
+  int *val = nullptr, *val2 = nullptr, *flag = nullptr, *rank = nullptr;
+  size_t cap_key = 0, cap_key2 = 0, cap_val = 0, cap_val2 = 0, cap_flag = 0, cap_rank = 0;
+  void* tmp = nullptr;
+  size_t cap_tmp = 0;
+  unsigned* mm = nullptr;
+  size_t cap_mm = 0;
+  VgPar* par = nullptr;
+  size_t cap_par = 0;
+  char* dtab = nullptr;        // device tables (segments, chunks, bases, out offsets)
+  size_t cap_dtab = 0;
+  char* htab = nullptr;        // pinned host staging of the same
+  size_t cap_htab = 0;
+  // local-map assembly
+  float4* mapbuf = nullptr;    // [corner map | surf map]
+  size_t cap_map = 0;
+  float4* dsbuf = nullptr;     // VoxelGrid output staging
+  size_t cap_ds = 0;
+  float4* poses = nullptr;     // selected key poses (x, y, z, index)
+  size_t cap_poses = 0;
+  char* hstage = nullptr;      // pinned staging of the extract's own uploads (poses, chunk table)
+  size_t cap_hstage = 0;
+  char* dxf = nullptr;         // device chunk table of k_map_transform
+  size_t cap_dxf = 0;
+};
+
+static int32_t mfail(llsr_map* m, int32_t code, const std::string& msg) {
+  if (m) m->err = msg;
+  return code;
+}
+
+#define MAP_OK(m, expr)                                                          \
+  do {                                                                           \
+    hipError_t e_ = (expr);                                                      \
+    if (e_ != hipSuccess)                                                        \
+      return mfail(m, LLSR_EIO, std::string(#expr ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+namespace {
+
+struct VgCloud {
+  const float4* src;
+  long long n;
+  float leaf;
+};
+
+hipError_t host_grow(char*& p, size_t& cap, size_t need) {
+  if (need <= cap) return hipSuccess;
+  size_t n = cap ? cap : 4096;
+  while (n < need) n *= 2;
+  if (p) {
+    hipError_t e = hipHostFree(p);
+    if (e != hipSuccess) return e;
+    p = nullptr;
+  }
+  cap = 0;
+  hipError_t e = hipHostMalloc(&p, n);
+  if (e == hipSuccess) cap = n;
+  return e;
+}
+
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// The segmented VoxelGrid: clouds -> d_out packed (capacity sum n), out_off[S+1] on the host.
+int32_t vg_run(llsr_map* m, const std::vector<VgCloud>& cl, float4* d_out, long long* out_off, hipStream_t s) {
+  const int S = (int)cl.size();
+  long long N = 0;
+  std::vector<long long> base(S + 1);
+  for (int k = 0; k < S; ++k) {
+    if (cl[k].n < 0 || !(cl[k].leaf > 0)) return mfail(m, LLSR_EINVAL, "voxel grid: bad cloud size or leaf");
+    base[k] = N;
+    N += cl[k].n;
+  }
+  base[S] = N;
+  if (N >= (long long)INT32_MAX) return mfail(m, LLSR_ERANGE, "voxel grid: more than 2^31 points");
+  if (N == 0) {
+    for (int k = 0; k <= S; ++k) out_off[k] = 0;
+    return LLSR_OK;
+  }
+  // host tables: segments, chunks, bases
+  std::vector<Chunk> ch;
+  for (int k = 0; k < S; ++k)
+    for (long long b = 0; b < cl[k].n; b += kChunk) ch.push_back({k, 0, b, std::min(cl[k].n, b + kChunk)});
+  const size_t o_seg = 0, o_ch = align256(S * sizeof(VgSeg)), o_base = o_ch + align256(ch.size() * sizeof(Chunk)),
+               o_out = o_base + align256((S + 1) * sizeof(long long)),
+               bytes = o_out + align256((S + 1) * sizeof(long long));
+  MAP_OK(m, host_grow(m->htab, m->cap_htab, bytes));
+  MAP_OK(m, grow(m->dtab, m->cap_dtab, bytes));
+  VgSeg* hs = reinterpret_cast<VgSeg*>(m->htab + o_seg);
+  for (int k = 0; k < S; ++k) hs[k] = {cl[k].src, cl[k].n, 1.0f / cl[k].leaf, 0};
+  std::memcpy(m->htab + o_ch, ch.data(), ch.size() * sizeof(Chunk));
+  std::memcpy(m->htab + o_base, base.data(), (S + 1) * sizeof(long long));
+  MAP_OK(m, hipMemcpyAsync(m->dtab, m->htab, o_out, hipMemcpyHostToDevice, s));
+  const VgSeg* dseg = reinterpret_cast<const VgSeg*>(m->dtab + o_seg);
+  const Chunk* dch = reinterpret_cast<const Chunk*>(m->dtab + o_ch);
+  const long long* dbase = reinterpret_cast<const long long*>(m->dtab + o_base);
+  long long* doff = reinterpret_cast<long long*>(m->dtab + o_out);
+  // scratch
+  MAP_OK(m, grow(m->key, m->cap_key, N));
+  MAP_OK(m, grow(m->key2, m->cap_key2, N));
+  MAP_OK(m, grow(m->val, m->cap_val, N));
+  MAP_OK(m, grow(m->val2, m->cap_val2, N));
+  MAP_OK(m, grow(m->flag, m->cap_flag, N));
+  MAP_OK(m, grow(m->rank, m->cap_rank, N));
+  MAP_OK(m, grow(m->mm, m->cap_mm, 6 * (size_t)S));
+  MAP_OK(m, grow(m->par, m->cap_par, (size_t)S));
+  const int end_bit = 32 + ceil_log2(S);
+  size_t tb_sort = 0, tb_scan = 0;
+  MAP_OK(m, hipcub::DeviceRadixSort::SortPairs(nullptr, tb_sort, m->key, m->key2, m->val, m->val2, (int)N, 0,
+                                                end_bit, s));
+  MAP_OK(m, hipcub::DeviceScan::ExclusiveSum(nullptr, tb_scan, m->flag, m->rank, (int)N, s));
+  MAP_OK(m, grow(reinterpret_cast<char*&>(m->tmp), m->cap_tmp, std::max(tb_sort, tb_scan)));
+  const int nch = (int)ch.size();
+  k_vg_init<<<(S + 63) / 64, 64, 0, s>>>(m->mm, S);
+  k_vg_minmax<<<nch, 256, 0, s>>>(dch, dseg, m->mm);
+  k_vg_params<<<(S + 63) / 64, 64, 0, s>>>(dseg, m->mm, m->par, S);
+  k_vg_keys<<<nch, 256, 0, s>>>(dch, dseg, m->par, dbase, m->key, m->val);
+  MAP_OK(m, hipGetLastError());
+  size_t tb = m->cap_tmp;
+  MAP_OK(m, hipcub::DeviceRadixSort::SortPairs(m->tmp, tb, m->key, m->key2, m->val, m->val2, (int)N, 0, end_bit,
+                                                s));
+  const int nb = (int)((N + 255) / 256);
+  k_vg_heads<<<nb, 256, 0, s>>>(m->key2, m->flag, N);
+  tb = m->cap_tmp;
+  MAP_OK(m, hipcub::DeviceScan::ExclusiveSum(m->tmp, tb, m->flag, m->rank, (int)N, s));
+  k_vg_centroid<<<nb, 256, 0, s>>>(m->key2, m->val2, m->flag, m->rank, dseg, d_out, N);
+  k_vg_offsets<<<(S + 64) / 64, 64, 0, s>>>(dbase, m->flag, m->rank, N, S, doff);
+  MAP_OK(m, hipGetLastError());
+  long long* hoff = reinterpret_cast<long long*>(m->htab + o_out);
+  MAP_OK(m, hipMemcpyAsync(hoff, doff, (S + 1) * sizeof(long long), hipMemcpyDeviceToHost, s));
+  MAP_OK(m, hipStreamSynchronize(s));
+  std::memcpy(out_off, hoff, (S + 1) * sizeof(long long));
+  return LLSR_OK;
+}
+
+hipStream_t pick(llsr_map* m, void* s) { return s ? static_cast<hipStream_t>(s) : m->stream; }
+
+}  // namespace
+
+extern "C" int32_t llsr_map_config_default(llsr_map_config* c) {
+  if (!c) return LLSR_EINVAL;
+  c->surrounding_radius = 50.0f;
+  c->keypose_leaf = 1.0f;
+  c->corner_leaf = 0.2f;
+  c->surf_leaf = 0.4f;
+  c->outlier_leaf = 0.4f;
+  return LLSR_OK;
+}
+
+extern "C" llsr_map* llsr_map_create(const llsr_map_config* cfg, int32_t dev) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || dev < 0 || dev >= n) return nullptr;
+  llsr_map* m = new (std::nothrow) llsr_map();
+  if (!m) return nullptr;
+  if (cfg) m->cfg = *cfg;
+  else llsr_map_config_default(&m->cfg);
+  m->device = dev;
+  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete m;
+    return nullptr;
+  }
+  return m;
+}
+
+extern "C" void llsr_map_destroy(llsr_map* m) {
+  if (!m) return;
+  (void)hipSetDevice(m->device);
+  (void)hipStreamSynchronize(m->stream);
+  void* dev[] = {m->store, m->key, m->key2, m->val, m->val2, m->flag, m->rank, m->tmp, m->mm, m->par, m->dtab,
+                 m->mapbuf, m->dsbuf, m->poses, m->dxf};
+  for (void* p : dev)
+    if (p) (void)hipFree(p);
+  if (m->htab) (void)hipHostFree(m->htab);
+  if (m->hstage) (void)hipHostFree(m->hstage);
+  (void)hipStreamDestroy(m->stream);
+  delete m;
+}
+
+extern "C" const char* llsr_map_last_error(const llsr_map* m) { return m ? m->err.c_str() : "null map"; }
+
+extern "C" int32_t llsr_map_reset(llsr_map* m) {
+  if (!m) return LLSR_EINVAL;
+  m->kf.clear();
+  m->existing.clear();
+  m->store_used = 0;
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_map_num_keyframes(const llsr_map* m) { return m ? (int32_t)m->kf.size() : LLSR_EINVAL; }
+
+extern "C" int32_t llsr_map_voxel_grid(llsr_map* m, const float* d_in, const int64_t* off, int32_t S,
+                                       const float* leaf, float* d_out, int64_t* out_off, void* hip_stream) {
+  if (!m || !off || !leaf || !out_off || S < 1) return mfail(m, LLSR_EINVAL, "voxel_grid: bad arguments");
+  if (off[S] > 0 && (!d_in || !d_out)) return mfail(m, LLSR_EINVAL, "voxel_grid: null cloud");
+  MAP_OK(m, hipSetDevice(m->device));
+  std::vector<VgCloud> cl(S);
+  for (int k = 0; k < S; ++k) {
+    if (off[k + 1] < off[k]) return mfail(m, LLSR_EINVAL, "voxel_grid: offsets must be non-decreasing");
+    cl[k] = {reinterpret_cast<const float4*>(d_in) + off[k], off[k + 1] - off[k], leaf[k]};
+  }
+  std::vector<long long> o(S + 1);
+  const int32_t rc = vg_run(m, cl, reinterpret_cast<float4*>(d_out), o.data(), pick(m, hip_stream));
+  if (rc != LLSR_OK) return rc;
+  for (int k = 0; k <= S; ++k) out_off[k] = o[k];
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_map_downsample_scan(llsr_map* m, const float* cl, int32_t ncl, const float* sl, int32_t nsl,
+                                            const float* ol, int32_t nol, const float* cs, int32_t ncs,
+                                            const float* ss, int32_t nss, float* d_out, int64_t* out_off,
+                                            void* hip_stream) {
+  if (!m || !d_out || !out_off || ncl < 0 || nsl < 0 || nol < 0 || ncs < 0 || nss < 0)
+    return mfail(m, LLSR_EINVAL, "downsample_scan: bad arguments");
+  MAP_OK(m, hipSetDevice(m->device));
+  const hipStream_t s = pick(m, hip_stream);
+  auto f4 = [](const float* p) { return reinterpret_cast<const float4*>(p); };
+  const std::vector<VgCloud> five = {{f4(cl), ncl, m->cfg.corner_leaf},  {f4(sl), nsl, m->cfg.surf_leaf},
+                                     {f4(ol), nol, m->cfg.outlier_leaf}, {f4(cs), ncs, m->cfg.corner_leaf},
+                                     {f4(ss), nss, m->cfg.surf_leaf}};
+  float4* out = reinterpret_cast<float4*>(d_out);
+  long long o[6];
+  int32_t rc = vg_run(m, five, out, o, s);
+  if (rc != LLSR_OK) return rc;
+  // laserCloudSurfTotalLast = SurfLastDS + OutlierLastDS, contiguous at [o[1], o[3]) (MO:1261-1266)
+  const std::vector<VgCloud> total = {{out + o[1], o[3] - o[1], m->cfg.surf_leaf}};
+  long long t[2];
+  rc = vg_run(m, total, out + o[5], t, s);
+  if (rc != LLSR_OK) return rc;
+  for (int k = 0; k < 6; ++k) out_off[k] = o[k];
+  out_off[6] = o[5] + t[1];
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_map_add_keyframe(llsr_map* m, const float pose[6], const float* c, int32_t nc,
+                                         const float* su, int32_t ns, const float* o, int32_t no, void* hip_stream) {
+  if (!m || !pose || nc < 0 || ns < 0 || no < 0 || (nc && !c) || (ns && !su) || (no && !o))
+    return mfail(m, LLSR_EINVAL, "add_keyframe: bad arguments");
+  MAP_OK(m, hipSetDevice(m->device));
+  const hipStream_t s = pick(m, hip_stream);
+  const size_t need = m->store_used + (size_t)nc + ns + no;
+  if (need > m->store_cap) {
+    size_t n = m->store_cap ? m->store_cap : (size_t)1 << 20;
+    while (n < need) n *= 2;
+    float4* p = nullptr;
+    MAP_OK(m, hipMalloc(&p, n * sizeof(float4)));
+    if (m->store_used) MAP_OK(m, hipMemcpyAsync(p, m->store, m->store_used * sizeof(float4), hipMemcpyDeviceToDevice, s));
+    MAP_OK(m, hipStreamSynchronize(s));
+    if (m->store) MAP_OK(m, hipFree(m->store));
+    m->store = p;
+    m->store_cap = n;
+  }
+  llsr_map::Kf k{};
+  std::memcpy(k.pose, pose, sizeof k.pose);
+  const float* src[3] = {c, su, o};
+  const int cnt[3] = {nc, ns, no};
+  for (int a = 0; a < 3; ++a) {
+    k.off[a] = (long long)m->store_used;
+    k.n[a] = cnt[a];
+    if (cnt[a])
+      MAP_OK(m, hipMemcpyAsync(m->store + m->store_used, src[a], cnt[a] * sizeof(float4), hipMemcpyDefault, s));
+    m->store_used += cnt[a];
+  }
+  m->kf.push_back(k);
+  return (int32_t)m->kf.size() - 1;
+}
+
+extern "C" int32_t llsr_map_extract(llsr_map* m, const float pos[3], float* d_corner, int64_t cap_c, float* d_surf,
+                                    int64_t cap_s, llsr_map_report* rep, void* hip_stream) {
+  if (!m || !pos || !rep) return mfail(m, LLSR_EINVAL, "extract: bad arguments");
+  const auto t0 = std::chrono::steady_clock::now();
+  std::memset(rep, 0, sizeof *rep);
+  MAP_OK(m, hipSetDevice(m->device));
+  const hipStream_t s = pick(m, hip_stream);
+  const int K = (int)m->kf.size();
+  if (K == 0) return LLSR_OK;  // MO:1097
+  // radiusSearch (MO:1157-1159): d^2 = ((0 + dx^2) + dy^2) + dz^2 < float(r^2), over K poses
+  const float r2 = (float)((double)m->cfg.surrounding_radius * (double)m->cfg.surrounding_radius);
+  std::vector<float4> sel;
+  for (int k = 0; k < K; ++k) {
+    const float* p = m->kf[k].pose;
+    float d = 0;
+    for (int a = 0; a < 3; ++a) {
+      const float df = pos[a] - p[a];
+      d += df * df;
+    }
+    if (d < r2) sel.push_back(make_float4(p[0], p[1], p[2], (float)k));
+  }
+  rep->n_in_radius = (int32_t)sel.size();
+  // surroundingKeyPosesDS (MO:1166-1167) on the device; intensity = the mean keyframe index
+  std::vector<int> ds_ids;
+  if (!sel.empty()) {
+    MAP_OK(m, grow(m->poses, m->cap_poses, 2 * sel.size()));
+    MAP_OK(m, host_grow(m->hstage, m->cap_hstage, sel.size() * sizeof(float4)));
+    std::memcpy(m->hstage, sel.data(), sel.size() * sizeof(float4));
+    MAP_OK(m, hipMemcpyAsync(m->poses, m->hstage, sel.size() * sizeof(float4), hipMemcpyHostToDevice, s));
+    long long po[2];
+    int32_t rc = vg_run(m, {{m->poses, (long long)sel.size(), m->cfg.keypose_leaf}}, m->poses + sel.size(), po, s);
+    if (rc != LLSR_OK) return rc;
+    std::vector<float4> ds(po[1]);
+    MAP_OK(m, hipMemcpyAsync(ds.data(), m->poses + sel.size(), po[1] * sizeof(float4), hipMemcpyDeviceToHost, s));
+    MAP_OK(m, hipStreamSynchronize(s));
+    for (const float4& q : ds) ds_ids.push_back((int)q.w);
+  }
+  rep->n_poses_ds = (int32_t)ds_ids.size();
+  // MO:1169-1189: drop listed keyframes no downsampled pose names; MO:1190-1222: append new ones
+  std::vector<int> kept;
+  for (int id : m->existing)
+    for (int d : ds_ids)
+      if (d == id) { kept.push_back(id); break; }
+  m->existing.swap(kept);
+  for (int d : ds_ids) {
+    bool found = false;
+    for (int id : m->existing)
+      if (id == d) { found = true; break; }
+    if (!found) {
+      if (d < 0 || d >= K) return mfail(m, LLSR_ERANGE, "extract: key pose index out of range");
+      m->existing.push_back(d);
+      ++rep->n_transformed;
+    }
+  }
+  rep->n_keyframes = (int32_t)m->existing.size();
+  // MO:1224-1228: corner map = corner clouds; surf map = surf + outlier clouds, in list order
+  std::vector<XfChunk> xc;
+  long long nc = 0, ns = 0;
+  for (int id : m->existing) nc += m->kf[id].n[0];
+  for (int id : m->existing) ns += m->kf[id].n[1] + m->kf[id].n[2];
+  long long dc = 0, dsf = nc;
+  auto add = [&](const llsr_map::Kf& k, int a, long long& dst) {
+    for (int b = 0; b < k.n[a]; b += 1024) {
+      XfChunk x{};
+      x.src = k.off[a] + b;
+      x.dst = dst + b;
+      x.n = std::min(1024, k.n[a] - b);
+      std::memcpy(x.t, k.pose, sizeof x.t);
+      xc.push_back(x);
+    }
+    dst += k.n[a];
+  };
+  for (int id : m->existing) {
+    add(m->kf[id], 0, dc);
+    add(m->kf[id], 1, dsf);
+    add(m->kf[id], 2, dsf);
+  }
+  rep->n_corner_map = nc;
+  rep->n_surf_map = ns;
+  MAP_OK(m, grow(m->mapbuf, m->cap_map, (size_t)(nc + ns)));
+  MAP_OK(m, grow(m->dsbuf, m->cap_ds, (size_t)(nc + ns)));
+  if (!xc.empty()) {
+    // hstage is free here: the key-pose VoxelGrid above ended with a stream sync
+    const size_t bytes = xc.size() * sizeof(XfChunk);
+    MAP_OK(m, host_grow(m->hstage, m->cap_hstage, bytes));
+    MAP_OK(m, grow(m->dxf, m->cap_dxf, bytes));
+    std::memcpy(m->hstage, xc.data(), bytes);
+    MAP_OK(m, hipMemcpyAsync(m->dxf, m->hstage, bytes, hipMemcpyHostToDevice, s));
+    k_map_transform<<<(int)xc.size(), 256, 0, s>>>(reinterpret_cast<const XfChunk*>(m->dxf), m->store, m->mapbuf);
+    MAP_OK(m, hipGetLastError());
+  }
+  // MO:1225-1231: VoxelGrid corner / surf
+  long long o[3];
+  const int32_t rc = vg_run(m, {{m->mapbuf, nc, m->cfg.corner_leaf}, {m->mapbuf + nc, ns, m->cfg.surf_leaf}},
+                            m->dsbuf, o, s);
+  if (rc != LLSR_OK) return rc;
+  rep->n_corner_ds = o[1] - o[0];
+  rep->n_surf_ds = o[2] - o[1];
+  if (rep->n_corner_ds > cap_c || rep->n_surf_ds > cap_s)
+    return mfail(m, LLSR_ERANGE, "extract: local map exceeds the output capacity");
+  if (rep->n_corner_ds && !d_corner) return mfail(m, LLSR_EINVAL, "extract: null corner output");
+  if (rep->n_surf_ds && !d_surf) return mfail(m, LLSR_EINVAL, "extract: null surf output");
+  if (rep->n_corner_ds)
+    MAP_OK(m, hipMemcpyAsync(d_corner, m->dsbuf, rep->n_corner_ds * sizeof(float4), hipMemcpyDeviceToDevice, s));
+  if (rep->n_surf_ds)
+    MAP_OK(m, hipMemcpyAsync(d_surf, m->dsbuf + o[1], rep->n_surf_ds * sizeof(float4), hipMemcpyDeviceToDevice, s));
+  MAP_OK(m, hipStreamSynchronize(s));
+  rep->ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_map_keyframe_ids(const llsr_map* m, int32_t* out, int32_t cap) {
+  if (!m) return LLSR_EINVAL;
+  const int n = (int)m->existing.size();
+  for (int k = 0; k < n && k < cap; ++k) out[k] = m->existing[k];
+  return n;
+}

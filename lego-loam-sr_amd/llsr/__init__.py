@@ -37,7 +37,9 @@ EXPORTS = [
     "llsr_shadow_points", "llsr_scan2scan_reserve", "llsr_scan2scan_batch", "llsr_scan2scan_check",
     "llsr_scan2scan", "llsr_scan2map_shard_begin", "llsr_scan2map_shard_partial",
     "llsr_scan2map_shard_step", "llsr_scan2map_shard_end", "llsr_odometry_batch", "llsr_odometry_fetch",
-    "llsr_odometry_reset",
+    "llsr_odometry_reset", "llsr_map_config_default", "llsr_map_create", "llsr_map_destroy",
+    "llsr_map_last_error", "llsr_map_reset", "llsr_map_voxel_grid", "llsr_map_downsample_scan",
+    "llsr_map_add_keyframe", "llsr_map_num_keyframes", "llsr_map_extract", "llsr_map_keyframe_ids",
 ]
 
 
@@ -87,10 +89,27 @@ def lib():
         L.llsr_odometry_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
         L.llsr_odometry_fetch.argtypes = [C.c_void_p, C.c_int32, C.POINTER(_abi.OdomSlot)] + [C.c_void_p] * 4
         L.llsr_odometry_reset.argtypes = [C.c_void_p]
+        L.llsr_map_config_default.argtypes = [C.POINTER(_abi.MapConfig)]
+        L.llsr_map_create.argtypes = [C.POINTER(_abi.MapConfig), C.c_int32]
+        L.llsr_map_destroy.argtypes = [C.c_void_p]
+        L.llsr_map_last_error.argtypes = [C.c_void_p]
+        L.llsr_map_reset.argtypes = [C.c_void_p]
+        L.llsr_map_voxel_grid.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
+                                          C.c_void_p, C.c_void_p]
+        L.llsr_map_downsample_scan.argtypes = [C.c_void_p] + [C.c_void_p, C.c_int32] * 5 + [C.c_void_p] * 3
+        L.llsr_map_add_keyframe.argtypes = [C.c_void_p, C.c_void_p] + [C.c_void_p, C.c_int32] * 3 + [C.c_void_p]
+        L.llsr_map_num_keyframes.argtypes = [C.c_void_p]
+        L.llsr_map_extract.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,
+                                       C.POINTER(_abi.MapReport), C.c_void_p]
+        L.llsr_map_keyframe_ids.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         for fn in EXPORTS:
-            if fn not in ("llsr_last_error", "llsr_kernel_name", "llsr_destroy"):
+            if fn not in ("llsr_last_error", "llsr_kernel_name", "llsr_destroy", "llsr_map_create",
+                          "llsr_map_destroy", "llsr_map_last_error"):
                 getattr(L, fn).restype = C.c_int32
         L.llsr_destroy.restype = None
+        L.llsr_map_create.restype = C.c_void_p
+        L.llsr_map_destroy.restype = None
+        L.llsr_map_last_error.restype = C.c_char_p
         _LIB = L
     return _LIB
 
@@ -349,3 +368,134 @@ class ImageProjection:
             "segmentedCloud_Intensity": r["seg_intensity"].astype(np.float64),
             "_full": r,
         }
+
+
+def map_config(**kw) -> _abi.MapConfig:
+    c = _abi.MapConfig()
+    lib().llsr_map_config_default(C.byref(c))
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+class LocalMap:
+    """MapOptimization's keyframe store + local map on a HIP device (llsr_map, include/llsr.h):
+    saveKeyFramesAndFactor's clouds (MO:1686-1752), extractSurroundingKeyFrames (MO:1096-1232),
+    downsampleCurrentScan (MO:1234-1267) and the VoxelGrid filters they use.
+
+    Clouds are torch CUDA float32 tensors of shape (n, 4) (x, y, z, intensity); torch is only the
+    device allocator here. Calls run on a private stream ordered after the caller's current stream
+    and return once their results are ready (as the reference's calls do)."""
+
+    def __init__(self, device: int = 0, cfg: _abi.MapConfig | None = None):
+        import torch
+        self._torch = torch
+        self.cfg = cfg or map_config()
+        self.device = torch.device("cuda", device)
+        self._m = lib().llsr_map_create(C.byref(self.cfg), device)
+        if not self._m:
+            raise LlsrError("llsr_map_create failed: no HIP device")
+        self._s = torch.cuda.Stream(device=self.device)
+        self._n_corner = 0
+        self._n_surf = 0
+
+    def close(self):
+        if getattr(self, "_m", None):
+            lib().llsr_map_destroy(self._m)
+            self._m = None
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, rc, what):
+        if rc < 0:
+            raise LlsrError(f"{what} failed ({rc}): {lib().llsr_map_last_error(self._m).decode()}")
+        return rc
+
+    def _enter(self):
+        self._s.wait_stream(self._torch.cuda.current_stream(self.device))
+        return C.c_void_p(self._s.cuda_stream)
+
+    def _leave(self):
+        self._torch.cuda.current_stream(self.device).wait_stream(self._s)
+
+    def _cloud(self, a):
+        t = self._torch.as_tensor(a, dtype=self._torch.float32, device=self.device).reshape(-1, 4).contiguous()
+        return t
+
+    def reset(self):
+        self._check(lib().llsr_map_reset(self._m), "llsr_map_reset")
+        self._n_corner = self._n_surf = 0
+
+    def voxel_grid(self, clouds, leaves):
+        """pcl::VoxelGrid::filter of every cloud (list) with its leaf size; returns the filtered clouds."""
+        torch = self._torch
+        cl = [self._cloud(c) for c in clouds]
+        off = np.zeros(len(cl) + 1, np.int64)
+        off[1:] = np.cumsum([c.shape[0] for c in cl])
+        packed = torch.cat(cl) if off[-1] else torch.zeros((0, 4), dtype=torch.float32, device=self.device)
+        out = torch.empty((max(int(off[-1]), 1), 4), dtype=torch.float32, device=self.device)
+        out_off = np.zeros(len(cl) + 1, np.int64)
+        leaf = np.asarray(leaves, np.float32)
+        s = self._enter()
+        self._check(lib().llsr_map_voxel_grid(self._m, C.c_void_p(packed.data_ptr()), off.ctypes.data, len(cl),
+                                              leaf.ctypes.data, C.c_void_p(out.data_ptr()), out_off.ctypes.data, s),
+                    "llsr_map_voxel_grid")
+        self._leave()
+        return [out[out_off[k]:out_off[k + 1]] for k in range(len(cl))]
+
+    def downsample_scan(self, corner_last, surf_last, outlier_last, corner_scan, surf_scan) -> dict:
+        """downsampleCurrentScan (MO:1234-1267): the six ...DS clouds."""
+        torch = self._torch
+        cl = [self._cloud(c) for c in (corner_last, surf_last, outlier_last, corner_scan, surf_scan)]
+        n = [c.shape[0] for c in cl]
+        out = torch.empty((max(sum(n) + n[1] + n[2], 1), 4), dtype=torch.float32, device=self.device)
+        out_off = np.zeros(7, np.int64)
+        args = []
+        for c, k in zip(cl, n):
+            args += [C.c_void_p(c.data_ptr() if k else 0), k]
+        s = self._enter()
+        self._check(lib().llsr_map_downsample_scan(self._m, *args, C.c_void_p(out.data_ptr()), out_off.ctypes.data,
+                                                   s), "llsr_map_downsample_scan")
+        self._leave()
+        names = ("corner_last_ds", "surf_last_ds", "outlier_last_ds", "corner_scan_ds", "surf_scan_ds",
+                 "surf_total_last_ds")
+        return {nm: out[out_off[k]:out_off[k + 1]] for k, nm in enumerate(names)}
+
+    def add_keyframe(self, pose6, corner, surf, outlier) -> int:
+        """Store a keyframe: PointTypePose x, y, z, roll, pitch, yaw + its three clouds."""
+        pose = np.ascontiguousarray(pose6, np.float32)
+        cl = [self._cloud(c) for c in (corner, surf, outlier)]
+        args = []
+        for c in cl:
+            args += [C.c_void_p(c.data_ptr() if c.shape[0] else 0), c.shape[0]]
+        s = self._enter()
+        k = self._check(lib().llsr_map_add_keyframe(self._m, pose.ctypes.data, *args, s), "llsr_map_add_keyframe")
+        self._s.synchronize()  # the copies read the caller's tensors
+        self._n_corner += cl[0].shape[0]
+        self._n_surf += cl[1].shape[0] + cl[2].shape[0]
+        return k
+
+    @property
+    def num_keyframes(self) -> int:
+        return lib().llsr_map_num_keyframes(self._m)
+
+    def extract(self, robot_pos):
+        """extractSurroundingKeyFrames: (laserCloudCornerFromMapDS, laserCloudSurfFromMapDS, report)."""
+        torch = self._torch
+        pos = np.ascontiguousarray(robot_pos, np.float32)
+        cc, cs = max(self._n_corner, 1), max(self._n_surf, 1)
+        oc = torch.empty((cc, 4), dtype=torch.float32, device=self.device)
+        os_ = torch.empty((cs, 4), dtype=torch.float32, device=self.device)
+        rep = _abi.MapReport()
+        s = self._enter()
+        self._check(lib().llsr_map_extract(self._m, pos.ctypes.data, C.c_void_p(oc.data_ptr()), cc,
+                                           C.c_void_p(os_.data_ptr()), cs, C.byref(rep), s), "llsr_map_extract")
+        self._leave()
+        return oc[:rep.n_corner_ds], os_[:rep.n_surf_ds], rep.as_dict()
+
+    def keyframe_ids(self) -> np.ndarray:
+        n = lib().llsr_map_keyframe_ids(self._m, None, 0)
+        out = np.zeros(max(n, 1), np.int32)
+        lib().llsr_map_keyframe_ids(self._m, out.ctypes.data, n)
+        return out[:n]

@@ -202,6 +202,22 @@ class S2MStats(C.Structure):
                 ("iterate_ms", C.c_float)]
 
 
+class MapConfig(C.Structure):
+    """llsr_map_config (include/llsr.h): MapOptimization's local-map parameters."""
+    _fields_ = [("surrounding_radius", C.c_float), ("keypose_leaf", C.c_float), ("corner_leaf", C.c_float),
+                ("surf_leaf", C.c_float), ("outlier_leaf", C.c_float)]
+
+
+class MapReport(C.Structure):
+    """llsr_map_report (include/llsr.h): one extractSurroundingKeyFrames call."""
+    _fields_ = [("n_in_radius", C.c_int32), ("n_poses_ds", C.c_int32), ("n_keyframes", C.c_int32),
+                ("n_transformed", C.c_int32), ("n_corner_map", C.c_int64), ("n_surf_map", C.c_int64),
+                ("n_corner_ds", C.c_int64), ("n_surf_ds", C.c_int64), ("ms", C.c_float)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class Sizes(C.Structure):
     _fields_ = [("cells", C.c_int32), ("rings", C.c_int32), ("max_points", C.c_int32),
                 ("shadow_points", C.c_int32)]

@@ -156,3 +156,44 @@ def make_batch(n_scans: int, lidar: str = VLP16, distinct: int | None = None, se
     offsets = np.zeros(n_scans + 1, dtype=np.int64)
     offsets[1:] = np.cumsum([s.shape[0] for s in scans])
     return np.concatenate(scans, axis=0), offsets
+
+
+def make_keyframes(n: int, seed: int = 7, corner: int = 400, surf: int = 1600, outlier: int = 250):
+    """Synthetic MapOptimization keyframes: PointTypePose (x, y, z, roll, pitch, yaw) along a path
+    that runs out ~90 m and back with uneven spacing (several poses share a 1 m key-pose voxel on the
+    slow stretches, so the VoxelGrid of key poses averages indices), and per-keyframe corner / surf /
+    outlier clouds in the keyframe's own frame (structure-like: points on a few planes and poles, so
+    the 0.2 / 0.4 m VoxelGrids merge points within and across keyframes)."""
+    rng = np.random.default_rng(seed)
+    step = np.where(rng.random(n) < 0.3, 0.35, 2.8).astype(np.float32)
+    half = n // 2
+    s = np.concatenate([np.cumsum(step[:half]), np.cumsum(step[:half])[::-1][: n - half] - 0.7])
+    poses = np.zeros((n, 6), np.float32)
+    poses[:, 0] = s                                   # x (LOAM frame)
+    poses[:, 1] = 0.05 * np.sin(s / 7.0)               # y
+    poses[:, 2] = 3.0 * np.sin(s / 23.0)               # z
+    poses[:, 3] = 0.01 * np.sin(s / 5.0)               # roll
+    poses[:, 4] = 0.2 * np.sin(s / 31.0)               # pitch (heading in the camera-style frame)
+    poses[:, 5] = 0.02 * np.cos(s / 11.0)              # yaw
+    frames = []
+    for k in range(n):
+        def cloud(m, kind):
+            pts = np.empty((m, 4), np.float32)
+            u = rng.random((m, 3)).astype(np.float32)
+            if kind == "pole":                        # vertical poles at fixed world-ish spots
+                cx = np.floor(u[:, 0] * 8) * 5.0 - 20.0
+                pts[:, 0] = cx + 0.05 * u[:, 1]
+                pts[:, 1] = u[:, 2] * 4.0 - 1.5
+                pts[:, 2] = np.floor(u[:, 1] * 6) * 4.0 - 12.0
+            elif kind == "plane":                     # ground + walls
+                w = np.floor(u[:, 0] * 3)
+                pts[:, 0] = np.where(w == 0, u[:, 1] * 60 - 30, np.where(w == 1, -10.0, 12.0))
+                pts[:, 1] = np.where(w == 0, -1.6, u[:, 2] * 5 - 1.6)
+                pts[:, 2] = np.where(w == 0, u[:, 2] * 60 - 30, u[:, 1] * 60 - 30)
+            else:                                     # scattered
+                pts[:, :3] = (u - 0.5) * np.array([80, 20, 80], np.float32)
+            pts[:, :3] += rng.normal(0, 0.02, (m, 3)).astype(np.float32)
+            pts[:, 3] = (np.floor(rng.random(m) * 16) + np.floor(rng.random(m) * 1800) / 1e4).astype(np.float32)
+            return pts
+        frames.append((poses[k].copy(), cloud(corner, "pole"), cloud(surf, "plane"), cloud(outlier, "scatter")))
+    return frames

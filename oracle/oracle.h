@@ -70,6 +70,23 @@ int32_t oracle_eig6(const float* A, float* evals, float* evecs);
 void oracle_qr_solve_5x3(const float* A, const float* b, float* x);
 void oracle_qr_solve_6x6(const float* A, const float* b, float* x);
 
+/* pcl::VoxelGrid<PointXYZI>::filter (oracle_voxel.h) of n float4 points; returns the centroid
+ * count written to `out` (capacity n float4), -1 on bad arguments. stable != 0 sums each voxel in
+ * input order (the device order) instead of the std::sort order. */
+int64_t oracle_voxel_grid(const float* in, int64_t n, float leaf, int32_t stable, float* out);
+/* Key poses (float4 x, y, z, intensity) with squared distance < float(radius^2) to pos, ascending
+ * index (MO:1155-1159). _ref exports ref_keypose_radius over the reference's nanoflann. */
+int32_t oracle_keypose_radius(const float* poses4, int32_t K, const float* pos, float radius, int32_t* out);
+/* MapOptimization keyframe store + extractSurroundingKeyFrames (oracle_map.cpp). */
+typedef struct oracle_map oracle_map;
+oracle_map* oracle_map_create(float radius, float keypose_leaf, float corner_leaf, float surf_leaf);
+void oracle_map_destroy(oracle_map* m);
+int32_t oracle_map_add_keyframe(oracle_map* m, const float* pose6, const float* corner, int32_t n_corner,
+                                const float* surf, int32_t n_surf, const float* outlier, int32_t n_outlier);
+int32_t oracle_map_extract(oracle_map* m, const float* pos, int32_t stable, float* corner_out, int64_t cap_corner,
+                           int64_t* n_corner, float* surf_out, int64_t cap_surf, int64_t* n_surf, int32_t* ids,
+                           int32_t cap_ids, int32_t* n_ids, int64_t* raw_counts);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,6 +7,7 @@
 // build with -O3 -ffp-contract=off like the reference's baseline x86-64 build (no FMA).
 // Unqualified float math resolves to the float overloads.
 #include "oracle.h"
+#include "oracle_voxel.h"
 
 #include <algorithm>
 #include <cfloat>
@@ -130,51 +131,12 @@ struct PlaneRansac {
   }
 };
 
-// ------------------------------------------------------------------------------------------
-// PCL 1.10 VoxelGrid<PointXYZI>::applyFilter, downsample_all_data_ = true (FA:1268-1270).
-// ------------------------------------------------------------------------------------------
+// PCL 1.10 VoxelGrid<PointXYZI>::applyFilter (FA:1268-1270), restated in oracle_voxel.h.
 void voxel_grid(const std::vector<P4>& in, float leaf, std::vector<P4>& out) {
-  out.clear();
-  if (in.empty()) return;
-  const float inv = 1.0f / leaf;
-  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-  for (const P4& p : in) {
-    const float v[3] = {p.x, p.y, p.z};
-    for (int a = 0; a < 3; ++a) { mn[a] = std::min(mn[a], v[a]); mx[a] = std::max(mx[a], v[a]); }
-  }
-  int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1, dy = (int64_t)((mx[1] - mn[1]) * inv) + 1,
-          dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
-  if (dx * dy * dz > (int64_t)INT32_MAX) { out = in; return; }
-  int minb[3], maxb[3], div[3];
-  for (int a = 0; a < 3; ++a) {
-    minb[a] = (int)std::floor(mn[a] * inv);
-    maxb[a] = (int)std::floor(mx[a] * inv);
-    div[a] = maxb[a] - minb[a] + 1;
-  }
-  const int mul1 = div[0], mul2 = div[0] * div[1];
-  struct Idx { unsigned idx; unsigned cloud; };
-  std::vector<Idx> iv;
-  iv.reserve(in.size());
-  for (size_t k = 0; k < in.size(); ++k) {
-    int i0 = (int)(std::floor(in[k].x * inv) - (float)minb[0]);
-    int i1 = (int)(std::floor(in[k].y * inv) - (float)minb[1]);
-    int i2 = (int)(std::floor(in[k].z * inv) - (float)minb[2]);
-    iv.push_back({(unsigned)(i0 + i1 * mul1 + i2 * mul2), (unsigned)k});
-  }
-  std::sort(iv.begin(), iv.end(), [](const Idx& a, const Idx& b) { return a.idx < b.idx; });
-  size_t k = 0;
-  while (k < iv.size()) {
-    size_t e = k + 1;
-    while (e < iv.size() && iv[e].idx == iv[k].idx) ++e;
-    float sx = 0, sy = 0, sz = 0, si = 0;
-    for (size_t q = k; q < e; ++q) {
-      const P4& p = in[iv[q].cloud];
-      sx += p.x; sy += p.y; sz += p.z; si += p.i;
-    }
-    const float n = (float)(e - k);
-    out.push_back({sx / n, sy / n, sz / n, si / n});
-    k = e;
-  }
+  std::vector<float> o;
+  oracle_voxel::voxel_grid(reinterpret_cast<const float*>(in.data()), in.size(), leaf, o);
+  out.resize(o.size() / 4);
+  std::memcpy(out.data(), o.data(), o.size() * sizeof(float));
 }
 
 }  // namespace

@@ -29,7 +29,8 @@ def lib():
     global _LIB
     if _LIB is None:
         path = os.path.join(_HERE, "_build", "liboracle.so")
-        srcs = [os.path.join(_HERE, f) for f in ("oracle_ipfa.cpp", "oracle_mo.cpp", "oracle_fa_lm.cpp")]
+        srcs = [os.path.join(_HERE, f) for f in ("oracle_ipfa.cpp", "oracle_mo.cpp", "oracle_fa_lm.cpp",
+                                                        "oracle_map.cpp", "oracle_voxel.h")]
         if not os.path.exists(path) or os.path.getmtime(path) < max(map(os.path.getmtime, srcs)):
             build()
         L = C.CDLL(path)
@@ -58,6 +59,19 @@ def lib():
         L.oracle_s2m_shard_step.restype = C.c_int32
         L.oracle_s2m_shard_step.argtypes = [C.c_void_p, C.c_void_p]
         L.oracle_s2m_shard_result.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(_abi.LmReport)]
+        L.oracle_voxel_grid.restype = C.c_int64
+        L.oracle_voxel_grid.argtypes = [C.c_void_p, C.c_int64, C.c_float, C.c_int32, C.c_void_p]
+        L.oracle_keypose_radius.restype = C.c_int32
+        L.oracle_keypose_radius.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_float, C.c_void_p]
+        L.oracle_map_create.restype = C.c_void_p
+        L.oracle_map_create.argtypes = [C.c_float] * 4
+        L.oracle_map_destroy.argtypes = [C.c_void_p]
+        L.oracle_map_add_keyframe.restype = C.c_int32
+        L.oracle_map_add_keyframe.argtypes = [C.c_void_p, C.c_void_p] + [C.c_void_p, C.c_int32] * 3
+        L.oracle_map_extract.restype = C.c_int32
+        L.oracle_map_extract.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p,
+                                         C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p,
+                                         C.c_void_p]
         _LIB = L
     return _LIB
 
@@ -375,3 +389,70 @@ class OracleOdometry:
         out.update(frames=self.frames, transform_cur=self.tcur.copy(), transform_sum=self.tsum.copy(),
                    corner_last=self.corner_last, surf_last=self.surf_last)
         return out
+
+
+def voxel_grid(xyzi, leaf: float, stable: bool = False) -> np.ndarray:
+    """pcl::VoxelGrid::filter (oracle_voxel.h); stable=True sums each voxel in input order."""
+    a = _f4(xyzi)
+    out = np.zeros((max(len(a), 1), 4), np.float32)
+    n = lib().oracle_voxel_grid(a.ctypes.data, len(a), leaf, int(stable), out.ctypes.data)
+    if n < 0:
+        raise ValueError("oracle_voxel_grid: bad arguments")
+    return out[:n].copy()
+
+
+def keypose_radius(poses4, pos, radius: float, knn: str = "brute") -> np.ndarray:
+    """Indices (ascending) of key poses with d^2 < float(radius^2); knn="kdtree" runs the reference's
+    nanoflann radiusSearch (oracle/_ref)."""
+    p = _f4(poses4)
+    q = np.ascontiguousarray(pos, np.float32)
+    out = np.zeros(max(len(p), 1), np.int32)
+    if knn == "kdtree":
+        L = ref_lib()
+        f = L.ref_keypose_radius
+        f.restype = C.c_int32
+        f.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_float, C.c_void_p]
+    else:
+        f = lib().oracle_keypose_radius
+    n = f(p.ctypes.data, len(p), q.ctypes.data, radius, out.ctypes.data)
+    return out[:n].copy()
+
+
+class OracleMap:
+    """MapOptimization keyframe store + extractSurroundingKeyFrames (oracle_map.cpp)."""
+
+    def __init__(self, radius=50.0, keypose_leaf=1.0, corner_leaf=0.2, surf_leaf=0.4, stable=False):
+        self._m = lib().oracle_map_create(radius, keypose_leaf, corner_leaf, surf_leaf)
+        self.stable = stable
+        self._nc = self._ns = 0
+
+    def __del__(self):
+        if getattr(self, "_m", None):
+            lib().oracle_map_destroy(self._m)
+            self._m = None
+
+    def add_keyframe(self, pose6, corner, surf, outlier) -> int:
+        pose = np.ascontiguousarray(pose6, np.float32)
+        cl = [_f4(c) for c in (corner, surf, outlier)]
+        args = []
+        for c in cl:
+            args += [c.ctypes.data, len(c)]
+        self._nc += len(cl[0])
+        self._ns += len(cl[1]) + len(cl[2])
+        return lib().oracle_map_add_keyframe(self._m, pose.ctypes.data, *args)
+
+    def extract(self, robot_pos):
+        pos = np.ascontiguousarray(robot_pos, np.float32)
+        oc = np.zeros((max(self._nc, 1), 4), np.float32)
+        os_ = np.zeros((max(self._ns, 1), 4), np.float32)
+        ids = np.zeros(4096, np.int32)
+        nc, ns, nid = C.c_int64(), C.c_int64(), C.c_int32()
+        raw = np.zeros(4, np.int64)
+        rc = lib().oracle_map_extract(self._m, pos.ctypes.data, int(self.stable), oc.ctypes.data, len(oc),
+                                      C.byref(nc), os_.ctypes.data, len(os_), C.byref(ns), ids.ctypes.data,
+                                      len(ids), C.byref(nid), raw.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"oracle_map_extract: {rc}")
+        rep = {"n_corner_map": int(raw[0]), "n_surf_map": int(raw[1]), "n_in_radius": int(raw[2]),
+               "n_poses_ds": int(raw[3]), "n_keyframes": nid.value}
+        return oc[:nc.value].copy(), os_[:ns.value].copy(), ids[:nid.value].copy(), rep

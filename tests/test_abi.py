@@ -64,3 +64,13 @@ def test_create_without_device_fails_loudly():
     assert rc == -19 and not h.value  # LLSR_ENODEV: no silent CPU fallback
     with pytest.raises(llsr.LlsrError):
         llsr.Pipeline(cfg)
+
+
+def test_map_create_fails_loudly_without_device():
+    """llsr_map_create returns NULL when no HIP device is visible (no CPU fallback)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a HIP device is visible")
+    assert not llsr.lib().llsr_map_create(None, 0)
+    with pytest.raises(llsr.LlsrError):
+        llsr.LocalMap(0)
