@@ -369,6 +369,78 @@ def odometry_leg(dev, lidar: str, B: int, seqs: int, frames: int, steps: int, wa
     return out
 
 
+def local_map_leg(dev, K: int, steps: int, warmup: int, dist, check: bool, cpu_seconds: float) -> dict:
+    """MapOptimization local map (llsr_map_extract, MO:1096-1232): a store of K synthetic keyframes
+    (VLP-16-sized clouds: 200 corner, 6000 surf, 1500 outlier points) along an out-and-back path;
+    one step = extractSurroundingKeyFrames at the next robot position (radius 50 m, key-pose
+    VoxelGrid 1.0, list update, transform, VoxelGrid 0.2 / 0.4), synchronous like the reference.
+    Each rank owns its map (independent sequences: weak scaling, no collective)."""
+    import torch
+    from llsr import LocalMap, synth
+    from llsr.dist import max_over_ranks
+    rank = dist.get_rank() if dist else 0
+    frames = synth.make_keyframes(K, seed=17 + rank, corner=200, surf=6000, outlier=1500)
+    m = LocalMap(dev)
+    for pose, c, s, o in frames:
+        m.add_keyframe(pose, torch.from_numpy(c).to(dev), torch.from_numpy(s).to(dev), torch.from_numpy(o).to(dev))
+    positions = [frames[(7 * i) % K][0][:3] + np.float32(0.25) for i in range(warmup + steps)]
+    reps = []
+    for i in range(warmup):
+        m.extract(positions[i])
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(warmup, warmup + steps):
+        gc, gs, rep = m.extract(positions[i])
+        reps.append(rep)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    el = max_over_ranks(time.perf_counter() - t0, dev)
+    world = dist.get_world_size() if dist else 1
+    pts = float(np.mean([r["n_corner_map"] + r["n_surf_map"] for r in reps]))
+    out = {"workload": f"extractSurroundingKeyFrames over {K} stored keyframes (200/6000/1500 pts), "
+                       "radius 50 m, VoxelGrid 0.2 / 0.4 of the assembled local map, one extract per step",
+           "value": round(steps * world / el, 1), "unit": "extracts/s", "scaling": "weak", "steps": steps,
+           "ms_per_extract": round(el / steps * 1e3, 3),
+           "map_points_per_extract": round(pts), "keyframes_per_extract": float(np.mean([r["n_keyframes"] for r in reps])),
+           "map_points_per_s": round(pts * steps * world / el, 1),
+           "ds_points_per_extract": round(float(np.mean([r["n_corner_ds"] + r["n_surf_ds"] for r in reps])))}
+    if check:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle_py
+        om = oracle_py.OracleMap(stable=True)
+        for pose, c, s, o in frames:
+            om.add_keyframe(pose, c, s, o)
+        t_cpu, n_cpu = 0.0, 0
+        for i, p in enumerate(positions):
+            t1 = time.perf_counter()
+            rc, rs, _, _ = om.extract(p)
+            t_cpu += time.perf_counter() - t1
+            n_cpu += 1
+        out["bit_exact_last_extract"] = bool(
+            np.array_equal(gc.cpu().numpy().view(np.uint32), rc.view(np.uint32))
+            and np.array_equal(gs.cpu().numpy().view(np.uint32), rs.view(np.uint32)))
+        # CPU baseline: the PCL-order restatement (std::sort), one core, bounded
+        op = oracle_py.OracleMap(stable=False)
+        for pose, c, s, o in frames:
+            op.add_keyframe(pose, c, s, o)
+        t_cpu, n_cpu, i = 0.0, 0, 0
+        while t_cpu < cpu_seconds and n_cpu < 200:
+            t1 = time.perf_counter()
+            op.extract(positions[i % len(positions)])
+            t_cpu += time.perf_counter() - t1
+            n_cpu += 1
+            i += 1
+        out["cpu_baseline"] = {"value": round(n_cpu / t_cpu, 2), "unit": "extracts/s", "cores": 1, "kind": "port",
+                               "sample": f"{n_cpu} extracts on the same map and path through oracle_map_extract "
+                                         f"(std::sort VoxelGrid as PCL), 1 thread, {t_cpu:.1f} s"}
+        out["speedup_vs_cpu"] = round(out["value"] / world / out["cpu_baseline"]["value"], 1)
+    m.close()
+    return out
+
+
 def ctypes_sizeof_report() -> int:
     import ctypes
     from llsr import _abi
@@ -393,6 +465,8 @@ def main():
     ap.add_argument("--s2m-modes", default="lm_applied,faithful", help="comma list; empty = skip the leg")
     ap.add_argument("--odo", default="hdl64e:128,vlp16:1024",
                     help="odometry legs lidar:sequences_per_gpu, comma list (empty = skip)")
+    ap.add_argument("--map-keyframes", type=int, default=200,
+                    help="local-map leg: keyframes in the store (0 = skip)")
     ap.add_argument("--allreduce-scans", type=int, default=8,
                     help="configs[4] leg: scans per step split over all ranks (0 = skip)")
     args = ap.parse_args()
@@ -511,6 +585,11 @@ def main():
         odo[lid] = odometry_leg(dev, lid, int(nb), 2, 4, args.s2m_steps, 2, dist,
                                 rank == 0 and not args.no_cpu and world == 1, min(args.cpu_seconds, 10.0))
 
+    lmap = None
+    if args.map_keyframes > 0:
+        lmap = local_map_leg(dev, args.map_keyframes, args.s2m_steps * 4, 2, dist,
+                             rank == 0 and not args.no_cpu and world == 1, min(args.cpu_seconds, 8.0))
+
     allred = None
     if args.allreduce_scans > 0:
         allred = scan2map_allreduce_leg(dev, args.allreduce_scans, args.s2m_steps, 1, dist,
@@ -546,6 +625,7 @@ def main():
             "scan2map": s2m,
             "scan2map_allreduce": allred,
             "odometry": odo,
+            "local_map": lmap,
         }
         if not args.no_cpu and world == 1:
             scans = [pts[off[k]:off[k + 1]] for k in range(min(args.distinct, B))]
