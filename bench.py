@@ -441,6 +441,59 @@ def local_map_leg(dev, K: int, steps: int, warmup: int, dist, check: bool, cpu_s
     return out
 
 
+def pc2_decode_leg(dev, pts: np.ndarray, off: np.ndarray, steps: int, dist) -> dict:
+    """sensor_msgs/PointCloud2 -> PointXYZI (pcl::fromROSMsg, IP:196; llsr_decode_pointcloud2) of the
+    bench's own B scans encoded in the velodyne_pointcloud layout (x, y, z, intensity, ring, time;
+    point_step 32), message bytes resident in HBM. One step = one decode call of the whole batch
+    (host table upload + k_decode_pc2 + sync). Algorithmic bytes: 32 read + 16 written per point."""
+    import ctypes as C
+    import torch
+    import llsr
+    from llsr import _abi
+    from llsr.dist import max_over_ranks
+    B = len(off) - 1
+    n = int(off[-1])
+    rec = np.zeros(n, dtype=[("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("pad", "<f4"), ("intensity", "<f4"),
+                             ("ring", "<u2"), ("pad2", "<u2"), ("time", "<f4"), ("pad3", "<f4")])
+    for a, name in enumerate(("x", "y", "z", "intensity")):
+        rec[name] = pts[:, a]
+    data = torch.from_numpy(rec.view(np.uint8).reshape(-1)).to(dev)
+    lay = llsr.pc2_layout([("x", 0, 7, 1), ("y", 4, 7, 1), ("z", 8, 7, 1), ("intensity", 16, 7, 1),
+                           ("ring", 20, 4, 1), ("time", 24, 7, 1)], 32)
+    msgs = (_abi.Pc2Msg * B)()
+    for b in range(B):
+        w = int(off[b + 1] - off[b])
+        msgs[b].data_offset, msgs[b].width, msgs[b].height, msgs[b].row_step = int(off[b]) * 32, w, 1, 32 * w
+    out = torch.empty((n, 4), dtype=torch.float32, device=dev)
+    hoff = np.zeros(B + 1, np.int64)
+    d_off = torch.empty(B + 1, dtype=torch.int64, device=dev)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
+
+    def step():
+        rc = llsr.lib().llsr_decode_pointcloud2(C.byref(lay), C.c_void_p(data.data_ptr()), msgs, B,
+                                                C.c_void_p(out.data_ptr()), hoff.ctypes.data,
+                                                C.c_void_p(d_off.data_ptr()), C.c_void_p(stream.cuda_stream))
+        assert rc == 0, rc
+
+    step()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    if dist:
+        dist.barrier()
+    el = max_over_ranks(time.perf_counter() - t0, dev)
+    world = dist.get_world_size() if dist else 1
+    exact = bool(np.array_equal(out.cpu().numpy().view(np.uint32), np.ascontiguousarray(pts, np.float32).view(np.uint32)))
+    gbs = 48.0 * n / (el / steps) / 1e9
+    return {"workload": f"PointCloud2 decode of {B} VLP-16 messages per GPU (velodyne layout, point_step 32)",
+            "value": round(B * steps * world / el, 1), "unit": "messages/s", "scaling": "weak",
+            "ms_per_call": round(el / steps * 1e3, 4), "points_per_call": n,
+            "algorithmic_GBs_incl_host_sync": round(gbs, 1), "bit_exact": exact}
+
+
 def ctypes_sizeof_report() -> int:
     import ctypes
     from llsr import _abi
@@ -467,6 +520,7 @@ def main():
                     help="odometry legs lidar:sequences_per_gpu, comma list (empty = skip)")
     ap.add_argument("--map-keyframes", type=int, default=200,
                     help="local-map leg: keyframes in the store (0 = skip)")
+    ap.add_argument("--pc2", type=int, default=1, help="PointCloud2 decode leg (0 = skip)")
     ap.add_argument("--allreduce-scans", type=int, default=8,
                     help="configs[4] leg: scans per step split over all ranks (0 = skip)")
     args = ap.parse_args()
@@ -585,6 +639,8 @@ def main():
         odo[lid] = odometry_leg(dev, lid, int(nb), 2, 4, args.s2m_steps, 2, dist,
                                 rank == 0 and not args.no_cpu and world == 1, min(args.cpu_seconds, 10.0))
 
+    pc2 = pc2_decode_leg(dev, pts, off, args.s2m_steps * 4, dist) if args.pc2 else None
+
     lmap = None
     if args.map_keyframes > 0:
         lmap = local_map_leg(dev, args.map_keyframes, args.s2m_steps * 4, 2, dist,
@@ -626,6 +682,7 @@ def main():
             "scan2map_allreduce": allred,
             "odometry": odo,
             "local_map": lmap,
+            "pointcloud2_decode": pc2,
         }
         if not args.no_cpu and world == 1:
             scans = [pts[off[k]:off[k + 1]] for k in range(min(args.distinct, B))]

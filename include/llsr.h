@@ -378,6 +378,51 @@ int32_t llsr_map_extract(llsr_map* m, const float robot_pos[3], float* d_corner,
 /* surroundingExistingKeyPosesID after the last extract; returns its length. */
 int32_t llsr_map_keyframe_ids(const llsr_map* m, int32_t* out, int32_t cap);
 
+
+/* ---- Input wire formats (llsr_input.hip) ----
+ * sensor_msgs/PointCloud2 (PointField datatype codes, sensor_msgs/msg/PointField.msg) decoded as
+ * pcl::fromROSMsg<PointXYZI> (IP:196): x, y, z, intensity are taken from the fields of that name
+ * whose datatype is FLOAT32 and count 1; any other field is ignored and an unmatched PointXYZI
+ * field reads 0 (its default). Byte order is taken as-is (PCL ignores is_bigendian). */
+#define LLSR_PC2_FLOAT32 7
+#define LLSR_PC2_MAX_FIELDS 16
+typedef struct llsr_pc2_field {
+  char name[16];
+  int32_t offset;    /* byte offset in the point */
+  int32_t datatype;  /* PointField.datatype */
+  int32_t count;
+} llsr_pc2_field;
+typedef struct llsr_pc2_layout {  /* the message's fields + point_step (constant per sensor) */
+  int32_t point_step;
+  int32_t num_fields;
+  llsr_pc2_field fields[LLSR_PC2_MAX_FIELDS];
+} llsr_pc2_layout;
+typedef struct llsr_pc2_msg {     /* one message of the batch */
+  int64_t data_offset;            /* first byte of its `data` in the packed device buffer */
+  int32_t width, height;          /* points = width * height */
+  int32_t row_step;               /* bytes per row (organized clouds, height > 1) */
+  int32_t pad;
+} llsr_pc2_msg;
+/* Decode B messages whose data bytes are packed in d_data (device) into float4 x, y, z, intensity
+ * points packed in d_out (device, capacity sum(width * height)), in row-major point order; writes
+ * the point offsets to out_off[B+1] (host) and, if not NULL, to d_out_off[B+1] (device) — the
+ * inputs llsr_process_batch / llsr_odometry_batch take. NaN points are kept (those calls remove
+ * them, IP:198). Synchronises hip_stream. */
+int32_t llsr_decode_pointcloud2(const llsr_pc2_layout* layout, const uint8_t* d_data, const llsr_pc2_msg* msgs,
+                                int32_t B, float* d_out, int64_t* out_off, int64_t* d_out_off, void* hip_stream);
+/* KITTI velodyne sequences (offlineKittiService IP:224-248, KittiLoader imageProjection.h:127-200):
+ * a frame file holds float32 x, y, z, reflectance records; like the reference, at most
+ * LLSR_KITTI_MAX_FLOATS floats are read and floor(floats / 4) points kept. */
+#define LLSR_KITTI_MAX_FLOATS 1000000
+/* Number of consecutive frames <dir>/%06d.bin starting at 0. */
+int32_t llsr_kitti_count(const char* velodyne_dir);
+/* One frame into a host buffer (capacity cap points); *n = points (LLSR_ERANGE if > cap). */
+int32_t llsr_kitti_read(const char* path, float* xyzi, int32_t cap, int32_t* n);
+/* Frames first .. first+B-1 of <dir> into d_xyzi (device, capacity cap_points) with one pinned
+ * upload; point offsets to off[B+1] (host) and, if not NULL, d_off[B+1] (device). Synchronises. */
+int32_t llsr_kitti_load(const char* velodyne_dir, int32_t first, int32_t B, float* d_xyzi, int64_t cap_points,
+                        int64_t* off, int64_t* d_off, void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -40,6 +40,7 @@ EXPORTS = [
     "llsr_odometry_reset", "llsr_map_config_default", "llsr_map_create", "llsr_map_destroy",
     "llsr_map_last_error", "llsr_map_reset", "llsr_map_voxel_grid", "llsr_map_downsample_scan",
     "llsr_map_add_keyframe", "llsr_map_num_keyframes", "llsr_map_extract", "llsr_map_keyframe_ids",
+    "llsr_decode_pointcloud2", "llsr_kitti_count", "llsr_kitti_read", "llsr_kitti_load",
 ]
 
 
@@ -102,6 +103,12 @@ def lib():
         L.llsr_map_extract.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,
                                        C.POINTER(_abi.MapReport), C.c_void_p]
         L.llsr_map_keyframe_ids.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+        L.llsr_decode_pointcloud2.argtypes = [C.POINTER(_abi.Pc2Layout), C.c_void_p, C.c_void_p, C.c_int32,
+                                              C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.llsr_kitti_count.argtypes = [C.c_char_p]
+        L.llsr_kitti_read.argtypes = [C.c_char_p, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)]
+        L.llsr_kitti_load.argtypes = [C.c_char_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p,
+                                      C.c_void_p, C.c_void_p]
         for fn in EXPORTS:
             if fn not in ("llsr_last_error", "llsr_kernel_name", "llsr_destroy", "llsr_map_create",
                           "llsr_map_destroy", "llsr_map_last_error"):
@@ -499,3 +506,80 @@ class LocalMap:
         out = np.zeros(max(n, 1), np.int32)
         lib().llsr_map_keyframe_ids(self._m, out.ctypes.data, n)
         return out[:n]
+
+
+# ---- input wire formats (llsr_input.hip) ----
+
+def pc2_layout(fields, point_step: int) -> _abi.Pc2Layout:
+    """fields: iterable of (name, offset, datatype, count) as in sensor_msgs/PointField."""
+    lay = _abi.Pc2Layout()
+    fields = list(fields)
+    if len(fields) > _abi.PC2_MAX_FIELDS:
+        raise ValueError("too many PointCloud2 fields")
+    lay.point_step = point_step
+    lay.num_fields = len(fields)
+    for k, (name, off, dt, cnt) in enumerate(fields):
+        lay.fields[k].name = name.encode()
+        lay.fields[k].offset, lay.fields[k].datatype, lay.fields[k].count = off, dt, cnt
+    return lay
+
+
+def decode_pointcloud2(layout: _abi.Pc2Layout, messages, device: int = 0, stream: int = 0):
+    """pcl::fromROSMsg<PointXYZI> of a batch of PointCloud2 messages. messages: list of
+    (data bytes, width, height, row_step). The bytes are uploaded, decoded on the device, and the
+    float4 points returned as a torch tensor (n, 4) with host and device point offsets [B+1]."""
+    import torch
+    dev = torch.device("cuda", device)
+    B = len(messages)
+    msgs = (_abi.Pc2Msg * B)()
+    blobs, pos = [], 0
+    for b, (data, width, height, row_step) in enumerate(messages):
+        raw = np.frombuffer(bytes(data), np.uint8)
+        pad = (-pos) % 16                     # keep every message 16-byte aligned in the pack
+        if pad:
+            blobs.append(np.zeros(pad, np.uint8))
+            pos += pad
+        msgs[b].data_offset, msgs[b].width, msgs[b].height, msgs[b].row_step = pos, width, height, row_step
+        blobs.append(raw)
+        pos += len(raw)
+    data = torch.from_numpy(np.concatenate(blobs) if blobs else np.zeros(1, np.uint8)).to(dev)
+    n = sum(w * h for _, w, h, _ in messages)
+    out = torch.empty((max(n, 1), 4), dtype=torch.float32, device=dev)
+    off = np.zeros(B + 1, np.int64)
+    d_off = torch.empty(B + 1, dtype=torch.int64, device=dev)
+    torch.cuda.current_stream(dev).synchronize()
+    rc = lib().llsr_decode_pointcloud2(C.byref(layout), C.c_void_p(data.data_ptr()), msgs, B,
+                                       C.c_void_p(out.data_ptr()), off.ctypes.data, C.c_void_p(d_off.data_ptr()),
+                                       C.c_void_p(stream))
+    if rc != 0:
+        raise LlsrError(f"llsr_decode_pointcloud2 failed ({rc})")
+    return out[:n], off, d_off
+
+
+def kitti_count(velodyne_dir: str) -> int:
+    return lib().llsr_kitti_count(velodyne_dir.encode())
+
+
+def kitti_read(path: str) -> np.ndarray:
+    """One KITTI .bin frame as (n, 4) float32, read the way the reference's loader reads it."""
+    out = np.zeros((_abi.KITTI_MAX_FLOATS // 4, 4), np.float32)
+    n = C.c_int32()
+    rc = lib().llsr_kitti_read(path.encode(), out.ctypes.data, len(out), C.byref(n))
+    if rc != 0:
+        raise LlsrError(f"llsr_kitti_read({path}) failed ({rc})")
+    return out[:n.value].copy()
+
+
+def kitti_load(velodyne_dir: str, first: int, B: int, cap_points: int, device: int = 0, stream: int = 0):
+    """Frames first .. first+B-1 into HBM: (points tensor (n, 4), host offsets, device offsets)."""
+    import torch
+    dev = torch.device("cuda", device)
+    out = torch.empty((max(cap_points, 1), 4), dtype=torch.float32, device=dev)
+    off = np.zeros(B + 1, np.int64)
+    d_off = torch.empty(B + 1, dtype=torch.int64, device=dev)
+    torch.cuda.current_stream(dev).synchronize()
+    rc = lib().llsr_kitti_load(velodyne_dir.encode(), first, B, C.c_void_p(out.data_ptr()), cap_points,
+                               off.ctypes.data, C.c_void_p(d_off.data_ptr()), C.c_void_p(stream))
+    if rc != 0:
+        raise LlsrError(f"llsr_kitti_load failed ({rc})")
+    return out[:off[-1]], off, d_off

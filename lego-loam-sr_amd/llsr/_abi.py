@@ -218,6 +218,27 @@ class MapReport(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+PC2_FLOAT32 = 7
+PC2_MAX_FIELDS = 16
+KITTI_MAX_FLOATS = 1000000
+
+
+class Pc2Field(C.Structure):
+    """llsr_pc2_field: sensor_msgs/PointField."""
+    _fields_ = [("name", C.c_char * 16), ("offset", C.c_int32), ("datatype", C.c_int32), ("count", C.c_int32)]
+
+
+class Pc2Layout(C.Structure):
+    """llsr_pc2_layout: the PointCloud2 fields + point_step."""
+    _fields_ = [("point_step", C.c_int32), ("num_fields", C.c_int32), ("fields", Pc2Field * PC2_MAX_FIELDS)]
+
+
+class Pc2Msg(C.Structure):
+    """llsr_pc2_msg: one message of a decode batch."""
+    _fields_ = [("data_offset", C.c_int64), ("width", C.c_int32), ("height", C.c_int32),
+                ("row_step", C.c_int32), ("pad", C.c_int32)]
+
+
 class Sizes(C.Structure):
     _fields_ = [("cells", C.c_int32), ("rings", C.c_int32), ("max_points", C.c_int32),
                 ("shadow_points", C.c_int32)]

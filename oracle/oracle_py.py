@@ -456,3 +456,30 @@ class OracleMap:
         rep = {"n_corner_map": int(raw[0]), "n_surf_map": int(raw[1]), "n_in_radius": int(raw[2]),
                "n_poses_ds": int(raw[3]), "n_keyframes": nid.value}
         return oc[:nc.value].copy(), os_[:ns.value].copy(), ids[:nid.value].copy(), rep
+
+
+def decode_pointcloud2(fields, point_step: int, data: bytes, width: int, height: int, row_step: int) -> np.ndarray:
+    """pcl::fromROSMsg<PointXYZI> (PCL 1.10 createMapping + copy, IP:196) restated with numpy:
+    x / y / z / intensity are copied from the field of that name when its datatype is FLOAT32 (7)
+    and count 1, else left at PointXYZI's default 0; points in row-major order, row r starting at
+    byte r * row_step. NaN points are kept (removeNaNFromPointCloud is a separate step)."""
+    raw = np.frombuffer(bytes(data), np.uint8)
+    n = width * height
+    out = np.zeros((n, 4), np.float32)
+    idx = np.arange(n)
+    base = (idx // max(width, 1)) * row_step + (idx % max(width, 1)) * point_step
+    for a, name in enumerate(("x", "y", "z", "intensity")):
+        for fname, off, dt, cnt in fields:
+            if fname == name and dt == 7 and cnt == 1:
+                b = base[:, None] + off + np.arange(4)[None, :]
+                out[:, a] = raw[b].copy().view(np.float32).reshape(n) if n else out[:, a]
+                break
+    return out
+
+
+def kitti_read(path: str) -> np.ndarray:
+    """KittiLoader::get_cloud / offlineKittiService (imageProjection.h:159-170, IP:234-241): at most
+    1,000,000 floats are read and floor(floats_read / 4) points kept."""
+    buf = np.fromfile(path, dtype=np.float32, count=1000000)
+    n = len(buf) // 4
+    return buf[:4 * n].reshape(n, 4).copy()
