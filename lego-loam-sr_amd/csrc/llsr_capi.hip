@@ -29,7 +29,7 @@ __global__ void k_fa_points(DevCfg, DevBufs);
 __global__ void k_select_ring(DevCfg, DevBufs);
 __global__ void k_fa_concat(DevCfg, DevBufs);
 __global__ void k_dbscan_adj(DevCfg, DevBufs);
-__global__ void k_dbscan_merge(DevCfg, DevBufs);
+template <int kDbL> __global__ void k_dbscan_merge(DevCfg, DevBufs);
 
 __global__ void k_init_counts(int* counts, int B) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -406,7 +406,8 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   mark();
   k_dbscan_adj<<<dim3(32, B), 256, 0, s>>>(c, h->d);
   mark();
-  k_dbscan_merge<<<B, 64, 0, s>>>(c, h->d);
+  if (c.HW <= 32768) k_dbscan_merge<1024><<<B, 64, 0, s>>>(c, h->d);
+  else k_dbscan_merge<2048><<<B, 64, 0, s>>>(c, h->d);
   mark();
   HIP_OK(h, hipGetLastError());
   if (h->profiling) {
@@ -454,7 +455,10 @@ extern "C" float llsr_debug_phase_ms(llsr_handle* h, int32_t k, int32_t phase, i
       case 8: k_select_ring<<<dim3(c.H, B), 256, 0, s>>>(c, h->d); break;
       case 9: k_fa_concat<<<B, 256, 0, s>>>(c, h->d); break;
       case 10: k_dbscan_adj<<<dim3(32, B), 256, 0, s>>>(c, h->d); break;
-      case 11: k_dbscan_merge<<<B, 64, 0, s>>>(c, h->d); break;
+      case 11:
+        if (c.HW <= 32768) k_dbscan_merge<1024><<<B, 64, 0, s>>>(c, h->d);
+        else k_dbscan_merge<2048><<<B, 64, 0, s>>>(c, h->d);
+        break;
       case 7: k_fa_points<<<B, 1024, 0, s>>>(c, h->d); break;
       case 6: k_segment<<<B, 1024, 0, s>>>(c, nullptr, nullptr, h->d); break;
       case 5:

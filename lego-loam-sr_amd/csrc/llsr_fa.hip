@@ -172,7 +172,8 @@ __device__ __forceinline__ int pow2_ceil(int n) {
 // each chunk of 64 candidates reads `picked` once; the first still-alive candidate is selected,
 // candidates inside its suppression interval die, repeat. Steps per chunk = picks in the chunk.
 // Returns the number selected; writes labels, picked and the output list in selection order.
-__device__ __forceinline__ int greedy_wave(const int* order, int nc, int ws, uint8_t* wpick, const uint8_t* wreach,
+template <class Order>
+__device__ __forceinline__ int greedy_wave(Order order, int nc, int ws, uint8_t* wpick, const uint8_t* wreach,
                                            int8_t* wlab, int8_t lab, int* outp) {
   const int l = lane_id();
   const unsigned long long lt = (1ull << l) - 1ull;
@@ -180,7 +181,8 @@ __device__ __forceinline__ int greedy_wave(const int* order, int nc, int ws, uin
   for (int t0 = 0; t0 < nc; t0 += 64) {
     const int t = t0 + l;
     const bool valid = t < nc;
-    const int w = valid ? order[t] - ws : 0;
+    const int ind = valid ? order(t) : 0;
+    const int w = valid ? ind - ws : 0;
     bool alive = valid && wpick[w] == 0;
     const int r = valid ? wreach[w] : 0;
     const int lo = w - (r >> 4), hi = w + (r & 15);
@@ -196,7 +198,7 @@ __device__ __forceinline__ int greedy_wave(const int* order, int nc, int ws, uin
     }
     if ((sel >> l) & 1ull) {
       wlab[w] = lab;
-      outp[nsel + __popcll(sel & lt)] = order[t];
+      outp[nsel + __popcll(sel & lt)] = ind;
       for (int q = lo; q <= hi; ++q) wpick[q] = 1;
     }
     nsel += __popcll(sel);
@@ -207,15 +209,18 @@ __device__ __forceinline__ int greedy_wave(const int* order, int nc, int ws, uin
 }
 
 __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
+  // LDS 36 KB -> 4 workgroups per CU. The window arrays are dead once the less-flat candidates are
+  // compacted, so the VoxelGrid's voxel ids reuse their bytes; the greedy passes read the visiting
+  // order straight from the sorted keys.
   __shared__ uint64_t key[kRingMax];
-  __shared__ uint8_t wpick[kWin];
-  __shared__ uint8_t wgnd[kWin];
-  __shared__ int8_t wlab[kWin];
-  __shared__ uint16_t wcol[kWin];
-  __shared__ uint8_t wreach[kWin];  // suppression reach: fwd | bwd << 4 (FA:1186-1205)
+  __shared__ uint32_t win_raw[6 * kWin / 4];
+  uint8_t* wpick = reinterpret_cast<uint8_t*>(win_raw);
+  uint8_t* wgnd = wpick + kWin;
+  int8_t* wlab = reinterpret_cast<int8_t*>(wpick + 2 * kWin);
+  uint8_t* wreach = wpick + 3 * kWin;  // suppression reach: fwd | bwd << 4 (FA:1186-1205)
+  uint16_t* wcol = reinterpret_cast<uint16_t*>(wpick + 4 * kWin);
   __shared__ uint16_t cpos[kRingMax];
   __shared__ uint16_t rstart[kRingMax + 1];
-  __shared__ int order[kRingMax + 1];
   __shared__ int tmp[8];
   __shared__ float red[6][4];
   __shared__ int s_cnt, s_sel;
@@ -284,11 +289,10 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   if (c.dbg_phase <= 1) return;
   // visiting order: the unsorted entry at ep first, then descending keys (FA:1175)
   const bool epE = curv[ep] > c.edge_thr && wgnd[ep - ws] == 0;
-  for (int t = tid; t < nE; t += nt) order[t + (epE ? 1 : 0)] = (int)(uint32_t)key[n2 - 1 - t];
-  if (tid == 0 && epE) order[0] = ep;
-  __syncthreads();
+  const int e0 = epE ? 1 : 0;
   if (tid < 64) {
-    const int cnt = greedy_wave(order, nE + (epE ? 1 : 0), ws, wpick, wreach, wlab, (int8_t)1, d.edge_tmp + base + sp);
+    auto order = [&](int t) { return t < e0 ? ep : (int)(uint32_t)key[n2 - 1 - (t - e0)]; };
+    const int cnt = greedy_wave(order, nE + e0, ws, wpick, wreach, wlab, (int8_t)1, d.edge_tmp + base + sp);
     if (tid == 0) { rc[i] = cnt; s_cnt = 0; }
   }
   __syncthreads();
@@ -309,10 +313,8 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   bitonic_sort_u64(key, n2);
   // visiting order: ascending keys, then the unsorted entry at ep (FA:1211)
   const bool epF = curv[ep] < c.surf_thr && wgnd[ep - ws] == 1;
-  for (int t = tid; t < nF; t += nt) order[t] = (int)(uint32_t)key[t];
-  if (tid == 0 && epF) order[nF] = ep;
-  __syncthreads();
   if (tid < 64) {
+    auto order = [&](int t) { return t < nF ? (int)(uint32_t)key[t] : ep; };
     const int cnt = greedy_wave(order, nF + (epF ? 1 : 0), ws, wpick, wreach, wlab, (int8_t)-1, d.flat_tmp + base + sp);
     if (tid == 0) rc[H + i] = cnt;
   }
@@ -370,7 +372,7 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   }
   const int mul1 = div[0], mul2 = div[0] * div[1];
   // voxel id of every candidate, in ring order (points of one voxel are mostly consecutive)
-  uint32_t* vk = (uint32_t*)order;
+  uint32_t* vk = win_raw;  // the window arrays are dead (barrier after the compaction above)
   for (int t = tid; t < L; t += nt) {
     const float4 p = lp[cpos[t]];
     const int i0 = (int)(floorf(p.x * inv) - (float)minb[0]);
@@ -698,17 +700,20 @@ __device__ __forceinline__ void dbscan_merge(const DevCfg& c, const DevBufs& d, 
   if (l == 0) d.counts[b * kCnt + C_SHARP] = ns;
 }
 
+// One wave per scan, so the LDS footprint sets how many scans a CU runs at once: kDbL = 1024
+// (24.6 KB, VLP-16-sized scans, M ~ 300) fits every SIMD of a CU; 2048 (49 KB) serves HDL-64E.
+template <int kDbL>
 __global__ __launch_bounds__(64) void k_dbscan_merge(DevCfg c, DevBufs d) {
-  __shared__ int sPar[2 * kDb + 4];
-  __shared__ int sRaw[kDb];
-  __shared__ int sNb[kDb];
-  __shared__ int sRt[kDb + 1];
-  __shared__ int sLive[kDb + 1];
+  __shared__ int sPar[2 * kDbL + 4];
+  __shared__ int sRaw[kDbL];
+  __shared__ int sNb[kDbL];
+  __shared__ int sRt[kDbL + 1];
+  __shared__ int sLive[kDbL + 1];
   __shared__ int sN[1];
   const int b = blockIdx.x;
   const size_t base = (size_t)b * c.HW;
   const int M = d.counts[b * kCnt + C_M];
-  if (M <= kDb) {
+  if (M <= kDbL) {
     dbscan_merge<true>(c, d, base, b, M, sPar, sRaw, sNb, sRt, sLive, sN);
   } else {  // global scratch: ccl_b (2*HW ints) parent, ccl_a raw, cluster nb, edge_tmp rt, shuf live
     dbscan_merge<false>(c, d, base, b, M, (int*)(d.ccl_b + base), d.ccl_a + base, d.flat_tmp + base,
@@ -716,4 +721,9 @@ __global__ __launch_bounds__(64) void k_dbscan_merge(DevCfg c, DevBufs d) {
   }
 }
 
+}  // namespace llsr
+
+namespace llsr {
+template __global__ void k_dbscan_merge<1024>(DevCfg, DevBufs);
+template __global__ void k_dbscan_merge<2048>(DevCfg, DevBufs);
 }  // namespace llsr
