@@ -223,7 +223,7 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   __shared__ uint16_t rstart[kRingMax + 1];
   __shared__ int tmp[8];
   __shared__ float red[6][4];
-  __shared__ int s_cnt, s_sel;
+  __shared__ int s_cnt;
   const int i = blockIdx.x, b = blockIdx.y;
   const int H = c.H, HW = c.HW;
   const size_t base = (size_t)b * HW;
@@ -265,12 +265,6 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
     wreach[t] = (uint8_t)(f | (bk << 4));
   }
   __syncthreads();
-  auto suppress = [&](int ind) {
-    const int w = ind - ws;
-    const int r = wreach[w];
-    const int lo = w - (r >> 4), hi = w + (r & 15);
-    for (int q = lo; q <= hi; ++q) wpick[q] = 1;
-  };
   // ---- edges: statically eligible sorted-part entries, visited in descending key order ----
   for (int p = sp + tid; p < ep; p += nt) {
     const int ind = p == 4 ? 0 : p;
@@ -519,8 +513,6 @@ __global__ __launch_bounds__(256) void k_dbscan_adj(DevCfg c, DevBufs d) {
 // into min_label; a new label only re-points the neighbours. Checked against a literal
 // transcription of the loop in tests/test_dbscan_uf.py. Per point: O(degree) work.
 // ---------------------------------------------------------------------------------------------
-constexpr int kDb = 2048;
-
 __device__ __forceinline__ void wave_fence() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();

@@ -414,7 +414,6 @@ __global__ __launch_bounds__(1024) void k_ground_elev_ransac(DevCfg c, DevBufs d
   __shared__ MT rng;
   __shared__ int sh_int[8];
   __shared__ float sh_cf[4], best_cf[4];
-  __shared__ int sample[3];
   const int b = blockIdx.x;
   const int W = c.W, H = c.H, HW = c.HW;
   const size_t base = (size_t)b * HW;
@@ -439,7 +438,7 @@ __global__ __launch_bounds__(1024) void k_ground_elev_ransac(DevCfg c, DevBufs d
     int last = -1;
     for (int j = j0; j < j1; ++j) last = colok[j] > last ? colok[j] : last;
     // inclusive max-scan over threads
-    const int l = lane_id(), w = tid >> 6, nw = nt >> 6;
+    const int l = lane_id(), w = tid >> 6;
     int x = last;
     for (int dl = 1; dl < 64; dl <<= 1) {
       int y = __shfl_up(x, dl, 64);
