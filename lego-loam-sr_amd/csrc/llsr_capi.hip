@@ -119,6 +119,10 @@ struct llsr_handle {
   std::string err;
 };
 
+// The fused projection keeps the winning raw index per cell in LDS (k_project_fused).
+static int fused_lds(const DevCfg& c) { return c.HW * (int)sizeof(int); }
+static bool use_fused(const llsr_handle* h) { return h->dc.ccl_lds != 0; }
+
 static int32_t fail(llsr_handle* h, int32_t code, const std::string& msg) {
   if (h) h->err = msg;
   return code;
@@ -275,7 +279,7 @@ extern "C" int32_t llsr_create(const llsr_config* cfg, int32_t hip_device, int32
     if (hipFuncSetAttribute((const void*)k_label<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             h->dc.HW * (int)sizeof(int)) != hipSuccess ||
         hipFuncSetAttribute((const void*)k_project_fused, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            h->dc.HW * (int)sizeof(int)) != hipSuccess) {
+                            fused_lds(h->dc)) != hipSuccess) {
       llsr_destroy(h);
       return LLSR_ENODEV;
     }
@@ -374,11 +378,12 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
     ++k;
   };
   mark();
-  if (!c.ccl_lds) HIP_OK(h, hipMemsetAsync(h->d.cell_pt, 0xFF, sizeof(int) * (size_t)B * c.HW, s));
+  const bool fused = use_fused(h);
+  if (!fused) HIP_OK(h, hipMemsetAsync(h->d.cell_pt, 0xFF, sizeof(int) * (size_t)B * c.HW, s));
   k_init_counts<<<(B + 255) / 256, 256, 0, s>>>(h->d.counts, B);
   mark();
-  if (c.ccl_lds) {  // fused projection + column ground pass with the cell table in LDS
-    k_project_fused<<<B, 1024, c.HW * sizeof(int), s>>>(c, pts, d_offsets, h->d);
+  if (fused) {  // fused projection + column ground pass with the cell table in LDS
+    k_project_fused<<<B, 1024, fused_lds(c), s>>>(c, pts, d_offsets, h->d);
     mark();
     mark();
   } else {
@@ -468,8 +473,8 @@ extern "C" float llsr_debug_phase_ms(llsr_handle* h, int32_t k, int32_t phase, i
       case 4: k_ground_elev_ransac<<<B, 1024, 0, s>>>(c, h->d); break;
       case 3: k_ground_add<<<dim3((c.H + 3) / 4, B), 256, 0, s>>>(c, h->d); break;
       case 1:
-        if (!c.ccl_lds) return -2.f;
-        k_project_fused<<<B, 1024, c.HW * sizeof(int), s>>>(c, h->last_pts, h->last_off, h->d);
+        if (!use_fused(h)) return -2.f;
+        k_project_fused<<<B, 1024, fused_lds(c), s>>>(c, h->last_pts, h->last_off, h->d);
         break;
       default: return -2.f;
     }

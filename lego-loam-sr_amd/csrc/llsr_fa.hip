@@ -552,9 +552,15 @@ __device__ __forceinline__ void wave_order() {
   asm volatile("" ::: "memory");
 }
 
-template <bool lds>
+// kRowBlk adjacency rows are staged into LDS per block (one load latency per block instead of one
+// per point: the rows of a 300-point scan come from L2 / the Infinity Cache, ~1 us away), the next
+// block's words waiting in registers (kPF per lane) while the current one is merged.
+constexpr int kRowBlk = 32;
+
+template <bool lds, int kPF = 1>
 __device__ __forceinline__ void dbscan_merge(const DevCfg& c, const DevBufs& d, size_t base, int b, int M,
-                                             int* par, int* raw, int* nb, int* rt, int* live, int* shn) {
+                                             int* par, int* raw, int* nb, int* rt, int* live, int* shn,
+                                             uint32_t* rowbuf = nullptr) {
   auto sync_ = [&]() {
     if (lds) wave_order();
     else __threadfence_block();
@@ -570,8 +576,21 @@ __device__ __forceinline__ void dbscan_merge(const DevCfg& c, const DevBufs& d, 
   const uint32_t* adj = d.db_adj + (size_t)b * kAdjCap * kAdjWords;
   const int W32 = (M + 31) / 32;
   int label = 0;
-  // rows are <= 64 words when precomputed (M <= kAdjCap): prefetch row i+1 while merging row i
-  uint32_t nextw = (pre && M > 0 && l < W32) ? adj[l] : 0u;
+  // rows are <= 64 words when precomputed (M <= kAdjCap)
+  const bool staged = lds && pre && kRowBlk * W32 <= 64 * kPF;
+  const int bw = kRowBlk * W32;  // words per staged block
+  uint32_t pf[kPF];
+  auto fetch_block = [&](int blk) {
+#pragma unroll
+    for (int e = 0; e < kPF; ++e) {
+      const int idx = l + 64 * e;
+      const int r = idx / (W32 > 0 ? W32 : 1), w = idx - r * W32;
+      const int row = blk * kRowBlk + r;
+      pf[e] = (idx < bw && row < M) ? adj[(size_t)row * kAdjWords + w] : 0u;
+    }
+  };
+  if (staged && M > 0) fetch_block(0);
+  uint32_t nextw = (!staged && pre && M > 0 && l < W32) ? adj[l] : 0u;
   for (int i = 0; i < M; ++i) {
     const int zi = M + 2 + i;
     if (l == 0) raw[i] = zi;
@@ -579,8 +598,20 @@ __device__ __forceinline__ void dbscan_merge(const DevCfg& c, const DevBufs& d, 
     int deg = 0;
     bool i_in = false;
     const float4 pi = pre ? make_float4(0.f, 0.f, 0.f, 0.f) : d.db_pts[base + i];
-    const uint32_t roww = nextw;
-    if (pre) nextw = (i + 1 < M && l < W32) ? adj[(size_t)(i + 1) * kAdjWords + l] : 0u;
+    uint32_t roww;
+    if (staged) {
+      if (i % kRowBlk == 0) {
+#pragma unroll
+        for (int e = 0; e < kPF; ++e)
+          if (l + 64 * e < bw) rowbuf[l + 64 * e] = pf[e];
+        wave_order();
+        fetch_block(i / kRowBlk + 1);
+      }
+      roww = l < W32 ? rowbuf[(i % kRowBlk) * W32 + l] : 0u;
+    } else {
+      roww = nextw;  // prefetch row i+1 while merging row i
+      if (pre) nextw = (i + 1 < M && l < W32) ? adj[(size_t)(i + 1) * kAdjWords + l] : 0u;
+    }
     for (int w0 = 0; w0 < W32; w0 += 64) {
       const int w = w0 + l;
       uint32_t word = 0u;
@@ -696,6 +727,8 @@ __device__ __forceinline__ void dbscan_merge(const DevCfg& c, const DevBufs& d, 
 // (24.6 KB, VLP-16-sized scans, M ~ 300) fits every SIMD of a CU; 2048 (49 KB) serves HDL-64E.
 template <int kDbL>
 __global__ __launch_bounds__(64) void k_dbscan_merge(DevCfg c, DevBufs d) {
+  constexpr int kPF = kRowBlk * (kDbL / 32) / 64;  // staged words per lane (M <= kDbL)
+  __shared__ uint32_t sRows[kRowBlk * (kDbL / 32)];
   __shared__ int sPar[2 * kDbL + 4];
   __shared__ int sRaw[kDbL];
   __shared__ int sNb[kDbL];
@@ -706,7 +739,7 @@ __global__ __launch_bounds__(64) void k_dbscan_merge(DevCfg c, DevBufs d) {
   const size_t base = (size_t)b * c.HW;
   const int M = d.counts[b * kCnt + C_M];
   if (M <= kDbL) {
-    dbscan_merge<true>(c, d, base, b, M, sPar, sRaw, sNb, sRt, sLive, sN);
+    dbscan_merge<true, kPF>(c, d, base, b, M, sPar, sRaw, sNb, sRt, sLive, sN, sRows);
   } else {  // global scratch: ccl_b (2*HW ints) parent, ccl_a raw, cluster nb, edge_tmp rt, shuf live
     dbscan_merge<false>(c, d, base, b, M, (int*)(d.ccl_b + base), d.ccl_a + base, d.flat_tmp + base,
                         d.edge_tmp + base, d.shuf + base, d.shuf + base + c.HW - 1);

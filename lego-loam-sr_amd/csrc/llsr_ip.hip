@@ -148,11 +148,19 @@ __device__ __forceinline__ void ground_column(const DevCfg& c, const float4* __r
                                               int j) {
   bool haveRV = false, obs = false;
   float RVx = 0.f, RVy = 0.f, RVz = 0.f, lx = 0.f, ly = 0.f, lz = 0.f;
-  float4 fn = full[j];  // the next row's cell is loaded one step ahead of the serial test
+  // the column's cells are loaded 8 rows at a time, ahead of the serial test over them
+  constexpr int kR = 8;
+  float4 fr[kR];
   for (int i = 0; i < c.H; ++i) {
     const int cell = j + i * c.W;
-    const float4 f = fn;
-    if (i + 1 < c.H) fn = full[cell + c.W];
+    if (i % kR == 0) {
+#pragma unroll
+      for (int u = 0; u < kR; ++u) fr[u] = i + u < c.H ? full[cell + u * c.W] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float4 f = fr[0];
+#pragma unroll
+    for (int u = 1; u < kR; ++u)
+      if (i % kR == u) f = fr[u];
     int8_t g;
     if (f.w == 0.0f) {
       g = -1;
@@ -179,6 +187,8 @@ __device__ __forceinline__ void ground_column(const DevCfg& c, const float4* __r
   }
 }
 
+// The cell table holds each cell's winning raw index (LDS atomicMax; -1 = empty), 115 KB for
+// VLP-16, next to the 25 KB pass-2 transpose tile.
 __global__ __launch_bounds__(1024) void k_project_fused(DevCfg c, const float4* __restrict__ pts,
                                                         const int64_t* __restrict__ off, DevBufs d) {
   extern __shared__ int cidx[];
@@ -192,15 +202,26 @@ __global__ __launch_bounds__(1024) void k_project_fused(DevCfg c, const float4* 
   for (int q = tid; q < HW; q += nt) cidx[q] = -1;
   __syncthreads();
   int nfin = 0, first = INT_MAX, last = -1;
-  for (int i = tid; i < n; i += nt) {
-    const float4 p = pts[o0 + i];
-    if (!finite3(p)) continue;
-    ++nfin;
-    first = i < first ? i : first;
-    last = i;
-    float r;
-    const int cell = project_cell(c, p, &r);
-    if (cell >= 0) atomicMax(&cidx[cell], i);
+  // four coalesced point loads in flight per lane before any of the projection math
+  constexpr int kP = 4;
+  for (int i0 = tid; i0 < n; i0 += kP * nt) {
+    float4 pp[kP];
+#pragma unroll
+    for (int u = 0; u < kP; ++u) {
+      const int i = i0 + u * nt;
+      pp[u] = i < n ? pts[o0 + i] : make_float4(__builtin_nanf(""), 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < kP; ++u) {
+      const int i = i0 + u * nt;
+      if (!finite3(pp[u])) continue;
+      ++nfin;
+      first = i < first ? i : first;
+      last = i;
+      float r;
+      const int cell = project_cell(c, pp[u], &r);
+      if (cell >= 0) atomicMax(&cidx[cell], i);
+    }
   }
   nfin = block_reduce_add(nfin, tmp);
   first = block_reduce_min(first, tmp);
@@ -212,40 +233,50 @@ __global__ __launch_bounds__(1024) void k_project_fused(DevCfg c, const float4* 
     cnt[C_LAST] = last;
   }
   if (c.dbg_phase <= 0) return;
-  // pass 2 over the cells: each cell's winner is re-read (the cells of a row hold neighbouring
-  // azimuths, so the gather stays within a few cache lines) and only its range is recomputed;
-  // row / column come from the cell. Empty cells get the resetParameters values (IP:170-179).
-  // Four cells per thread per step: every LDS read and gather is issued before the stores.
+  // Pass 2 over tiles of H rows x 64 columns. A firing-ordered sensor stream (Velodyne: the rings of
+  // one azimuth are consecutive raw points) stores a tile's winners as one contiguous run of the
+  // input, so the tile is gathered column by column (coalesced) into LDS and written out row by
+  // row (coalesced full lines): neither side strides. Empty cells get the resetParameters values
+  // (IP:170-179); only the winner's range is recomputed, row / column come from the cell.
+  constexpr int kTC = 64, kTP = kTC + 1;  // padded rows: column-major LDS writes spread over banks
+  __shared__ float4 tfull[16 * kTP];
+  __shared__ float tvis[16 * kTP];
+  __shared__ int tpi[16 * kTP];
   const float qnan = __builtin_nanf("");
-  constexpr int kU = 4;
-  for (int q0 = tid; q0 < HW; q0 += kU * nt) {
-    int pi[kU];
-    float4 p[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int q = q0 + u * nt;
-      pi[u] = q < HW ? cidx[q] : -1;
+  const int H = c.H, W = c.W;
+  for (int c0 = 0; c0 < W; c0 += kTC) {
+    if (tid < H * kTC) {  // column-major over the tile
+      const int row = tid % H, ck = tid / H, col = c0 + ck;
+      int pi = -1;
+      float4 f = make_float4(qnan, qnan, qnan, 0.0f);
+      float vis = 0.0f;
+      if (col < W) {
+        pi = cidx[row * W + col];
+        if (pi >= 0) {
+          const float4 p = pts[o0 + pi];
+          f = make_float4(p.x, p.y, p.z, (float)((double)(float)row + (double)(float)col / 10000.0));
+          vis = p.w;
+        }
+      }
+      tfull[row * kTP + ck] = f;
+      tvis[row * kTP + ck] = vis;
+      tpi[row * kTP + ck] = pi;
     }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) p[u] = pi[u] >= 0 ? pts[o0 + pi[u]] : make_float4(qnan, qnan, qnan, 0.0f);
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int q = q0 + u * nt;
-      if (q >= HW) continue;
-      d.cell_pt[base + q] = pi[u];
-      if (pi[u] >= 0) {
-        const int row = q / c.W, col = q - row * c.W;
-        d.range[base + q] = sqrt_(p[u].x * p[u].x + p[u].y * p[u].y + p[u].z * p[u].z);
-        d.full[base + q] = make_float4(p[u].x, p[u].y, p[u].z, (float)((double)(float)row + (double)(float)col / 10000.0));
-        d.vis[base + q] = p[u].w;
-      } else {
-        d.range[base + q] = FLT_MAX;
-        d.full[base + q] = p[u];
-        d.vis[base + q] = 0.0f;
+    __syncthreads();
+    if (tid < H * kTC) {  // row-major over the tile
+      const int row = tid / kTC, ck = tid % kTC, col = c0 + ck;
+      if (col < W) {
+        const size_t q = base + (size_t)row * W + col;
+        const float4 f = tfull[row * kTP + ck];
+        const int pi = tpi[row * kTP + ck];
+        d.cell_pt[q] = pi;
+        d.range[q] = pi >= 0 ? sqrt_(f.x * f.x + f.y * f.y + f.z * f.z) : FLT_MAX;
+        d.full[q] = f;
+        d.vis[q] = tvis[row * kTP + ck];
       }
     }
+    __syncthreads();
   }
-  __syncthreads();
   if (c.dbg_phase <= 1) return;
   for (int j = tid; j < c.W; j += nt) ground_column(c, d.full + base, d.ground + base, j);
 }
