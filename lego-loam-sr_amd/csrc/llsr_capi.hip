@@ -403,7 +403,7 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   mark();
   k_segment<<<B, 1024, 0, s>>>(c, pts, d_offsets, h->d);
   mark();
-  k_fa_points<<<B, 1024, 0, s>>>(c, h->d);
+  k_fa_points<<<B, 512, 0, s>>>(c, h->d);
   mark();
   k_select_ring<<<dim3(c.H, B), 256, 0, s>>>(c, h->d);
   mark();
@@ -464,7 +464,7 @@ extern "C" float llsr_debug_phase_ms(llsr_handle* h, int32_t k, int32_t phase, i
         if (c.HW <= 32768) k_dbscan_merge<1024><<<B, 64, 0, s>>>(c, h->d);
         else k_dbscan_merge<2048><<<B, 64, 0, s>>>(c, h->d);
         break;
-      case 7: k_fa_points<<<B, 1024, 0, s>>>(c, h->d); break;
+      case 7: k_fa_points<<<B, 512, 0, s>>>(c, h->d); break;
       case 6: k_segment<<<B, 1024, 0, s>>>(c, nullptr, nullptr, h->d); break;
       case 5:
         if (c.ccl_lds) k_label<true><<<B, 1024, c.HW * sizeof(int), s>>>(c, h->d);

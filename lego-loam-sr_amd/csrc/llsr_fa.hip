@@ -27,9 +27,26 @@ __device__ __forceinline__ float ori_branch1(float o, float start) {
   return o;
 }
 
-constexpr int kTile = 1024;
+constexpr int kTile = 2048;  // points per tile: 4 per lane (512 lanes), so every lane has 4 loads in flight
 
-__global__ __launch_bounds__(1024) void k_fa_points(DevCfg c, DevBufs d) {
+// LOAM-frame point of segmented point i (FA:565-598): orientation branch by the halfPassed latch
+// (`first`), relative time, intensity = ring + scan_period * relTime.
+__device__ __forceinline__ float4 loam_point(const DevCfg& c, float4 p, int i, int first, float start, float endo,
+                                             float diff) {
+  float o = -atan2f_(p.y, p.x);  // point.x = y, point.z = x (FA:573-577)
+  if (i <= first) {
+    o = ori_branch1(o, start);
+  } else {
+    o = (float)(o + 2 * kPi);
+    if ((double)o < (double)endo - kPi * 3 / 2) o = (float)(o + 2 * kPi);
+    else if ((double)o > (double)endo + kPi / 2) o = (float)(o - 2 * kPi);
+  }
+  const float relTime = (o - start) / diff;
+  const float inten = (float)(int)(p.w) + c.scan_period * relTime;
+  return make_float4(p.y, p.z, p.x, inten);
+}
+
+__global__ __launch_bounds__(512) void k_fa_points(DevCfg c, DevBufs d) {
   __shared__ float4 tp[kTile + 10];
   __shared__ uint8_t fl[kTile + 12];  // bit0 A_i, bit1 B_i, bit2 C_i for i in [t0-6, t0+T+6)
   __shared__ int tmp[32];
@@ -43,38 +60,49 @@ __global__ __launch_bounds__(1024) void k_fa_points(DevCfg c, DevBufs d) {
   float4* loam = d.loam + base;
 
   int first = INT_MAX;
-  for (int i = tid; i < S; i += nt) {
-    const float4 p = seg[i];
-    const float o = ori_branch1(-atan2f_(p.y, p.x), start);
-    if ((double)(o - start) > kPi && i < first) first = i;
+  constexpr int kP = 4;
+  for (int i0 = tid; i0 < S; i0 += kP * nt) {
+    float4 pp[kP];
+#pragma unroll
+    for (int u = 0; u < kP; ++u) pp[u] = i0 + u * nt < S ? seg[i0 + u * nt] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < kP; ++u) {
+      const int i = i0 + u * nt;
+      if (i >= S) continue;
+      const float o = ori_branch1(-atan2f_(pp[u].y, pp[u].x), start);
+      if ((double)(o - start) > kPi && i < first) first = i;
+    }
   }
   first = block_reduce_min(first, tmp);
-  for (int i = tid; i < S; i += nt) {
-    const float4 p = seg[i];
-    float o = -atan2f_(p.y, p.x);  // point.x = y, point.z = x (FA:573-577)
-    if (i <= first) {
-      o = ori_branch1(o, start);
-    } else {
-      o = (float)(o + 2 * kPi);
-      if ((double)o < (double)endo - kPi * 3 / 2) o = (float)(o + 2 * kPi);
-      else if ((double)o > (double)endo + kPi / 2) o = (float)(o - 2 * kPi);
-    }
-    const float relTime = (o - start) / diff;
-    const float inten = (float)(int)(p.w) + c.scan_period * relTime;
-    loam[i] = make_float4(p.y, p.z, p.x, inten);
-  }
   if (tid == 0) cnt[C_HALF] = first;
-  __syncthreads();
 
+  // Tiles of kTile points: the LOAM points (and the +-5 halo) are computed straight into LDS from
+  // the segmented cloud, written out once, and the curvature / occlusion pass reads them there.
   const float* rng = d.seg_range + base;
   const uint32_t* col = d.seg_col + base;
   uint8_t* picked = d.picked + base;
   int8_t* clabel = d.clabel + base;
   float* curv = d.curv + base;
   for (int t0 = 0; t0 < S; t0 += kTile) {
-    for (int q = tid; q < kTile + 10; q += nt) {
-      const int k = t0 - 5 + q;
-      tp[q] = (k >= 0 && k < S) ? loam[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int q0 = tid; q0 < kTile + 10; q0 += kP * nt) {
+      float4 pp[kP];
+#pragma unroll
+      for (int u = 0; u < kP; ++u) {
+        const int k = t0 - 5 + q0 + u * nt;
+        pp[u] = (q0 + u * nt < kTile + 10 && k >= 0 && k < S) ? seg[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < kP; ++u) {
+        const int q = q0 + u * nt, k = t0 - 5 + q;
+        if (q >= kTile + 10) continue;
+        if (k >= 0 && k < S) {
+          const float4 lp = loam_point(c, pp[u], k, first, start, endo, diff);
+          tp[q] = lp;
+          if (q >= 5 && q < kTile + 5) loam[k] = lp;
+        } else {
+          tp[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
     }
     for (int q = tid; q < kTile + 12; q += nt) {
       const int i = t0 - 6 + q;
@@ -93,12 +121,13 @@ __global__ __launch_bounds__(1024) void k_fa_points(DevCfg c, DevBufs d) {
       fl[q] = f;
     }
     __syncthreads();
-    const int k = t0 + tid;
-    if (tid < kTile && k < S) {
+    for (int q0 = tid; q0 < kTile; q0 += nt) {
+      const int k = t0 + q0;
+      if (k >= S) break;
       const bool inner = k >= 5 && k < S - 5;
       float cv = 0.0f;
       if (inner) {
-        const int q = tid + 5;
+        const int q = q0 + 5;
         float dx = 0.f, dy = 0.f, dz = 0.f;
 #pragma unroll
         for (int m = -5; m < 6; ++m) dx += tp[q + m].x;
@@ -115,7 +144,7 @@ __global__ __launch_bounds__(1024) void k_fa_points(DevCfg c, DevBufs d) {
       curv[k] = cv;
       // picked[k]: reset on [5, S-5) by the smoothness loop, then any occlusion write
       bool occ = false;
-      const int fq = k - t0 + 6;  // fl index of i = k
+      const int fq = q0 + 6;  // fl index of i = k
       if (fl[fq] & 4) occ = true;
 #pragma unroll
       for (int m = 0; m <= 5; ++m) occ |= (fl[fq + m] & 1) != 0;   // A_i, i in [k, k+5]

@@ -807,29 +807,52 @@ __global__ __launch_bounds__(1024) void k_segment(DevCfg c, const float4* __rest
     if (gv == 1 && (j % 5 != 0 && j > 5 && j < W - 5)) return 0;
     return 1;
   };
-  // row-major compaction in coalesced tiles of blockDim cells; one packed scan per tile
+  // row-major compaction in tiles of 4 * blockDim cells, 4 consecutive cells per lane (their loads
+  // and gathers all in flight together); one packed block scan of the lane totals per tile
+  constexpr int kC = 4;
   int baseS = 0, baseO = 0;
-  for (int t0 = 0; t0 < HW; t0 += nt) {
-    const int cell = t0 + tid;
-    const int k = cell < HW ? kind(cell) : 0;
+  for (int t0 = 0; t0 < HW; t0 += kC * nt) {
+    const int c0 = t0 + kC * tid;
+    int kk[kC];
+    int ns = 0, no = 0;
+#pragma unroll
+    for (int u = 0; u < kC; ++u) {
+      kk[u] = c0 + u < HW ? kind(c0 + u) : 0;
+      ns += kk[u] == 1;
+      no += kk[u] == 2;
+    }
+    float4 f[kC];
+    float rg[kC], vs[kC];
+#pragma unroll
+    for (int u = 0; u < kC; ++u) {
+      if (kk[u] == 0) continue;
+      f[u] = d.full[base + c0 + u];
+      vs[u] = d.vis[base + c0 + u];
+      rg[u] = kk[u] == 1 ? d.range[base + c0 + u] : 0.0f;
+    }
     int tot;
-    const int ex = block_excl_scan((k == 1 ? 1 : 0) | (k == 2 ? 1 << 16 : 0), tmp, &tot);
-    const int ps = baseS + (ex & 0xffff), po = baseO + (ex >> 16);
-    if (cell < HW) {
+    const int ex = block_excl_scan(ns | (no << 16), tmp, &tot);
+    int ps = baseS + (ex & 0xffff), po = baseO + (ex >> 16);
+#pragma unroll
+    for (int u = 0; u < kC; ++u) {
+      const int cell = c0 + u;
+      if (cell >= HW) break;
       const int i = cell / W, j = cell - i * W;
       if (j == 0) {
         d.start_ring[b * H + i] = ps - 1 + 5;
         if (i > 0) d.end_ring[b * H + i - 1] = ps - 1 - 5;
       }
-      if (k == 1) {
-        d.seg[base + ps] = d.full[base + cell];
+      if (kk[u] == 1) {
+        d.seg[base + ps] = f[u];
         d.seg_ground[base + ps] = g[cell] == 1;
         d.seg_col[base + ps] = (uint32_t)j;
-        d.seg_range[base + ps] = d.range[base + cell];
-        d.seg_int[base + ps] = d.vis[base + cell];
-      } else if (k == 2) {
-        d.outl[base + po] = d.full[base + cell];
-        d.outl_int[base + po] = d.vis[base + cell];
+        d.seg_range[base + ps] = rg[u];
+        d.seg_int[base + ps] = vs[u];
+        ++ps;
+      } else if (kk[u] == 2) {
+        d.outl[base + po] = f[u];
+        d.outl_int[base + po] = vs[u];
+        ++po;
       }
     }
     baseS += tot & 0xffff;
