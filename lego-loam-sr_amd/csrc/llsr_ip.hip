@@ -741,21 +741,32 @@ __global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
     }
   }
   __syncthreads();
-  // feasibility and rank of feasible seeds in row-major order (coalesced tiles)
+  // feasibility and rank of feasible seeds in row-major order: tiles of 4 consecutive cells per
+  // lane, one block scan of the lane counts per tile
+  constexpr int kC = 4;
   int rank = 0;
-  for (int t0 = 0; t0 < HW; t0 += nt) {
-    const int cell = t0 + tid;
-    bool root = false, feas = false;
-    if (cell < HW && lab[cell] == cell) {
-      root = true;
-      int size, lines;
-      if (kLds) { size = (unsigned)stat[cell] >> 16; lines = __popc(stat[cell] & 0xffff); }
-      else { size = stat[cell]; lines = __popcll(rowm[cell]); }
-      feas = size >= 30 || (size >= c.pointNum && lines >= c.lineNum);
+  for (int t0 = 0; t0 < HW; t0 += kC * nt) {
+    const int c0 = t0 + kC * tid;
+    bool root[kC], feas[kC];
+    int nf = 0;
+#pragma unroll
+    for (int u = 0; u < kC; ++u) {
+      const int cell = c0 + u;
+      root[u] = cell < HW && lab[cell] == cell;
+      feas[u] = false;
+      if (root[u]) {
+        int size, lines;
+        if (kLds) { size = (unsigned)stat[cell] >> 16; lines = __popc(stat[cell] & 0xffff); }
+        else { size = stat[cell]; lines = __popcll(rowm[cell]); }
+        feas[u] = size >= 30 || (size >= c.pointNum && lines >= c.lineNum);
+      }
+      nf += feas[u];
     }
     int tot;
-    const int ex = block_excl_scan(feas ? 1 : 0, tmp, &tot);  // barriers: all stat reads done
-    if (root) stat[cell] = feas ? rank + ex + 1 : 999999;
+    int ex = rank + block_excl_scan(nf, tmp, &tot);  // barriers: all stat reads done
+#pragma unroll
+    for (int u = 0; u < kC; ++u)
+      if (root[u]) stat[c0 + u] = feas[u] ? ++ex : 999999;
     rank += tot;
   }
   __syncthreads();
