@@ -145,26 +145,26 @@ LLSR_HD float atanf_(float x) {
   const float one = 1.0f, huge = 1.0e30f;
   int32_t hx = (int32_t)fbits(x);
   int32_t ix = hx & 0x7fffffff;
-  int id;
   if (ix >= 0x4c000000) {
     if (ix > 0x7f800000) return x + x;
     return hx > 0 ? atanhi3 + atanlo3 : -atanhi3 - atanlo3;
   }
-  if (ix < 0x3ee00000) {
-    if (ix < 0x31000000) {
-      if (huge + x > one) return x;
-    }
-    id = -1;
-  } else {
-    x = fabs_(x);
-    if (ix < 0x3f980000) {
-      if (ix < 0x3f300000) { id = 0; x = (2.0f * x - one) / (2.0f + x); }
-      else { id = 1; x = (x - one) / (x + one); }
-    } else {
-      if (ix < 0x401c0000) { id = 2; x = (x - 1.5f) / (one + 1.5f * x); }
-      else { id = 3; x = -1.0f / x; }
-    }
+  if (ix < 0x31000000) {
+    if (huge + x > one) return x;
   }
+  // The four reductions of fdlibm as ONE quotient (a |x| + b) / (c |x| + d) with per-range
+  // constants, so lanes of a wave in different ranges share one division instead of running up
+  // to four divergent ones. Each is the same float operation sequence as its branch:
+  //   id 0: (2|x| - 1) / (|x| + 2)     id 1: (|x| - 1) / (|x| + 1)
+  //   id 2: (|x| - 1.5) / (1.5|x| + 1) id 3: (0|x| - 1) / (|x| + 0) = -1 / |x|
+  // and id -1 keeps x: (1 x + 0) / (0 x + 1) = x exactly (x != 0 here).
+  const int id = ix < 0x3ee00000 ? -1 : ix < 0x3f300000 ? 0 : ix < 0x3f980000 ? 1 : ix < 0x401c0000 ? 2 : 3;
+  const float xin = id < 0 ? x : fabs_(x);
+  const float ca = id == 0 ? 2.0f : id == 3 ? 0.0f : one;
+  const float cb = id < 0 ? 0.0f : id == 2 ? -1.5f : -one;
+  const float cc = id < 0 ? 0.0f : id == 2 ? 1.5f : one;
+  const float cd = id < 0 ? one : id == 0 ? 2.0f : id == 3 ? 0.0f : one;
+  x = (ca * xin + cb) / (cc * xin + cd);
   float z = x * x;
   float w = z * z;
   float s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
