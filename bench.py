@@ -516,7 +516,7 @@ def main():
     ap.add_argument("--s2m-problems", type=int, default=256, help="scan-to-map problems per GPU per step")
     ap.add_argument("--s2m-steps", type=int, default=5)
     ap.add_argument("--s2m-modes", default="lm_applied,faithful", help="comma list; empty = skip the leg")
-    ap.add_argument("--odo", default="hdl64e:128,vlp16:1024",
+    ap.add_argument("--odo", default="hdl64e:512,vlp16:1024",
                     help="odometry legs lidar:sequences_per_gpu, comma list (empty = skip)")
     ap.add_argument("--map-keyframes", type=int, default=200,
                     help="local-map leg: keyframes in the store (0 = skip)")
