@@ -12,6 +12,7 @@
 
 #include "../../include/llsr.h"
 #include "llsr_device.h"
+#include "llsr_libm.h"
 #include "llsr_grid.h"
 #include "llsr_mo.h"
 #include "llsr_odo.h"
@@ -189,6 +190,9 @@ static void make_devcfg(const llsr_config& c, DevCfg& d) {
   d.RatioXY = c.RatioXY;
   d.RatioZ = c.RatioZ;
   d.DBFr = c.DBFr;
+  d.gnd_cos[0] = llsr_libm::ground_cos_threshold(12.5f);
+  d.gnd_cos[1] = llsr_libm::ground_cos_threshold(60.0f);
+  d.gnd_cos[2] = llsr_libm::ground_cos_threshold(25.0f);
   d.ccl_lds = (d.H <= 16 && d.HW <= 32768) ? 1 : 0;
   d.dbg_phase = 1 << 30;
 }

@@ -14,11 +14,93 @@ namespace llsr {
 
 using namespace llsr_libm;
 
-constexpr double kDegToRad = 3.14159265358979323846 / 180.0;  // utility.h:49
 constexpr double kPi = 3.14159265358979323846;
 
 __device__ __forceinline__ bool finite3(float4 p) {
   return __builtin_isfinite(p.x) && __builtin_isfinite(p.y) && __builtin_isfinite(p.z);
+}
+
+__device__ __forceinline__ int project_cell(const DevCfg& c, float4 p, float* range_out) {
+  const float range = sqrt_(p.x * p.x + p.y * p.y + p.z * p.z);
+  *range_out = range;
+  const float va = asinf_(p.z / range);
+  const int row = trunc_i32((double)((va + c.ip_angBottom) / c.ip_resY));
+  if (row < 0 || row >= c.H) return -1;
+  const float ha = atan2f_(p.x, p.y);
+  int col = trunc_i32(-round(((double)ha - kPi / 2) / (double)c.ip_resX) + c.W * 0.5);
+  if (col >= c.W) col -= c.W;
+  if (col < 0 || col >= c.W || (double)range < 0.1) return -1;
+  return col + row * c.W;
+}
+
+// Certified fast path for project_cell. The cell depends on asinf/atan2f only through a truncated
+// (row) and a rounded (column) quotient, both monotone in the angle, so an approximation with a
+// known error bound decides the cell exactly unless the quotient lies within that bound of a
+// decision boundary; only then (and for |z/r| >= 0.5, zero / non-finite operands) the lane takes
+// the exact libm path. Row: asinf_ below 0.5 IS the fdlibm odd polynomial (same ops as asinf_),
+// its quotient by res_Y becomes a multiply by the reciprocal (|err| <= 2^-22 |q|; margin
+// 1e-5 |q| + 1e-6 around every non-zero integer, trunc maps (-1, 1) to 0). Column: atan2 from a
+// hardware reciprocal (<= 1 ulp) and a degree-15 odd minimax polynomial (3.7e-8 on [0, 1]) plus
+// the octant fix-ups: |ha - atan2f_| < 1e-6 rad (measured < 6e-7, tests/test_libm.py); the double
+// quotient (ha - pi/2) / res_X becomes a float multiply (|err| <= 2^-22 |q| + 3e-7 / res_X), and
+// the margin 4e-6 / res_X + 2.4e-7 |q| around every half-integer covers both with 2-4x to spare.
+// Bit-exact by construction; tests/test_gpu_projection_edges.py puts points on the boundaries.
+__device__ __forceinline__ int project_cell_fast(const DevCfg& c, float4 p, float invResY, float invResX,
+                                                 bool* ok) {
+  const float range = sqrt_(p.x * p.x + p.y * p.y + p.z * p.z);
+  const float s = p.z / range;
+  const uint32_t is = fbits(s) & 0x7fffffffu;
+  bool good = is < 0x3f000000u;  // |s| < 0.5 (false for NaN)
+  const float p0 = 1.666675248e-1f, p1 = 7.495297643e-2f, p2 = 4.547037598e-2f,
+              p3 = 2.417951451e-2f, p4 = 4.216630880e-2f;
+  const float t2 = s * s;
+  const float w = t2 * (p0 + t2 * (p1 + t2 * (p2 + t2 * (p3 + t2 * p4))));
+  const float va = is < 0x32000000u ? s : s + s * w;
+  const float qr = (va + c.ip_angBottom) * invResY;
+  const float rr = __builtin_rintf(qr);
+  good = good && (rr == 0.0f || fabsf(qr - rr) > 1e-5f * fabsf(qr) + 1e-6f);
+  const int row = (int)__builtin_truncf(qr);
+  const float a = p.x, b = p.y;
+  const float ax = fabsf(a), bx = fabsf(b);
+  const float mx = fmaxf(ax, bx), mn = fminf(ax, bx);
+  good = good && mn > 0.0f && mx < 1e30f;
+  if (!good || row < 0 || row >= c.H) {
+    *ok = good;
+    return -1;
+  }
+  const float t = mn * __builtin_amdgcn_rcpf(mx);
+  const float u = t * t;
+  float pa = __builtin_fmaf(u, -0x1.09b84ap-8f, 0x1.6633d8p-6f);
+  pa = __builtin_fmaf(u, pa, -0x1.ca08a0p-5f);
+  pa = __builtin_fmaf(u, pa, 0x1.8af1c2p-4f);
+  pa = __builtin_fmaf(u, pa, -0x1.1cd946p-3f);
+  pa = __builtin_fmaf(u, pa, 0x1.988174p-3f);
+  pa = __builtin_fmaf(u, pa, -0x1.554c3ap-2f);
+  pa = __builtin_fmaf(u, pa, 0x1.ffffeap-1f);
+  float ha = pa * t;
+  ha = ax > bx ? 1.57079637f - ha : ha;
+  ha = b < 0.0f ? 3.14159274f - ha : ha;
+  ha = a < 0.0f ? -ha : ha;
+  const float qc = (ha - 1.57079637f) * invResX;
+  const float fl = __builtin_floorf(qc);
+  good = fabsf(qc - fl - 0.5f) > 4e-6f * invResX + 2.4e-7f * fabsf(qc);
+  *ok = good;
+  int col = trunc_i32(-(double)(fl + 1.0f) + c.W * 0.5);  // round(qc) = fl + (qc - fl > 0.5)
+  if (qc - fl < 0.5f) col = trunc_i32(-(double)fl + c.W * 0.5);
+  if (col >= c.W) col -= c.W;
+  if (col < 0 || col >= c.W || (double)range < 0.1) return -1;
+  return col + row * c.W;
+}
+
+// project_cell's result through the certified fast path, the exact libm path where it cannot decide
+__device__ __forceinline__ int project_cell_any(const DevCfg& c, float4 p, float invResY, float invResX) {
+  bool ok;
+  int cell = project_cell_fast(c, p, invResY, invResX, &ok);
+  if (!ok) {
+    float r;
+    cell = project_cell(c, p, &r);
+  }
+  return cell;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -39,16 +121,8 @@ __global__ __launch_bounds__(256) void k_project(DevCfg c, const float4* __restr
     const float4 p = pts[o0 + i];
     fin = finite3(p);
     if (fin) {
-      const float range = sqrt_(p.x * p.x + p.y * p.y + p.z * p.z);
-      const float va = asinf_(p.z / range);
-      const int row = trunc_i32((double)((va + c.ip_angBottom) / c.ip_resY));
-      if (row >= 0 && row < c.H) {
-        const float ha = atan2f_(p.x, p.y);
-        int col = trunc_i32(-round(((double)ha - kPi / 2) / (double)c.ip_resX) + c.W * 0.5);
-        if (col >= c.W) col -= c.W;
-        if (col >= 0 && col < c.W && !((double)range < 0.1))
-          atomicMax(&d.cell_pt[(size_t)b * c.HW + col + row * c.W], i);
-      }
+      const int cell = project_cell_any(c, p, 1.0f / c.ip_resY, 1.0f / c.ip_resX);
+      if (cell >= 0) atomicMax(&d.cell_pt[(size_t)b * c.HW + cell], i);
     }
   }
   const unsigned long long m = __ballot(fin);
@@ -107,12 +181,11 @@ __global__ __launch_bounds__(256) void k_gather_column(DevCfg c, const float4* _
       g = 1;
     } else {
       const float TVx = f.x - lx, TVy = f.y - ly, TVz = f.z - lz;
-      const float ang = (float)((double)acosf_((TVx * RVx + TVy * RVy + TVz * RVz) /
-                                               (sqrt_(TVx * TVx + TVy * TVy + TVz * TVz) *
-                                                sqrt_(RVx * RVx + RVy * RVy + RVz * RVz))) /
-                                kDegToRad);
-      const float D = c.use_kitti ? (i < 16 ? 60.0f : 25.0f) : 12.5f;
-      if (ang <= D) { RVx += TVx; RVy += TVy; RVz += TVz; g = 1; }
+      // (float)(acosf(x) / deg) <= D  <=>  gnd_cos(D) <= x <= 1  (llsr_libm.h ground_cos_threshold)
+      const float x = (TVx * RVx + TVy * RVy + TVz * RVz) /
+                      (sqrt_(TVx * TVx + TVy * TVy + TVz * TVz) * sqrt_(RVx * RVx + RVy * RVy + RVz * RVz));
+      const float xs = c.use_kitti ? (i < 16 ? c.gnd_cos[1] : c.gnd_cos[2]) : c.gnd_cos[0];
+      if (x >= xs && x <= 1.0f) { RVx += TVx; RVy += TVy; RVz += TVz; g = 1; }
       else g = 0;
       lx = f.x; ly = f.y; lz = f.z;
     }
@@ -131,19 +204,6 @@ __global__ __launch_bounds__(256) void k_gather_column(DevCfg c, const float4* _
 // values (IP:170-179); pass 3 runs the per-column ground test + Filter (IP:524-629) on the cell
 // arrays. No global atomics, no gather of scattered input points.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ int project_cell(const DevCfg& c, float4 p, float* range_out) {
-  const float range = sqrt_(p.x * p.x + p.y * p.y + p.z * p.z);
-  *range_out = range;
-  const float va = asinf_(p.z / range);
-  const int row = trunc_i32((double)((va + c.ip_angBottom) / c.ip_resY));
-  if (row < 0 || row >= c.H) return -1;
-  const float ha = atan2f_(p.x, p.y);
-  int col = trunc_i32(-round(((double)ha - kPi / 2) / (double)c.ip_resX) + c.W * 0.5);
-  if (col >= c.W) col -= c.W;
-  if (col < 0 || col >= c.W || (double)range < 0.1) return -1;
-  return col + row * c.W;
-}
-
 __device__ __forceinline__ void ground_column(const DevCfg& c, const float4* __restrict__ full, int8_t* ground,
                                               int j) {
   bool haveRV = false, obs = false;
@@ -172,12 +232,11 @@ __device__ __forceinline__ void ground_column(const DevCfg& c, const float4* __r
       g = 1;
     } else {
       const float TVx = f.x - lx, TVy = f.y - ly, TVz = f.z - lz;
-      const float ang = (float)((double)acosf_((TVx * RVx + TVy * RVy + TVz * RVz) /
-                                               (sqrt_(TVx * TVx + TVy * TVy + TVz * TVz) *
-                                                sqrt_(RVx * RVx + RVy * RVy + RVz * RVz))) /
-                                kDegToRad);
-      const float D = c.use_kitti ? (i < 16 ? 60.0f : 25.0f) : 12.5f;
-      if (ang <= D) { RVx += TVx; RVy += TVy; RVz += TVz; g = 1; }
+      // (float)(acosf(x) / deg) <= D  <=>  gnd_cos(D) <= x <= 1  (llsr_libm.h ground_cos_threshold)
+      const float x = (TVx * RVx + TVy * RVy + TVz * RVz) /
+                      (sqrt_(TVx * TVx + TVy * TVy + TVz * TVz) * sqrt_(RVx * RVx + RVy * RVy + RVz * RVz));
+      const float xs = c.use_kitti ? (i < 16 ? c.gnd_cos[1] : c.gnd_cos[2]) : c.gnd_cos[0];
+      if (x >= xs && x <= 1.0f) { RVx += TVx; RVy += TVy; RVz += TVz; g = 1; }
       else g = 0;
       lx = f.x; ly = f.y; lz = f.z;
     }
@@ -202,6 +261,7 @@ __global__ __launch_bounds__(1024) void k_project_fused(DevCfg c, const float4* 
   for (int q = tid; q < HW; q += nt) cidx[q] = -1;
   __syncthreads();
   int nfin = 0, first = INT_MAX, last = -1;
+  const float invResY = 1.0f / c.ip_resY, invResX = 1.0f / c.ip_resX;
   // four coalesced point loads in flight per lane before any of the projection math
   constexpr int kP = 4;
   for (int i0 = tid; i0 < n; i0 += kP * nt) {
@@ -218,8 +278,7 @@ __global__ __launch_bounds__(1024) void k_project_fused(DevCfg c, const float4* 
       ++nfin;
       first = i < first ? i : first;
       last = i;
-      float r;
-      const int cell = project_cell(c, pp[u], &r);
+      const int cell = project_cell_any(c, pp[u], invResY, invResX);
       if (cell >= 0) atomicMax(&cidx[cell], i);
     }
   }

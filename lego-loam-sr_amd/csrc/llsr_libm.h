@@ -375,4 +375,25 @@ LLSR_HD float cosf_(float y) {
   return (y - y) / (y - y);
 }
 
+// ---- groundRemovalOurs' angle test (imageProjection.cpp:555-566) as one comparison ----------
+// The reference keeps a cell as ground iff (float)(acosf(x) / (pi/180)) <= D, x = TV.RV/(|TV||RV|).
+// That predicate is monotone in x (acosf_ non-increasing on [-1, 1], NaN for |x| > 1 or NaN x),
+// so it equals  xs <= x <= 1  with xs = the smallest float it accepts; ground_cos_threshold finds
+// xs by bisection over the ordered float bits. oracle/libm_check ("gnd" rows) verifies the
+// equivalence over all 2^32 x for every D the reference uses (12.5, 25, 60 degrees).
+LLSR_HD float ground_angle_deg(float x) {
+  return (float)((double)acosf_(x) / (3.14159265358979323846 / 180.0));
+}
+LLSR_HD bool ground_angle_ok(float x, float D) { return ground_angle_deg(x) <= D; }
+LLSR_HD float ground_cos_threshold(float D) {
+  auto key2f = [](int32_t k) { return bitsf(k < 0 ? (0x80000000u | (uint32_t)(-k)) : (uint32_t)k); };
+  int32_t lo = -(int32_t)0x3f800000, hi = 0x3f800000;  // keys of -1 (rejected) and 1 (accepted)
+  while (hi - lo > 1) {
+    const int32_t mid = lo + (hi - lo) / 2;
+    if (ground_angle_ok(key2f(mid), D)) hi = mid;
+    else lo = mid;
+  }
+  return key2f(hi);
+}
+
 }  // namespace llsr_libm

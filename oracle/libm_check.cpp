@@ -86,6 +86,15 @@ int main(int argc, char** argv) {
     }
     failed += bad != 0;
   }
+  // ground angle test as a threshold on the cosine (llsr_libm.h ground_cos_threshold)
+  for (float D : {12.5f, 25.0f, 60.0f}) {
+    const float xs = ground_cos_threshold(D);
+    char name[16];
+    std::snprintf(name, sizeof name, "gnd%g", D);
+    failed += sweep(name, [xs](float x) { return (float)(x >= xs && x <= 1.0f); },
+                    [D](float x) { return (float)((float)((double)std::acos(x) / (M_PI / 180.0)) <= D); },
+                    0, ALL, stride, nthreads) != 0;
+  }
   std::printf("libm_check: %d function(s) with mismatches\n", failed);
   return failed;
 }

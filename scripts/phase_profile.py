@@ -24,6 +24,8 @@ pipe.process_batch(d_pts.data_ptr(), d_off.data_ptr(), B)
 res = {"kernels": pipe.kernel_times()}
 names = {3: "k_ground_add", 4: "k_ground_elev_ransac", 5: "k_label", 6: "k_segment", 7: "k_fa_points",
          8: "k_select_ring", 9: "k_fa_concat", 10: "k_dbscan_adj", 11: "k_dbscan_merge"}
-for k, phases in ((8, range(0, 8)),):
+names[1] = "k_project_fused"
+todo = [(int(k), range(int(n))) for k, n in (x.split(":") for x in os.environ.get("PHASES", "8:8").split(","))]
+for k, phases in todo:
     res[names[k]] = {p: round(pipe.debug_phase_ms(k, p, 5), 4) for p in phases}
 print(json.dumps(res))

@@ -1,11 +1,13 @@
 """GPU parity of the projection on points placed at the row / column decision boundaries.
 
-projectPointCloud (IP:305-336) truncates the float row quotient and rounds the double column
-quotient. The device evaluates both with a multiply by the reciprocal and falls back to the
-reference's division only when the quotient sits within a tolerance of an integer (row) or a
-half-integer (column) — this test puts thousands of points within a few ulp of those boundaries
-(and exactly on them, as far as float coordinates allow) and requires the cell of every point,
-the range image and the cell -> point map to be bit-identical to the oracle's exact divisions.
+projectPointCloud (IP:305-336) truncates the float row quotient of asinf and rounds the double
+column quotient of atan2f. The device decides both with a certified fast path (fdlibm's asinf
+polynomial, a minimax atan2 and reciprocal multiplies; csrc/llsr_ip.hip project_cell_fast) and
+falls back to the bit-exact libm ports and the reference's divisions only when a quotient sits
+within the path's error bound of an integer (row) or a half-integer (column). These tests put
+thousands of points within a few ulp of those boundaries (and exactly on them, as far as float
+coordinates allow), and at uniformly random directions, and require the cell of every point, the
+range image and the cell -> point map to be bit-identical to the oracle's exact libm projection.
 """
 import numpy as np
 import pytest
@@ -51,4 +53,29 @@ def test_projection_boundaries_bit_exact(lidar, require_gpu):
     assert np.array_equal(g["cell_point"], o["cell_point"])
     assert np.array_equal(g["range_image"].view(np.uint32), o["range_image"].view(np.uint32))
     assert not compare(g, o)
+    pipe.close()
+
+
+@pytest.mark.parametrize("lidar", ["vlp16", "hdl64e"])
+def test_projection_random_directions_bit_exact(lidar, require_gpu):
+    """Uniformly random directions (no bin-centred angles): every point's cell from the certified
+    fast path (or its exact fallback) equals the oracle's libm projection, incl. |z/r| >= 0.5,
+    points on the axes (x or y == 0) and ranges below the 0.1 m cut."""
+    cfg = default_config(lidar, 1024 if lidar == "hdl64e" else None)
+    rng = np.random.default_rng(21 if lidar == "vlp16" else 22)
+    n = 30000
+    v = rng.normal(size=(n, 3))
+    v[:, 2] *= 0.3
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    R = np.exp(rng.uniform(np.log(0.05), np.log(80.0), n))
+    pts = np.zeros((n, 4), np.float32)
+    pts[:, :3] = v * R[:, None]
+    pts[:200, 0] = 0.0   # on the axes: the fast path defers these to the exact atan2f
+    pts[200:400, 1] = 0.0
+    pts[:, 3] = rng.integers(0, 100, n)
+    pipe = Pipeline(cfg, max_batch=1, max_points=n)
+    g = pipe.process_scan(pts)
+    o = oracle_py.Oracle(cfg).process(pts)
+    assert np.array_equal(g["cell_point"], o["cell_point"])
+    assert np.array_equal(g["range_image"].view(np.uint32), o["range_image"].view(np.uint32))
     pipe.close()
