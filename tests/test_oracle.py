@@ -196,3 +196,14 @@ def test_add_automaton_scan_matches_serial():
             g = rng.choice(np.array([-1, 0, 1, 2]), size=W, p=[0.1, 0.2, 0.3, 0.4])
             cF, cB = rng.random(W) < 0.7, rng.random(W) < 0.7
             assert np.array_equal(_add_scan(g, cF, cB), _add_serial(g, cF, cB))
+
+
+def test_cell_intensity_multiply_equals_division():
+    """k_project_fused writes full_cloud's intensity (float)(row + (double)col / 10000.0)
+    (IP:339) as (float)(row + col * 1e-4) when H <= 256 and W <= 8192: the doubles differ for
+    some columns but the rounded floats agree for every (row, col) in that domain."""
+    r = np.arange(256, dtype=np.float64)[:, None]
+    c = np.arange(8192, dtype=np.float64)[None, :]
+    a = (r + c / 10000.0).astype(np.float32)
+    b = (r + c * 1e-4).astype(np.float32)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
