@@ -59,9 +59,13 @@ __global__ __launch_bounds__(512) void k_fa_points(DevCfg c, DevBufs d) {
   const float4* seg = d.seg + base;
   float4* loam = d.loam + base;
 
+  // The latch index is the smallest i whose test passes, so the scan stops after the first chunk
+  // of kP * nt points that holds one (normally inside ring 0, half a turn in): later chunks only
+  // hold larger indices. Typical cost: one chunk of orientations instead of all S.
   int first = INT_MAX;
   constexpr int kP = 4;
-  for (int i0 = tid; i0 < S; i0 += kP * nt) {
+  for (int c0 = 0; c0 < S; c0 += kP * nt) {
+    const int i0 = c0 + tid;
     float4 pp[kP];
 #pragma unroll
     for (int u = 0; u < kP; ++u) pp[u] = i0 + u * nt < S ? seg[i0 + u * nt] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -72,8 +76,9 @@ __global__ __launch_bounds__(512) void k_fa_points(DevCfg c, DevBufs d) {
       const float o = ori_branch1(-atan2f_(pp[u].y, pp[u].x), start);
       if ((double)(o - start) > kPi && i < first) first = i;
     }
+    first = block_reduce_min(first, tmp);
+    if (first != INT_MAX) break;
   }
-  first = block_reduce_min(first, tmp);
   if (tid == 0) cnt[C_HALF] = first;
 
   // Tiles of kTile points: the LOAM points (and the +-5 halo) are computed straight into LDS from
