@@ -517,6 +517,7 @@ __device__ __forceinline__ float ransac_dist(const float cf[4], float4 q) {
 __global__ __launch_bounds__(1024) void k_ground_elev_ransac(DevCfg c, DevBufs d) {
   __shared__ float colz[2048];
   __shared__ int colok[2048];
+  __shared__ uint64_t colm2[2048];  // per column: rows with ground == 2 (H <= 64)
   __shared__ int tmp[32];
   __shared__ MT rng;
   __shared__ int sh_int[8];
@@ -529,13 +530,24 @@ __global__ __launch_bounds__(1024) void k_ground_elev_ransac(DevCfg c, DevBufs d
   const int tid = threadIdx.x, nt = blockDim.x;
 
   // ---- ELEVATION: per-column ground count and top ground z (IP:676-687) ----
+  // The column's ground bytes are loaded 16 rows at a time (all in flight), reduced to bit masks;
+  // only the top ground cell's z is fetched, and the cells == 2 are remembered for the Filter pass.
   for (int j = tid; j < W; j += nt) {
-    int cnt = 0;
-    float zt = 0.0f;
-    for (int i = 0; i < H; ++i)
-      if (g[j + i * W] == 1) { ++cnt; zt = full[j + i * W].z; }
-    colz[j] = zt;
+    uint64_t m1 = 0ull, m2 = 0ull;
+    for (int i0 = 0; i0 < H; i0 += 16) {
+      int8_t gv[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) gv[u] = i0 + u < H ? g[j + (i0 + u) * W] : (int8_t)0;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        m1 |= (uint64_t)(gv[u] == 1) << (i0 + u);
+        m2 |= (uint64_t)(gv[u] == 2) << (i0 + u);
+      }
+    }
+    const int cnt = __popcll(m1);
+    colz[j] = m1 ? full[j + (63 - __clzll((long long)m1)) * W].z : 0.0f;
     colok[j] = cnt >= 5 ? j : -1;
+    colm2[j] = m2;
   }
   __syncthreads();
   // last-valid carry across columns: max-scan of colok (block-sequential chunks of 2)
@@ -567,31 +579,47 @@ __global__ __launch_bounds__(1024) void k_ground_elev_ransac(DevCfg c, DevBufs d
   __syncthreads();
   for (int j = tid; j < W; j += nt) {
     const float EH = colok[j] >= 0 ? colz[colok[j]] : -1.3f;
-    for (int i = 0; i < H; ++i) {
-      const int cell = j + i * W;
-      if (g[cell] == 2) g[cell] = ((double)full[cell].z < (double)EH + 0.3) ? 1 : 0;
+    const uint64_t m2 = colm2[j];
+    for (int i0 = 0; i0 < H && (m2 >> i0); i0 += 16) {
+      float z[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) z[u] = (m2 >> (i0 + u)) & 1ull ? full[j + (i0 + u) * W].z : 0.0f;
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if ((m2 >> (i0 + u)) & 1ull) g[j + (i0 + u) * W] = ((double)z[u] < (double)EH + 0.3) ? 1 : 0;
     }
   }
   __syncthreads();
 
   // ---- NEAR (IP:701-715): row-major compaction, intensity = linear index ----
+  // 4 consecutive cells per lane per tile (loads in flight together, one block scan per tile).
   float4* nearp = d.near_pts + base;
   int K = 0;
-  for (int t0 = 0; t0 < HW; t0 += nt) {
-    const int cell = t0 + tid;
-    bool nearc = false;
-    float depth = 0.f;
-    if (cell < HW && g[cell] == 1) {
-      const float4 p = full[cell];
-      depth = sqrt_(p.x * p.x + p.y * p.y);
-      nearc = (double)depth <= 10;
+  constexpr int kC = 4;
+  for (int t0 = 0; t0 < HW; t0 += kC * nt) {
+    const int c0 = t0 + kC * tid;
+    int8_t gv[kC];
+#pragma unroll
+    for (int u = 0; u < kC; ++u) gv[u] = c0 + u < HW ? g[c0 + u] : (int8_t)0;
+    float4 p[kC];
+#pragma unroll
+    for (int u = 0; u < kC; ++u) p[u] = gv[u] == 1 ? full[c0 + u] : make_float4(0.f, 0.f, 0.f, 0.f);
+    bool nearc[kC];
+    float depth[kC];
+    int nn = 0;
+#pragma unroll
+    for (int u = 0; u < kC; ++u) {
+      depth[u] = sqrt_(p[u].x * p[u].x + p[u].y * p[u].y);
+      nearc[u] = gv[u] == 1 && (double)depth[u] <= 10;
+      nn += nearc[u];
     }
     int tot;
-    const int ex = block_excl_scan(nearc ? 1 : 0, tmp, &tot);
-    if (nearc) {
-      const float4 p = full[cell];
-      nearp[K + ex] = make_float4(p.x, p.y, p.z, (float)cell);
-      if ((double)depth <= 5) g[cell] = 0;
+    int pos = K + block_excl_scan(nn, tmp, &tot);
+#pragma unroll
+    for (int u = 0; u < kC; ++u) {
+      if (!nearc[u]) continue;
+      nearp[pos++] = make_float4(p[u].x, p[u].y, p[u].z, (float)(c0 + u));
+      if ((double)depth[u] <= 5) g[c0 + u] = 0;
     }
     K += tot;
   }
@@ -885,26 +913,39 @@ __global__ __launch_bounds__(1024) void k_segment(DevCfg c, const float4* __rest
     d.orient[b * 4 + 2] = o2;
   }
   // 0 = skip, 1 = segmented, 2 = outlier
-  auto kind = [&](int cell) -> int {
+  auto kind = [&](int cell, int L, int8_t gv) -> int {
     const int i = cell / W, j = cell - i * W;
-    const int L = lab[cell];
-    const int8_t gv = g[cell];
     if (!(L > 0 || gv == 1)) return 0;
     if (L == 999999) return (i > c.gsi && j % 5 == 0) ? 2 : 0;
     if (gv == 1 && (j % 5 != 0 && j > 5 && j < W - 5)) return 0;
     return 1;
   };
   // row-major compaction in tiles of 4 * blockDim cells, 4 consecutive cells per lane (their loads
-  // and gathers all in flight together); one packed block scan of the lane totals per tile
+  // and gathers all in flight together); one packed block scan of the lane totals per tile. The
+  // label / ground loads of the next tile are issued before this tile's scan, so a tile pays one
+  // exposed memory round trip (its gathers) instead of two.
   constexpr int kC = 4;
   int baseS = 0, baseO = 0;
+  int labn[kC];
+  int8_t gn[kC];
+  auto load_kind = [&](int t0) {
+    const int c0 = t0 + kC * tid;
+#pragma unroll
+    for (int u = 0; u < kC; ++u) {
+      labn[u] = c0 + u < HW ? lab[c0 + u] : 0;
+      gn[u] = c0 + u < HW ? g[c0 + u] : (int8_t)0;
+    }
+  };
+  load_kind(0);
   for (int t0 = 0; t0 < HW; t0 += kC * nt) {
     const int c0 = t0 + kC * tid;
     int kk[kC];
+    int8_t gc[kC];
     int ns = 0, no = 0;
 #pragma unroll
     for (int u = 0; u < kC; ++u) {
-      kk[u] = c0 + u < HW ? kind(c0 + u) : 0;
+      gc[u] = gn[u];
+      kk[u] = c0 + u < HW ? kind(c0 + u, labn[u], gn[u]) : 0;
       ns += kk[u] == 1;
       no += kk[u] == 2;
     }
@@ -917,6 +958,7 @@ __global__ __launch_bounds__(1024) void k_segment(DevCfg c, const float4* __rest
       vs[u] = d.vis[base + c0 + u];
       rg[u] = kk[u] == 1 ? d.range[base + c0 + u] : 0.0f;
     }
+    if (t0 + kC * nt < HW) load_kind(t0 + kC * nt);
     int tot;
     const int ex = block_excl_scan(ns | (no << 16), tmp, &tot);
     int ps = baseS + (ex & 0xffff), po = baseO + (ex >> 16);
@@ -931,7 +973,7 @@ __global__ __launch_bounds__(1024) void k_segment(DevCfg c, const float4* __rest
       }
       if (kk[u] == 1) {
         d.seg[base + ps] = f[u];
-        d.seg_ground[base + ps] = g[cell] == 1;
+        d.seg_ground[base + ps] = gc[u] == 1;
         d.seg_col[base + ps] = (uint32_t)j;
         d.seg_range[base + ps] = rg[u];
         d.seg_int[base + ps] = vs[u];
