@@ -193,7 +193,7 @@ static void make_devcfg(const llsr_config& c, DevCfg& d) {
   d.gnd_cos[0] = llsr_libm::ground_cos_threshold(12.5f);
   d.gnd_cos[1] = llsr_libm::ground_cos_threshold(60.0f);
   d.gnd_cos[2] = llsr_libm::ground_cos_threshold(25.0f);
-  d.ccl_lds = (d.H <= 16 && d.HW <= 32768) ? 1 : 0;
+  d.ccl_lds = (d.H <= 16 && d.HW <= 32000) ? 1 : 0;
   d.dbg_phase = 1 << 30;
 }
 

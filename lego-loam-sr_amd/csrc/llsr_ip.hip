@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void k_gather_column(DevCfg c, const float4* _
 }
 
 // ---------------------------------------------------------------------------------------------
-// K1+K2 fused for range images that fit LDS (H*W <= 32768, e.g. VLP-16): one workgroup per scan.
+// K1+K2 fused for range images that fit LDS (H <= 16, H*W <= 32000, e.g. VLP-16): one workgroup per scan.
 // Pass 1 projects every raw point (coalesced reads) and resolves IP:337-347's serial "last writer
 // wins" with an LDS atomicMax of the raw index per cell; pass 2 re-reads the points and only each
 // cell's winner writes range / full_cloud / raw intensity; empty cells get the resetParameters
@@ -817,6 +817,57 @@ __global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
     }
   }
   __syncthreads();
+  if constexpr (kLds) {
+    // Everything stays in the LDS word of each cell: -1 = not label 0; a member holds its root's
+    // index (>= 0); a root holds 0x80000000 | size << 16 | row mask of its pushed members (size <=
+    // HW <= 32000 keeps the word != -1), later 0x80000000 | label. Global memory sees the labels once.
+    // read-only walks: the only stores are P[cell] = its root, so every word a concurrent walk
+    // reads is still an ancestor (path halving here could store a stale grandparent over a root)
+    for (int cell = tid; cell < HW; cell += nt) {
+      int x = P.ld(cell);
+      if (x < 0) continue;
+      for (int px = P.ld(x); px != x; px = P.ld(x)) x = px;
+      P.st(cell, x);
+    }
+    __syncthreads();
+    for (int cell = tid; cell < HW; cell += nt)
+      if (P.ld(cell) == cell) P.st(cell, (int)(0x80000000u | (1u << 16)));
+    __syncthreads();
+    for (int cell = tid; cell < HW; cell += nt) {
+      const int root = P.ld(cell);
+      if (root < 0) continue;
+      atomicAdd(&lds_parent[root], 1 << 16);
+      atomicOr(&lds_parent[root], 1 << (cell / W));
+    }
+    __syncthreads();
+    constexpr int kC = 4;
+    int rank = 0;
+    for (int t0 = 0; t0 < HW; t0 += kC * nt) {
+      const int c0 = t0 + kC * tid;
+      bool root[kC], feas[kC];
+      int nf = 0;
+#pragma unroll
+      for (int u = 0; u < kC; ++u) {
+        const int v = c0 + u < HW ? P.ld(c0 + u) : -1;
+        root[u] = v < 0 && v != -1;
+        const int size = (int)(((unsigned)v >> 16) & 0x7fffu), lines = __popc((unsigned)v & 0xffffu);
+        feas[u] = root[u] && (size >= 30 || (size >= c.pointNum && lines >= c.lineNum));
+        nf += feas[u];
+      }
+      int tot;
+      int ex = rank + block_excl_scan(nf, tmp, &tot);  // barriers: all root words read
+#pragma unroll
+      for (int u = 0; u < kC; ++u)
+        if (root[u]) P.st(c0 + u, (int)(0x80000000u | (unsigned)(feas[u] ? ++ex : 999999)));
+      rank += tot;
+    }
+    __syncthreads();
+    for (int cell = tid; cell < HW; cell += nt) {
+      const int v = P.ld(cell);
+      lab[cell] = v == -1 ? -1 : v < 0 ? (v & 0x7fffffff) : (P.ld(v) & 0x7fffffff);
+    }
+    return;
+  }
   // flatten: root per cell -> lab (temporarily), -1 for non-label-0 cells
   for (int cell = tid; cell < HW; cell += nt) {
     const int p = P.ld(cell);
