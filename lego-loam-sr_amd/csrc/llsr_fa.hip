@@ -273,12 +273,35 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   const int ws = sp - 5 > 0 ? sp - 5 : 0;
   const int we = ep + 5 < HW - 1 ? ep + 5 : HW - 1;
   const int wn = we - ws + 1;
-  for (int t = tid; t < wn; t += nt) {
-    const int pos = ws + t;
-    wpick[t] = d.picked[base + pos];
-    wgnd[t] = d.seg_ground[base + pos];
-    wlab[t] = d.clabel[base + pos];
-    wcol[t] = (uint16_t)d.seg_col[base + pos];
+  // the whole window (and its curvatures, kept in registers for both candidate passes) is loaded
+  // in one round trip: kPer positions per lane, all loads in flight together (blockDim.x == 256)
+  constexpr int kPer = (kWin + 255) / 256;
+  float cvr[kPer];
+  {
+    uint8_t pk[kPer], gd[kPer];
+    int8_t lb[kPer];
+    uint32_t cl[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int t = tid + u * 256, pos = ws + t;
+      if (t < wn) {
+        pk[u] = d.picked[base + pos];
+        gd[u] = d.seg_ground[base + pos];
+        lb[u] = d.clabel[base + pos];
+        cl[u] = d.seg_col[base + pos];
+        cvr[u] = curv[pos];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int t = tid + u * 256;
+      if (t < wn) {
+        wpick[t] = pk[u];
+        wgnd[t] = gd[u];
+        wlab[t] = lb[u];
+        wcol[t] = (uint16_t)cl[u];
+      }
+    }
   }
   if (tid == 0) s_cnt = 0;
   __syncthreads();
@@ -300,9 +323,12 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   }
   __syncthreads();
   // ---- edges: statically eligible sorted-part entries, visited in descending key order ----
-  for (int p = sp + tid; p < ep; p += nt) {
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int p = ws + tid + u * 256;
+    if (p < sp || p >= ep) continue;
     const int ind = p == 4 ? 0 : p;
-    const float v = p == 4 ? 0.0f : curv[p];
+    const float v = p == 4 ? 0.0f : cvr[u];
     const int w = ind - ws;
     if (wpick[w] == 0 && v > c.edge_thr && wgnd[w] == 0)
       key[atomicAdd(&s_cnt, 1)] = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)ind;
@@ -326,9 +352,12 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   __syncthreads();
   if (c.dbg_phase <= 2) return;
   // ---- flats: ascending key order, entry ep last ----
-  for (int p = sp + tid; p < ep; p += nt) {
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int p = ws + tid + u * 256;
+    if (p < sp || p >= ep) continue;
     const int ind = p == 4 ? 0 : p;
-    const float v = p == 4 ? 0.0f : curv[p];
+    const float v = p == 4 ? 0.0f : cvr[u];
     const int w = ind - ws;
     if (wpick[w] == 0 && v < c.surf_thr && wgnd[w] == 1)
       key[atomicAdd(&s_cnt, 1)] = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)ind;
@@ -366,9 +395,17 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   if (c.dbg_phase <= 4) return;
   const float4* lp = d.loam + base + sp;
   // ---- VoxelGrid(0.2) applyFilter (PCL 1.10), centroids summed in (voxel, input) order ----
+  // each lane's candidates (t = tid + 256 u, L <= 2048) are gathered once, for the bounds and the keys
+  constexpr int kLp = kRingMax / 256;
+  float4 lpr[kLp];
   float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-  for (int t = tid; t < L; t += nt) {
-    const float4 p = lp[cpos[t]];
+#pragma unroll
+  for (int u = 0; u < kLp; ++u)
+    if (tid + u * 256 < L) lpr[u] = lp[cpos[tid + u * 256]];
+#pragma unroll
+  for (int u = 0; u < kLp; ++u) {
+    if (tid + u * 256 >= L) continue;
+    const float4 p = lpr[u];
     mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
     mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
   }
@@ -401,8 +438,11 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   const int mul1 = div[0], mul2 = div[0] * div[1];
   // voxel id of every candidate, in ring order (points of one voxel are mostly consecutive)
   uint32_t* vk = win_raw;  // the window arrays are dead (barrier after the compaction above)
-  for (int t = tid; t < L; t += nt) {
-    const float4 p = lp[cpos[t]];
+#pragma unroll
+  for (int u = 0; u < kLp; ++u) {
+    const int t = tid + u * 256;
+    if (t >= L) continue;
+    const float4 p = lpr[u];
     const int i0 = (int)(floorf(p.x * inv) - (float)minb[0]);
     const int i1 = (int)(floorf(p.y * inv) - (float)minb[1]);
     const int i2 = (int)(floorf(p.z * inv) - (float)minb[2]);
