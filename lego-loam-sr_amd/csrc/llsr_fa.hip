@@ -273,6 +273,7 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   const int ws = sp - 5 > 0 ? sp - 5 : 0;
   const int we = ep + 5 < HW - 1 ? ep + 5 : HW - 1;
   const int wn = we - ws + 1;
+  if (c.dbg_phase <= -2) return;
   // the whole window (and its curvatures, kept in registers for both candidate passes) is loaded
   // in one round trip: kPer positions per lane, all loads in flight together (blockDim.x == 256)
   constexpr int kPer = (kWin + 255) / 256;
@@ -305,33 +306,54 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   }
   if (tid == 0) s_cnt = 0;
   __syncthreads();
+  if (c.dbg_phase <= -1) return;
   // Marking from `ind` runs forward while consecutive column gaps stay <= 10 (at most 5 steps,
   // stopping at H*W) and likewise backward (stopping at 0). Column indices are static, so the
-  // reach of every selectable position is computed in parallel up front.
-  for (int t = tid; t < wn; t += nt) {
-    const int ind = ws + t;
-    int f = 0, bk = 0;
-    for (int l = 1; l <= 5 && ind + l < HW && ind + l - ws < wn; ++l) {
-      if (abs((int)wcol[ind + l - ws] - (int)wcol[ind + l - 1 - ws]) > 10) break;
-      f = l;
+  // reach of every selectable position is computed up front: one bit per window position marks a
+  // stop between t and t + 1 (a gap > 10 or the window end, which also bounds H*W), and the
+  // forward / backward reach is the distance to the nearest stop bit (ctz / clz of 64 bits).
+  {
+    uint64_t* gbits = reinterpret_cast<uint64_t*>(key);  // key[] is free until the edge candidates
+    const int l = lane_id();
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int t = tid + u * 256;
+      const bool stop = t + 1 >= wn || abs((int)wcol[t + 1] - (int)wcol[t]) > 10;
+      const uint64_t m = __ballot(t < wn && stop);
+      if (l == 0 && (t >> 6) <= (wn >> 6)) gbits[t >> 6] = m;
     }
-    for (int l = 1; l <= 5 && ind - l >= 0 && ind - l >= ws; ++l) {
-      if (abs((int)wcol[ind - l - ws] - (int)wcol[ind - l + 1 - ws]) > 10) break;
-      bk = l;
+    __syncthreads();
+    const int nw = (wn >> 6) + 1;
+    for (int t = tid; t < wn; t += nt) {
+      const int k = t >> 6, sh = t & 63;
+      uint64_t fw = gbits[k] >> sh;
+      if (sh && k + 1 < nw) fw |= gbits[k + 1] << (64 - sh);
+      const int f = fw ? min(5, __ffsll((long long)fw) - 1) : 5;
+      int bk = 0;
+      if (t > 0) {
+        const int q = t - 1, kq = q >> 6, s2 = q & 63;
+        uint64_t bw = gbits[kq] << (63 - s2);
+        if (s2 < 63 && kq > 0) bw |= gbits[kq - 1] >> (s2 + 1);
+        bk = min(min(5, t), bw ? (int)__clzll((long long)bw) : 64);
+      }
+      wreach[t] = (uint8_t)(f | (bk << 4));
     }
-    wreach[t] = (uint8_t)(f | (bk << 4));
   }
   __syncthreads();
   // ---- edges: statically eligible sorted-part entries, visited in descending key order ----
 #pragma unroll
-  for (int u = 0; u < kPer; ++u) {
+  for (int u = 0; u < kPer; ++u) {  // wave-aggregated append: one LDS atomic per wave
     const int p = ws + tid + u * 256;
-    if (p < sp || p >= ep) continue;
+    const bool in = p >= sp && p < ep;
     const int ind = p == 4 ? 0 : p;
     const float v = p == 4 ? 0.0f : cvr[u];
-    const int w = ind - ws;
-    if (wpick[w] == 0 && v > c.edge_thr && wgnd[w] == 0)
-      key[atomicAdd(&s_cnt, 1)] = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)ind;
+    const int w = in ? ind - ws : 0;
+    const bool e = in && wpick[w] == 0 && v > c.edge_thr && wgnd[w] == 0;
+    const unsigned long long m = __ballot(e);
+    int wb = 0;
+    if (lane_id() == 0 && m) wb = atomicAdd(&s_cnt, (int)__popcll(m));
+    wb = __shfl(wb, 0, 64);
+    if (e) key[wb + __popcll(m & ((1ull << lane_id()) - 1ull))] = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)ind;
   }
   __syncthreads();
   if (c.dbg_phase <= 0) return;
@@ -353,14 +375,18 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   if (c.dbg_phase <= 2) return;
   // ---- flats: ascending key order, entry ep last ----
 #pragma unroll
-  for (int u = 0; u < kPer; ++u) {
+  for (int u = 0; u < kPer; ++u) {  // wave-aggregated append: one LDS atomic per wave
     const int p = ws + tid + u * 256;
-    if (p < sp || p >= ep) continue;
+    const bool in = p >= sp && p < ep;
     const int ind = p == 4 ? 0 : p;
     const float v = p == 4 ? 0.0f : cvr[u];
-    const int w = ind - ws;
-    if (wpick[w] == 0 && v < c.surf_thr && wgnd[w] == 1)
-      key[atomicAdd(&s_cnt, 1)] = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)ind;
+    const int w = in ? ind - ws : 0;
+    const bool e = in && wpick[w] == 0 && v < c.surf_thr && wgnd[w] == 1;
+    const unsigned long long m = __ballot(e);
+    int wb = 0;
+    if (lane_id() == 0 && m) wb = atomicAdd(&s_cnt, (int)__popcll(m));
+    wb = __shfl(wb, 0, 64);
+    if (e) key[wb + __popcll(m & ((1ull << lane_id()) - 1ull))] = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)ind;
   }
   __syncthreads();
   const int nF = s_cnt;

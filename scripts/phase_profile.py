@@ -25,7 +25,10 @@ res = {"kernels": pipe.kernel_times()}
 names = {3: "k_ground_add", 4: "k_ground_elev_ransac", 5: "k_label", 6: "k_segment", 7: "k_fa_points",
          8: "k_select_ring", 9: "k_fa_concat", 10: "k_dbscan_adj", 11: "k_dbscan_merge"}
 names[1] = "k_project_fused"
-todo = [(int(k), range(int(n))) for k, n in (x.split(":") for x in os.environ.get("PHASES", "8:8").split(","))]
+todo = []
+for x in os.environ.get("PHASES", "8:8").split(","):  # "k:n" = phases 0..n-1, "k:a:b" = a..b-1
+    f = [int(v) for v in x.split(":")]
+    todo.append((f[0], range(f[1]) if len(f) == 2 else range(f[1], f[2])))
 for k, phases in todo:
     res[names[k]] = {p: round(pipe.debug_phase_ms(k, p, 5), 4) for p in phases}
 print(json.dumps(res))
