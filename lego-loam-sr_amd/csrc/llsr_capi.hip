@@ -204,6 +204,18 @@ static T* carve(char*& p, size_t n) {
   return r;
 }
 
+// boost::mt19937 seeded with 12345 (PCL 1.10 SampleConsensusModel's rng_alg_, IP:716-721), state
+// after the seeding recurrence and the first twist: every scan's RANSAC starts its draws here, so
+// the device loads 624 words instead of running 1248 serial steps on one lane per scan.
+static void mt_first_state(uint32_t* m) {
+  m[0] = 12345u;
+  for (int k = 1; k < 624; ++k) m[k] = 1812433253u * (m[k - 1] ^ (m[k - 1] >> 30)) + (uint32_t)k;
+  for (int k = 0; k < 624; ++k) {
+    const uint32_t y = (m[k] & 0x80000000u) | (m[(k + 1) % 624] & 0x7fffffffu);
+    m[k] = m[(k + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+  }
+}
+
 static size_t layout(DevBufs& d, char* p0, int B, int H, int HW) {
   char* p = p0;
   const size_t n = (size_t)B * HW;
@@ -244,6 +256,7 @@ static size_t layout(DevBufs& d, char* p0, int B, int H, int HW) {
   d.db_pts = carve<float4>(p, n);
   d.db_kz = carve<float>(p, n);
   d.db_adj = carve<uint32_t>(p, (size_t)B * kAdjCap * kAdjWords);
+  d.mt0 = carve<uint32_t>(p, 624);
   return (size_t)(p - p0);
 }
 
@@ -270,6 +283,14 @@ extern "C" int32_t llsr_create(const llsr_config* cfg, int32_t hip_device, int32
   if (hipMalloc(&h->pool, bytes) != hipSuccess) { delete h; return LLSR_ENOMEM; }
   h->pool_bytes = bytes;
   layout(h->d, (char*)h->pool, max_batch, h->dc.H, h->dc.HW);
+  {
+    uint32_t mt0[624];
+    mt_first_state(mt0);
+    if (hipMemcpy(h->d.mt0, mt0, sizeof(mt0), hipMemcpyHostToDevice) != hipSuccess) {
+      llsr_destroy(h);
+      return LLSR_ENODEV;
+    }
+  }
   if (hipMalloc(&h->d_in, sizeof(float4) * (size_t)max_points) != hipSuccess ||
       hipMalloc(&h->d_off, sizeof(int64_t) * 2) != hipSuccess ||
       hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {

@@ -77,6 +77,7 @@ struct DevBufs {
   float4* db_pts;       // [B][HW] DBSCAN point records: (x0, y0, z0, kxy)
   float* db_kz;         // [B][HW]
   uint32_t* db_adj;     // [B][kAdjCap][kAdjWords] eps-neighbourhood bitmask rows
+  uint32_t* mt0;        // [624] RANSAC's mt19937 state after seed(12345) and its first twist
 };
 
 // DBSCAN adjacency capacity per scan (edge candidates); larger M falls back to on-the-fly rows.

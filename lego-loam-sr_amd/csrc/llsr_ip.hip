@@ -483,11 +483,6 @@ struct MT {
   uint32_t mt[624];
   int idx;
 };
-__device__ void mt_seed(MT& m, uint32_t s) {
-  m.mt[0] = s;
-  for (int k = 1; k < 624; ++k) m.mt[k] = 1812433253u * (m.mt[k - 1] ^ (m.mt[k - 1] >> 30)) + (uint32_t)k;
-  m.idx = 624;
-}
 __device__ uint32_t mt_next(MT& m) {
   if (m.idx >= 624) {
     for (int k = 0; k < 624; ++k) {
@@ -591,6 +586,7 @@ __global__ __launch_bounds__(1024) void k_ground_elev_ransac(DevCfg c, DevBufs d
   }
   __syncthreads();
 
+  if (c.dbg_phase <= 0) return;
   // ---- NEAR (IP:701-715): row-major compaction, intensity = linear index ----
   // 4 consecutive cells per lane per tile (loads in flight together, one block scan per tile).
   float4* nearp = d.near_pts + base;
@@ -626,12 +622,14 @@ __global__ __launch_bounds__(1024) void k_ground_elev_ransac(DevCfg c, DevBufs d
   int* shuf = d.shuf + base;
   for (int k = tid; k < K; k += nt) shuf[k] = k;
   __syncthreads();
+  if (c.dbg_phase <= 1) return;
 
   // ---- RANSAC (PCL 1.10 RandomSampleConsensus::computeModel, threshold 0.5) ----
   // sh_int: 0 stop, 1 valid-model, 2 iterations, 3 best count, 4 skipped, 5 have-best
   __shared__ double kk;
+  for (int k = tid; k < 624; k += nt) rng.mt[k] = d.mt0[k];  // seeded and twisted on the host
   if (tid == 0) {
-    mt_seed(rng, 12345u);
+    rng.idx = 0;
     sh_int[0] = K < 3 ? 1 : 0;
     sh_int[2] = K < 3 ? INT_MAX - 1 : 0;
     sh_int[3] = -INT_MAX;
@@ -711,6 +709,7 @@ __global__ __launch_bounds__(1024) void k_ground_elev_ransac(DevCfg c, DevBufs d
     }
     __syncthreads();
   }
+  if (c.dbg_phase <= 2) return;
   // ---- inliers with depth <= 5 become ground again (IP:727-735) ----
   int ninl = 0;
   if (sh_int[5]) {
@@ -805,6 +804,7 @@ __global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
     P.st(cell, l0 ? cell : -1);
   }
   __syncthreads();
+  if (c.dbg_phase <= 0) return;
   for (int cell = tid; cell < HW; cell += nt) {
     if (P.ld(cell) < 0) continue;
     const int i = cell / W, j = cell - i * W;
@@ -817,6 +817,7 @@ __global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
     }
   }
   __syncthreads();
+  if (c.dbg_phase <= 1) return;
   if constexpr (kLds) {
     // Everything stays in the LDS word of each cell: -1 = not label 0; a member holds its root's
     // index (>= 0); a root holds 0x80000000 | size << 16 | row mask of its pushed members (size <=
@@ -830,6 +831,7 @@ __global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
       P.st(cell, x);
     }
     __syncthreads();
+    if (c.dbg_phase <= 2) return;
     for (int cell = tid; cell < HW; cell += nt)
       if (P.ld(cell) == cell) P.st(cell, (int)(0x80000000u | (1u << 16)));
     __syncthreads();
@@ -840,6 +842,7 @@ __global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
       atomicOr(&lds_parent[root], 1 << (cell / W));
     }
     __syncthreads();
+    if (c.dbg_phase <= 3) return;
     constexpr int kC = 4;
     int rank = 0;
     for (int t0 = 0; t0 < HW; t0 += kC * nt) {
@@ -862,6 +865,7 @@ __global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
       rank += tot;
     }
     __syncthreads();
+    if (c.dbg_phase <= 4) return;
     for (int cell = tid; cell < HW; cell += nt) {
       const int v = P.ld(cell);
       lab[cell] = v == -1 ? -1 : v < 0 ? (v & 0x7fffffff) : (P.ld(v) & 0x7fffffff);
