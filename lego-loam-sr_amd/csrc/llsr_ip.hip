@@ -383,6 +383,14 @@ __device__ __forceinline__ uint32_t st_column(bool one, bool cand) {
   return f;
 }
 
+// st_compose(st_column(one, cand), F) on the packed table directly: every 2-bit entry v = (a | b<<1)
+// becomes b | c<<1, c = one || (cand && (a || b)) — four bit operations instead of the generic loop.
+__device__ __forceinline__ uint32_t st_push(uint32_t F, bool one, bool cand) {
+  const uint32_t lo = (F >> 1) & 0x55u;
+  const uint32_t hi = one ? 0xAAu : cand ? (((F | (F >> 1)) & 0x55u) << 1) : 0u;
+  return lo | hi;
+}
+
 __device__ __forceinline__ bool add_test(const float4* __restrict__ full, int cell, int nb) {
   const float4 p = full[cell], q = full[nb];
   const float r = sqrt_(p.x * p.x + p.y * p.y + p.z * p.z);
@@ -416,7 +424,7 @@ __global__ __launch_bounds__(256) void k_ground_add(DevCfg c, DevBufs d) {
       const bool two = g[j] == 2;
       const bool cand = two && add_test(full, j, j - 2);
       if (cand) candBits |= 1ull << (j - j0);
-      F = st_compose(st_column(g[j] == 1, cand), F);
+      F = st_push(F, g[j] == 1, cand);
     }
     // exclusive scan of maps over lanes (lane order = column order)
     uint32_t incl = F;
@@ -451,7 +459,7 @@ __global__ __launch_bounds__(256) void k_ground_add(DevCfg c, DevBufs d) {
       const bool two = g[j] == 2;
       const bool cand = two && add_test(full, j, j + 2);
       if (cand) candBits |= 1ull << (j1 - j);
-      F = st_compose(st_column(g[j] == 1, cand), F);
+      F = st_push(F, g[j] == 1, cand);
     }
     uint32_t incl = F;
 #pragma unroll

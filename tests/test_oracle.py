@@ -207,3 +207,31 @@ def test_cell_intensity_multiply_equals_division():
     a = (r + c / 10000.0).astype(np.float32)
     b = (r + c * 1e-4).astype(np.float32)
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_ground_add_state_push_equals_composition():
+    """k_ground_add composes each column's 4-state map into the chunk map with st_push (bit ops);
+    it must equal st_compose(st_column(one, cand), F) of csrc/llsr_ip.hip for every packed F."""
+    def apply(f, s):
+        return (f >> (2 * s)) & 3
+
+    def compose(g, f):
+        return sum(apply(g, apply(f, s)) << (2 * s) for s in range(4))
+
+    def column(one, cand):
+        f = 0
+        for s in range(4):
+            a, bb = s & 1, s >> 1
+            cc = 1 if one else (1 if (cand and (a | bb)) else 0)
+            f |= (bb | (cc << 1)) << (2 * s)
+        return f
+
+    def push(F, one, cand):
+        lo = (F >> 1) & 0x55
+        hi = 0xAA if one else ((((F | (F >> 1)) & 0x55) << 1) if cand else 0)
+        return lo | hi
+
+    for F in range(256):
+        for one in (False, True):
+            for cand in (False, True):
+                assert push(F, one, cand) == compose(column(one, cand), F)
