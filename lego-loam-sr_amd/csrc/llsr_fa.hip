@@ -577,6 +577,23 @@ __device__ __forceinline__ bool db_near(const DevCfg& c, float4 pi, float4 pj, f
   return eps <= c.DBFr;
 }
 
+// Certified fast form of db_near: the squared scaled distance from hardware reciprocals (all three
+// terms are >= 0, so its relative error against the reference's float evaluation is < 1e-6) decides
+// eps <= DBFr whenever it is more than 2e-5 (relative) away from DBFr^2: below, sqrt(s) < DBFr and
+// its rounding cannot exceed DBFr; above, sqrt(s) exceeds DBFr by > 4 ulp. Pairs in the band, zero or
+// non-finite scales and NaN coordinates take the exact expression.
+__device__ __forceinline__ bool db_near_fast(const DevCfg& c, float4 pi, float4 pj, float kzj) {
+  const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
+  const float k2 = pj.w * pj.w, z2 = kzj * kzj;
+  if (c.DBFr > 0.0f && k2 > 1e-30f && k2 < 1e30f && z2 > 1e-30f && z2 < 1e30f) {
+    const float s = (dx * dx + dy * dy) * __builtin_amdgcn_rcpf(k2) + dz * dz * __builtin_amdgcn_rcpf(z2);
+    const float r2 = c.DBFr * c.DBFr;
+    if (s < r2 * (1.0f - 2e-5f)) return true;
+    if (s > r2 * (1.0f + 2e-5f)) return false;
+  }
+  return db_near(c, pi, pj, kzj);
+}
+
 // ---------------------------------------------------------------------------------------------
 // K9b eps-neighbourhood bitmask for every (i, j) of a scan (M <= kAdjCap): one wave evaluates
 // 64 consecutive j of one row i and stores the ballot as two words. Massively parallel; this
@@ -596,7 +613,7 @@ __global__ __launch_bounds__(256) void k_dbscan_adj(DevCfg c, DevBufs d) {
     const int i = task / nch, ch = task - i * nch;
     const int j = ch * 64 + l;
     bool nb = false;
-    if (j < M) nb = db_near(c, d.db_pts[base + i], d.db_pts[base + j], d.db_kz[base + j]);
+    if (j < M) nb = db_near_fast(c, d.db_pts[base + i], d.db_pts[base + j], d.db_kz[base + j]);
     const unsigned long long m = __ballot(nb);
     if (l == 0) adj[(size_t)i * kAdjWords + 2 * ch] = (uint32_t)m;
     if (l == 1 && 2 * ch + 1 < kAdjWords) adj[(size_t)i * kAdjWords + 2 * ch + 1] = (uint32_t)(m >> 32);

@@ -67,3 +67,37 @@ def test_projection_fast_atan2_error_bound():
     bound = err.max() + 2.0 ** -23 + 2.0 ** -22  # + rcp's extra ulp in t (atan' <= 1) + glibc's 1 ulp at pi
     assert err.max() < 5e-7, err.max()
     assert bound < 1e-6, bound
+
+
+def test_dbscan_fast_eps_margin_sound():
+    """k_dbscan_adj's db_near_fast decides eps <= DBFr from reciprocal-based squared distances and
+    defers to the exact expression (FA:1353-1354) within 2e-5 of DBFr^2. Statement in float32 with
+    the hardware reciprocal's 1-ulp error applied in both directions: every decided pair agrees with
+    the reference's float evaluation, including pairs placed on the boundary."""
+    import numpy as np
+    f = np.float32
+    rng = np.random.default_rng(7)
+    n = 400_000
+    DBFr = f(1.5)
+    kxy = rng.uniform(0.01, 0.5, n).astype(f)
+    kz = rng.uniform(0.01, 0.5, n).astype(f)
+    u = rng.normal(size=(n, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    # scaled radius: uniform around DBFr plus a dense band within 1e-5 of it
+    rad = np.where(rng.random(n) < 0.5, rng.uniform(0, 3, n), 1.5 * (1 + rng.uniform(-3e-5, 3e-5, n)))
+    d = (u * rad[:, None] * np.stack([kxy, kxy, kz], 1)).astype(f)
+    p0 = rng.uniform(-30, 30, (n, 3)).astype(f)
+    pj = (p0 - d).astype(f)
+    dx, dy, dz = (p0[:, 0] - pj[:, 0]), (p0[:, 1] - pj[:, 1]), (p0[:, 2] - pj[:, 2])
+    k2, z2 = kxy * kxy, kz * kz
+    exact = np.sqrt(dx * dx / k2 + dy * dy / k2 + dz * dz / z2) <= DBFr
+    r2 = DBFr * DBFr
+    lo, hi = r2 * f(1 - 2e-5), r2 * f(1 + 2e-5)
+    for sgn in (-1, 1):  # v_rcp_f32 within 1 ulp of 1/x
+        rk = (f(1) / k2) * f(1 + sgn * 2.0 ** -23)
+        rz = (f(1) / z2) * f(1 + sgn * 2.0 ** -23)
+        s = (dx * dx + dy * dy) * rk + dz * dz * rz
+        decided = (s < lo) | (s > hi)
+        fast = s < lo
+        assert np.array_equal(fast[decided], exact[decided])
+        assert decided.mean() > 0.4  # the band is narrow: most pairs never reach the exact path
