@@ -109,21 +109,37 @@ __global__ __launch_bounds__(512) void k_fa_points(DevCfg c, DevBufs d) {
         }
       }
     }
-    for (int q = tid; q < kTile + 12; q += nt) {
-      const int i = t0 - 6 + q;
-      uint8_t f = 0;
-      if (i >= 5 && i < S - 6) {
-        const float d1 = rng[i], d2 = rng[i + 1];
-        const int colDiff = abs((int)(col[i + 1] - col[i]));
-        if (colDiff < 10) {
-          if ((double)(d1 - d2) > 0.3) f |= 1;
-          else if ((double)(d2 - d1) > 0.3) f |= 2;
+    // occlusion flags of the tile (+ halo): every lane's ranges / columns are loaded in one batch
+    constexpr int kQ = (kTile + 12 + 511) / 512;
+    {
+      float r0[kQ], r1[kQ], r2[kQ];
+      uint32_t c1[kQ], c2[kQ];
+#pragma unroll
+      for (int u = 0; u < kQ; ++u) {
+        const int q = tid + u * nt, i = t0 - 6 + q;
+        if (q < kTile + 12 && i >= 5 && i < S - 6) {
+          r0[u] = rng[i - 1]; r1[u] = rng[i]; r2[u] = rng[i + 1];
+          c1[u] = col[i]; c2[u] = col[i + 1];
         }
-        const float diff1 = fabs_((float)(rng[i - 1] - rng[i]));
-        const float diff2 = fabs_((float)(rng[i + 1] - rng[i]));
-        if ((double)diff1 > 0.02 * (double)rng[i] && (double)diff2 > 0.02 * (double)rng[i]) f |= 4;
       }
-      fl[q] = f;
+#pragma unroll
+      for (int u = 0; u < kQ; ++u) {
+        const int q = tid + u * nt, i = t0 - 6 + q;
+        if (q >= kTile + 12) continue;
+        uint8_t f = 0;
+        if (i >= 5 && i < S - 6) {
+          const float d1 = r1[u], d2 = r2[u];
+          const int colDiff = abs((int)(c2[u] - c1[u]));
+          if (colDiff < 10) {
+            if ((double)(d1 - d2) > 0.3) f |= 1;
+            else if ((double)(d2 - d1) > 0.3) f |= 2;
+          }
+          const float diff1 = fabs_((float)(r0[u] - r1[u]));
+          const float diff2 = fabs_((float)(r2[u] - r1[u]));
+          if ((double)diff1 > 0.02 * (double)r1[u] && (double)diff2 > 0.02 * (double)r1[u]) f |= 4;
+        }
+        fl[q] = f;
+      }
     }
     __syncthreads();
     for (int q0 = tid; q0 < kTile; q0 += nt) {
@@ -155,8 +171,8 @@ __global__ __launch_bounds__(512) void k_fa_points(DevCfg c, DevBufs d) {
       for (int m = 0; m <= 5; ++m) occ |= (fl[fq + m] & 1) != 0;   // A_i, i in [k, k+5]
 #pragma unroll
       for (int m = 1; m <= 6; ++m) occ |= (fl[fq - m] & 2) != 0;   // B_i, i in [k-6, k-1]
-      const uint8_t old = picked[k];
-      picked[k] = (inner ? (uint8_t)0 : old) | (occ ? (uint8_t)1 : (uint8_t)0);
+      const uint8_t old = inner ? (uint8_t)0 : picked[k];  // only the 10 edge points keep theirs
+      picked[k] = old | (occ ? (uint8_t)1 : (uint8_t)0);
       if (inner) clabel[k] = 0;
     }
     __syncthreads();
