@@ -953,7 +953,6 @@ template __global__ void k_label<false>(DevCfg, DevBufs);
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void k_segment(DevCfg c, const float4* __restrict__ pts,
                                                   const int64_t* __restrict__ off, DevBufs d) {
-  __shared__ int tmp[32];
   const int b = blockIdx.x;
   const int W = c.W, H = c.H, HW = c.HW;
   const size_t base = (size_t)b * HW;
@@ -983,52 +982,70 @@ __global__ __launch_bounds__(1024) void k_segment(DevCfg c, const float4* __rest
     if (gv == 1 && (j % 5 != 0 && j > 5 && j < W - 5)) return 0;
     return 1;
   };
-  // row-major compaction in tiles of 4 * blockDim cells, 4 consecutive cells per lane (their loads
-  // and gathers all in flight together); one packed block scan of the lane totals per tile. The
-  // label / ground loads of the next tile are issued before this tile's scan, so a tile pays one
-  // exposed memory round trip (its gathers) instead of two.
+  // Row-major compaction in tiles of 4 * blockDim cells, cell t0 + u * blockDim + tid in slot u of
+  // a lane, so every load and every output store of one slot is contiguous across the wave (the
+  // kept cells of a wave land in consecutive output positions). Offsets: per (slot, wave) ballot
+  // counts, one scan of those <= 64 words in (slot, wave) = row-major order. The label / ground
+  // loads of the next tile are issued before this tile's scan.
   constexpr int kC = 4;
+  __shared__ int wcnt[2][kC * 16 + 1];  // packed segmented | outlier << 16 counts, double-buffered
+  const int nw = nt >> 6, wv = tid >> 6, l = lane_id();
+  const unsigned long long lt = (1ull << l) - 1ull;
   int baseS = 0, baseO = 0;
   int labn[kC];
   int8_t gn[kC];
   auto load_kind = [&](int t0) {
-    const int c0 = t0 + kC * tid;
 #pragma unroll
     for (int u = 0; u < kC; ++u) {
-      labn[u] = c0 + u < HW ? lab[c0 + u] : 0;
-      gn[u] = c0 + u < HW ? g[c0 + u] : (int8_t)0;
+      const int cell = t0 + u * nt + tid;
+      labn[u] = cell < HW ? lab[cell] : 0;
+      gn[u] = cell < HW ? g[cell] : (int8_t)0;
     }
   };
   load_kind(0);
-  for (int t0 = 0; t0 < HW; t0 += kC * nt) {
-    const int c0 = t0 + kC * tid;
+  int par = 0;
+  for (int t0 = 0; t0 < HW; t0 += kC * nt, par ^= 1) {
     int kk[kC];
     int8_t gc[kC];
-    int ns = 0, no = 0;
 #pragma unroll
     for (int u = 0; u < kC; ++u) {
+      const int cell = t0 + u * nt + tid;
       gc[u] = gn[u];
-      kk[u] = c0 + u < HW ? kind(c0 + u, labn[u], gn[u]) : 0;
-      ns += kk[u] == 1;
-      no += kk[u] == 2;
+      kk[u] = cell < HW ? kind(cell, labn[u], gn[u]) : 0;
     }
     float4 f[kC];
     float rg[kC], vs[kC];
 #pragma unroll
     for (int u = 0; u < kC; ++u) {
       if (kk[u] == 0) continue;
-      f[u] = d.full[base + c0 + u];
-      vs[u] = d.vis[base + c0 + u];
-      rg[u] = kk[u] == 1 ? d.range[base + c0 + u] : 0.0f;
+      const size_t q = base + t0 + u * nt + tid;
+      f[u] = d.full[q];
+      vs[u] = d.vis[q];
+      rg[u] = kk[u] == 1 ? d.range[q] : 0.0f;
     }
     if (t0 + kC * nt < HW) load_kind(t0 + kC * nt);
-    int tot;
-    const int ex = block_excl_scan(ns | (no << 16), tmp, &tot);
-    int ps = baseS + (ex & 0xffff), po = baseO + (ex >> 16);
+    unsigned long long mS[kC], mO[kC];
 #pragma unroll
     for (int u = 0; u < kC; ++u) {
-      const int cell = c0 + u;
+      mS[u] = __ballot(kk[u] == 1);
+      mO[u] = __ballot(kk[u] == 2);
+      if (l == 0) wcnt[par][u * nw + wv] = (int)__popcll(mS[u]) | ((int)__popcll(mO[u]) << 16);
+    }
+    __syncthreads();
+    if (wv == 0) {
+      const int v = l < kC * nw ? wcnt[par][l] : 0;
+      const int incl = wave_incl_scan_add(v);
+      if (l < kC * nw) wcnt[par][l] = incl - v;
+      if (l == 63) wcnt[par][kC * 16] = incl;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kC; ++u) {
+      const int cell = t0 + u * nt + tid;
       if (cell >= HW) break;
+      const int ex = wcnt[par][u * nw + wv];
+      const int ps = baseS + (ex & 0xffff) + (int)__popcll(mS[u] & lt);
+      const int po = baseO + (ex >> 16) + (int)__popcll(mO[u] & lt);
       const int i = cell / W, j = cell - i * W;
       if (j == 0) {
         d.start_ring[b * H + i] = ps - 1 + 5;
@@ -1040,13 +1057,12 @@ __global__ __launch_bounds__(1024) void k_segment(DevCfg c, const float4* __rest
         d.seg_col[base + ps] = (uint32_t)j;
         d.seg_range[base + ps] = rg[u];
         d.seg_int[base + ps] = vs[u];
-        ++ps;
       } else if (kk[u] == 2) {
         d.outl[base + po] = f[u];
         d.outl_int[base + po] = vs[u];
-        ++po;
       }
     }
+    const int tot = wcnt[par][kC * 16];
     baseS += tot & 0xffff;
     baseO += tot >> 16;
   }
