@@ -596,36 +596,51 @@ __global__ __launch_bounds__(1024) void k_ground_elev_ransac(DevCfg c, DevBufs d
 
   if (c.dbg_phase <= 0) return;
   // ---- NEAR (IP:701-715): row-major compaction, intensity = linear index ----
-  // 4 consecutive cells per lane per tile (loads in flight together, one block scan per tile).
+  // Cells interleaved across lanes per slot (t0 + u * blockDim + tid): loads and the compacted
+  // stores of a wave are contiguous; row-major positions from per-(slot, wave) ballot counts.
   float4* nearp = d.near_pts + base;
   int K = 0;
   constexpr int kC = 4;
-  for (int t0 = 0; t0 < HW; t0 += kC * nt) {
-    const int c0 = t0 + kC * tid;
+  __shared__ int ncnt[2][kC * 16 + 1];
+  const int nw = nt >> 6, wv = tid >> 6, ln = lane_id();
+  int par = 0;
+  for (int t0 = 0; t0 < HW; t0 += kC * nt, par ^= 1) {
     int8_t gv[kC];
 #pragma unroll
-    for (int u = 0; u < kC; ++u) gv[u] = c0 + u < HW ? g[c0 + u] : (int8_t)0;
+    for (int u = 0; u < kC; ++u) {
+      const int cell = t0 + u * nt + tid;
+      gv[u] = cell < HW ? g[cell] : (int8_t)0;
+    }
     float4 p[kC];
 #pragma unroll
-    for (int u = 0; u < kC; ++u) p[u] = gv[u] == 1 ? full[c0 + u] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < kC; ++u) p[u] = gv[u] == 1 ? full[t0 + u * nt + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
     bool nearc[kC];
     float depth[kC];
-    int nn = 0;
+    unsigned long long mN[kC];
 #pragma unroll
     for (int u = 0; u < kC; ++u) {
       depth[u] = sqrt_(p[u].x * p[u].x + p[u].y * p[u].y);
       nearc[u] = gv[u] == 1 && (double)depth[u] <= 10;
-      nn += nearc[u];
+      mN[u] = __ballot(nearc[u]);
+      if (ln == 0) ncnt[par][u * nw + wv] = (int)__popcll(mN[u]);
     }
-    int tot;
-    int pos = K + block_excl_scan(nn, tmp, &tot);
+    __syncthreads();
+    if (wv == 0) {
+      const int v = ln < kC * nw ? ncnt[par][ln] : 0;
+      const int incl = wave_incl_scan_add(v);
+      if (ln < kC * nw) ncnt[par][ln] = incl - v;
+      if (ln == 63) ncnt[par][kC * 16] = incl;
+    }
+    __syncthreads();
 #pragma unroll
     for (int u = 0; u < kC; ++u) {
       if (!nearc[u]) continue;
-      nearp[pos++] = make_float4(p[u].x, p[u].y, p[u].z, (float)(c0 + u));
-      if ((double)depth[u] <= 5) g[c0 + u] = 0;
+      const int cell = t0 + u * nt + tid;
+      const int pos = K + ncnt[par][u * nw + wv] + (int)__popcll(mN[u] & ((1ull << ln) - 1ull));
+      nearp[pos] = make_float4(p[u].x, p[u].y, p[u].z, (float)cell);
+      if ((double)depth[u] <= 5) g[cell] = 0;
     }
-    K += tot;
+    K += ncnt[par][kC * 16];
   }
   int* shuf = d.shuf + base;
   for (int k = tid; k < K; k += nt) shuf[k] = k;
