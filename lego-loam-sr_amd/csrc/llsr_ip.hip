@@ -204,45 +204,63 @@ __global__ __launch_bounds__(256) void k_gather_column(DevCfg c, const float4* _
 // values (IP:170-179); pass 3 runs the per-column ground test + Filter (IP:524-629) on the cell
 // arrays. No global atomics, no gather of scattered input points.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void ground_column(const DevCfg& c, const float4* __restrict__ full, int8_t* ground,
-                                              int j) {
+// groundRemovalOurs' per-column test (IP:524-629) as a step over one column's state, so a lane can
+// carry two columns at once: their serial 16-row chains interleave (ILP) instead of running in two
+// rounds of lanes.
+struct GndState {
   bool haveRV = false, obs = false;
   float RVx = 0.f, RVy = 0.f, RVz = 0.f, lx = 0.f, ly = 0.f, lz = 0.f;
-  // the column's cells are loaded 8 rows at a time, ahead of the serial test over them
+};
+__device__ __forceinline__ int8_t ground_step(const DevCfg& c, GndState& st, float4 f, int i) {
+  int8_t g;
+  if (f.w == 0.0f) {
+    g = -1;
+  } else if (!st.haveRV) {
+    const float d0 = sqrt_(f.x * f.x + f.y * f.y);
+    st.RVx = f.x / d0; st.RVy = f.y / d0; st.RVz = 0.0f;
+    st.haveRV = true;
+    st.lx = f.x; st.ly = f.y; st.lz = f.z;
+    g = 1;
+  } else {
+    const float TVx = f.x - st.lx, TVy = f.y - st.ly, TVz = f.z - st.lz;
+    // (float)(acosf(x) / deg) <= D  <=>  gnd_cos(D) <= x <= 1  (llsr_libm.h ground_cos_threshold)
+    const float x = (TVx * st.RVx + TVy * st.RVy + TVz * st.RVz) /
+                    (sqrt_(TVx * TVx + TVy * TVy + TVz * TVz) *
+                     sqrt_(st.RVx * st.RVx + st.RVy * st.RVy + st.RVz * st.RVz));
+    const float xs = c.use_kitti ? (i < 16 ? c.gnd_cos[1] : c.gnd_cos[2]) : c.gnd_cos[0];
+    if (x >= xs && x <= 1.0f) { st.RVx += TVx; st.RVy += TVy; st.RVz += TVz; g = 1; }
+    else g = 0;
+    st.lx = f.x; st.ly = f.y; st.lz = f.z;
+  }
+  // Filter (IP:620-628): after the first 0 of the column every 1 becomes 2.
+  if (g == 0) st.obs = true;
+  else if (g == 1 && st.obs) g = 2;
+  return g;
+}
+
+// columns j0 and j1 (j1 >= W: none), their cells loaded 8 rows at a time ahead of the tests
+__device__ __forceinline__ void ground_columns2(const DevCfg& c, const float4* __restrict__ full, int8_t* ground,
+                                                int j0, int j1) {
+  GndState s0, s1;
+  const bool has1 = j1 < c.W;
   constexpr int kR = 8;
-  float4 fr[kR];
-  for (int i = 0; i < c.H; ++i) {
-    const int cell = j + i * c.W;
-    if (i % kR == 0) {
+  for (int i0 = 0; i0 < c.H; i0 += kR) {
+    float4 f0[kR], f1[kR];
 #pragma unroll
-      for (int u = 0; u < kR; ++u) fr[u] = i + u < c.H ? full[cell + u * c.W] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < kR; ++u) {
+      const bool in = i0 + u < c.H;
+      f0[u] = in ? full[j0 + (i0 + u) * c.W] : make_float4(0.f, 0.f, 0.f, 0.f);
+      f1[u] = in && has1 ? full[j1 + (i0 + u) * c.W] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    float4 f = fr[0];
 #pragma unroll
-    for (int u = 1; u < kR; ++u)
-      if (i % kR == u) f = fr[u];
-    int8_t g;
-    if (f.w == 0.0f) {
-      g = -1;
-    } else if (!haveRV) {
-      const float d0 = sqrt_(f.x * f.x + f.y * f.y);
-      RVx = f.x / d0; RVy = f.y / d0; RVz = 0.0f;
-      haveRV = true;
-      lx = f.x; ly = f.y; lz = f.z;
-      g = 1;
-    } else {
-      const float TVx = f.x - lx, TVy = f.y - ly, TVz = f.z - lz;
-      // (float)(acosf(x) / deg) <= D  <=>  gnd_cos(D) <= x <= 1  (llsr_libm.h ground_cos_threshold)
-      const float x = (TVx * RVx + TVy * RVy + TVz * RVz) /
-                      (sqrt_(TVx * TVx + TVy * TVy + TVz * TVz) * sqrt_(RVx * RVx + RVy * RVy + RVz * RVz));
-      const float xs = c.use_kitti ? (i < 16 ? c.gnd_cos[1] : c.gnd_cos[2]) : c.gnd_cos[0];
-      if (x >= xs && x <= 1.0f) { RVx += TVx; RVy += TVy; RVz += TVz; g = 1; }
-      else g = 0;
-      lx = f.x; ly = f.y; lz = f.z;
+    for (int u = 0; u < kR; ++u) {
+      const int i = i0 + u;
+      if (i >= c.H) break;
+      const int8_t g0 = ground_step(c, s0, f0[u], i);
+      const int8_t g1 = ground_step(c, s1, f1[u], i);
+      ground[j0 + i * c.W] = g0;
+      if (has1) ground[j1 + i * c.W] = g1;
     }
-    if (g == 0) obs = true;
-    else if (g == 1 && obs) g = 2;
-    ground[cell] = g;
   }
 }
 
@@ -354,7 +372,7 @@ __global__ __launch_bounds__(1024) void k_project_fused(DevCfg c, const float4* 
     __syncthreads();
   }
   if (c.dbg_phase <= 1) return;
-  for (int j = tid; j < c.W; j += nt) ground_column(c, d.full + base, d.ground + base, j);
+  for (int j = tid; j < c.W; j += 2 * nt) ground_columns2(c, d.full + base, d.ground + base, j, j + nt);
 }
 
 // ---------------------------------------------------------------------------------------------
