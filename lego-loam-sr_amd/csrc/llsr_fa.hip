@@ -194,18 +194,40 @@ __global__ __launch_bounds__(512) void k_fa_points(DevCfg c, DevBufs d) {
 constexpr int kRingMax = 2048;  // >= max W
 constexpr int kWin = kRingMax + 16;
 
-// Block bitonic sort of n2 (power of two) 64-bit keys in LDS, ascending; one compare-exchange
-// pair per thread-iteration (no idle half), one barrier per stage.
+// Block bitonic sort of n2 (power of two) 64-bit keys in LDS, ascending.
+// Two consecutive stages (j, j/2) of one merge step run on groups of four keys {t, t+h, t+j, t+j+h}
+// (h = j/2, t with zeros at bits log2 h and log2 j) held in registers: the same compare-exchanges
+// as the one-stage network, half the LDS round trips and barriers.
+__device__ __forceinline__ void bitonic_cx(uint64_t& a, uint64_t& e, bool up) {
+  if ((a > e) == up) { const uint64_t t = a; a = e; e = t; }
+}
 __device__ __forceinline__ void bitonic_sort_u64(uint64_t* key, int n2) {
-  const int half = n2 >> 1;
+  const int half = n2 >> 1, quarter = n2 >> 2;
   for (int k = 2; k <= n2; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int p = threadIdx.x; p < half; p += blockDim.x) {
-        const int t = ((p & ~(j - 1)) << 1) | (p & (j - 1));  // p with a 0 inserted at bit log2(j)
-        const int u = t | j;
-        const uint64_t a = key[t], e = key[u];
+    int j = k >> 1;
+    while (j >= 2) {
+      const int h = j >> 1;
+      for (int p = threadIdx.x; p < quarter; p += blockDim.x) {
+        const int a = ((p & ~(h - 1)) << 1) | (p & (h - 1));  // 0 inserted at bit log2(h)
+        const int t = ((a & ~(j - 1)) << 1) | (a & (j - 1));  // and at bit log2(j)
         const bool up = (t & k) == 0;
-        if ((a > e) == up) { key[t] = e; key[u] = a; }
+        uint64_t v0 = key[t], v1 = key[t + h], v2 = key[t + j], v3 = key[t + j + h];
+        bitonic_cx(v0, v2, up);
+        bitonic_cx(v1, v3, up);
+        bitonic_cx(v0, v1, up);
+        bitonic_cx(v2, v3, up);
+        key[t] = v0; key[t + h] = v1; key[t + j] = v2; key[t + j + h] = v3;
+      }
+      __syncthreads();
+      j >>= 2;
+    }
+    if (j == 1) {
+      for (int p = threadIdx.x; p < half; p += blockDim.x) {
+        const int t = p << 1;
+        const bool up = (t & k) == 0;
+        uint64_t v0 = key[t], v1 = key[t + 1];
+        bitonic_cx(v0, v1, up);
+        key[t] = v0; key[t + 1] = v1;
       }
       __syncthreads();
     }
