@@ -533,15 +533,33 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   if (c.dbg_phase <= 5) return;
   bitonic_sort_u64(key, R2);
   if (c.dbg_phase <= 6) return;
-  // voxels = groups of sorted runs with equal id; sum members in (run start, position) order
-  const int perv = (R + nt - 1) / nt;
-  const int v0 = min(tid * perv, R), v1 = min(v0 + perv, R);
-  int vh = 0;
-  for (int t = v0; t < v1; ++t) vh += (t == 0 || (key[t] >> 32) != (key[t - 1] >> 32));
-  int V;
-  int vo = block_excl_scan(vh, tmp, &V);
-  for (int t = v0; t < v1; ++t) {
-    if (!(t == 0 || (key[t] >> 32) != (key[t - 1] >> 32))) continue;
+  // voxels = groups of sorted runs with equal id; sum members in (run start, position) order.
+  // Sorted run t = u * 256 + tid sits in slot u of a lane, so a wave's voxel heads of one slot are
+  // consecutive voxels and their centroids are stored contiguously; output positions come from
+  // per-(slot, wave) ballot counts scanned in (slot, wave) = sorted order.
+  __shared__ int vcnt[kLp * 4 + 1];
+  const int wv = tid >> 6, ln = lane_id();
+  unsigned long long mH[kLp];
+#pragma unroll
+  for (int u = 0; u < kLp; ++u) {
+    const int t = u * 256 + tid;
+    const bool head = t < R && (t == 0 || (key[t] >> 32) != (key[t - 1] >> 32));
+    mH[u] = __ballot(head);
+    if (ln == 0) vcnt[u * 4 + wv] = (int)__popcll(mH[u]);
+  }
+  __syncthreads();
+  if (wv == 0) {
+    const int v = ln < kLp * 4 ? vcnt[ln] : 0;
+    const int incl = wave_incl_scan_add(v);
+    if (ln < kLp * 4) vcnt[ln] = incl - v;
+    if (ln == 63) vcnt[kLp * 4] = incl;
+  }
+  __syncthreads();
+  const int V = vcnt[kLp * 4];
+#pragma unroll
+  for (int u = 0; u < kLp; ++u) {
+    const int t = u * 256 + tid;
+    if (!((mH[u] >> ln) & 1ull)) continue;
     const uint32_t vid = (uint32_t)(key[t] >> 32);
     float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
     int cntp = 0;
@@ -554,7 +572,8 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
       }
     }
     const float nn = (float)cntp;
-    out[vo++] = make_float4(sx / nn, sy / nn, sz / nn, si / nn);
+    const int vo = vcnt[u * 4 + wv] + (int)__popcll(mH[u] & ((1ull << ln) - 1ull));
+    out[vo] = make_float4(sx / nn, sy / nn, sz / nn, si / nn);
   }
   if (tid == 0) rc[2 * H + i] = V;
 }
