@@ -513,18 +513,38 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
     vk[t] = (uint32_t)(i0 + i1 * mul1 + i2 * mul2);
   }
   __syncthreads();
-  // runs of equal voxel id in ring order -> one sort key per run: (voxel id, run index)
-  const int perr = (L + nt - 1) / nt;
-  const int r0 = min(tid * perr, L), r1 = min(r0 + perr, L);
-  int heads = 0;
-  for (int t = r0; t < r1; ++t) heads += (t == 0 || vk[t] != vk[t - 1]);
-  int R;
-  int ro = block_excl_scan(heads, tmp, &R);
-  for (int t = r0; t < r1; ++t) {
-    if (!(t == 0 || vk[t] != vk[t - 1])) continue;
+  // runs of equal voxel id in ring order -> one sort key per run: (voxel id, run index). Position
+  // t = u * 256 + tid in slot u of a lane; run indices from per-(slot, wave) ballot counts scanned in
+  // (slot, wave) = ring order.
+  __shared__ int scnt[kLp * 4 + 1];
+  const int wv = tid >> 6, ln = lane_id();
+  const unsigned long long ltm = (1ull << ln) - 1ull;
+  auto slot_scan = [&]() {  // exclusive scan of scnt[0 .. kLp*4) in place, total in scnt[kLp*4]
+    __syncthreads();
+    if (wv == 0) {
+      const int v = ln < kLp * 4 ? scnt[ln] : 0;
+      const int incl = wave_incl_scan_add(v);
+      if (ln < kLp * 4) scnt[ln] = incl - v;
+      if (ln == 63) scnt[kLp * 4] = incl;
+    }
+    __syncthreads();
+  };
+  unsigned long long mR[kLp];
+#pragma unroll
+  for (int u = 0; u < kLp; ++u) {
+    const int t = u * 256 + tid;
+    mR[u] = __ballot(t < L && (t == 0 || vk[t] != vk[t - 1]));
+    if (ln == 0) scnt[u * 4 + wv] = (int)__popcll(mR[u]);
+  }
+  slot_scan();
+  const int R = scnt[kLp * 4];
+#pragma unroll
+  for (int u = 0; u < kLp; ++u) {
+    if (!((mR[u] >> ln) & 1ull)) continue;
+    const int t = u * 256 + tid;
+    const int ro = scnt[u * 4 + wv] + (int)__popcll(mR[u] & ltm);
     rstart[ro] = (uint16_t)t;
     key[ro] = ((uint64_t)vk[t] << 32) | (uint32_t)ro;
-    ++ro;
   }
   if (tid == 0) rstart[R] = (uint16_t)L;
   const int R2 = pow2_ceil(R);
@@ -537,25 +557,16 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   // Sorted run t = u * 256 + tid sits in slot u of a lane, so a wave's voxel heads of one slot are
   // consecutive voxels and their centroids are stored contiguously; output positions come from
   // per-(slot, wave) ballot counts scanned in (slot, wave) = sorted order.
-  __shared__ int vcnt[kLp * 4 + 1];
-  const int wv = tid >> 6, ln = lane_id();
   unsigned long long mH[kLp];
 #pragma unroll
   for (int u = 0; u < kLp; ++u) {
     const int t = u * 256 + tid;
     const bool head = t < R && (t == 0 || (key[t] >> 32) != (key[t - 1] >> 32));
     mH[u] = __ballot(head);
-    if (ln == 0) vcnt[u * 4 + wv] = (int)__popcll(mH[u]);
+    if (ln == 0) scnt[u * 4 + wv] = (int)__popcll(mH[u]);
   }
-  __syncthreads();
-  if (wv == 0) {
-    const int v = ln < kLp * 4 ? vcnt[ln] : 0;
-    const int incl = wave_incl_scan_add(v);
-    if (ln < kLp * 4) vcnt[ln] = incl - v;
-    if (ln == 63) vcnt[kLp * 4] = incl;
-  }
-  __syncthreads();
-  const int V = vcnt[kLp * 4];
+  slot_scan();
+  const int V = scnt[kLp * 4];
 #pragma unroll
   for (int u = 0; u < kLp; ++u) {
     const int t = u * 256 + tid;
@@ -572,7 +583,7 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
       }
     }
     const float nn = (float)cntp;
-    const int vo = vcnt[u * 4 + wv] + (int)__popcll(mH[u] & ((1ull << ln) - 1ull));
+    const int vo = scnt[u * 4 + wv] + (int)__popcll(mH[u] & ltm);
     out[vo] = make_float4(sx / nn, sy / nn, sz / nn, si / nn);
   }
   if (tid == 0) rc[2 * H + i] = V;
