@@ -596,6 +596,7 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_fa_concat(DevCfg c, DevBufs d) {
   __shared__ int roff[3][65];
+  __shared__ int rsp[64];
   const int b = blockIdx.x;
   const int H = c.H;
   const size_t base = (size_t)b * c.HW;
@@ -609,13 +610,24 @@ __global__ __launch_bounds__(256) void k_fa_concat(DevCfg c, DevBufs d) {
       if (tid == 63) roff[q][H] = incl;
     }
   }
+  if (tid < H) rsp[tid] = d.start_ring[b * H + tid];
   __syncthreads();
   const int M = roff[0][H];
-  for (int r = 0; r < H; ++r) {
-    const int sp = d.start_ring[b * H + r];
-    for (int t = tid; t < rc[r]; t += nt) d.less_sharp[base + roff[0][r] + t] = d.edge_tmp[base + sp + t];
-    for (int t = tid; t < rc[H + r]; t += nt) d.flat[base + roff[1][r] + t] = d.flat_tmp[base + sp + t];
-    for (int t = tid; t < rc[2 * H + r]; t += nt) d.lflat[base + roff[2][r] + t] = d.lflat_tmp[base + sp + t];
+  // all rings of a list at once: output a comes from ring r with roff[r] <= a < roff[r + 1]
+  for (int q = 0; q < 3; ++q) {
+    const int tot = roff[q][H];
+    for (int a = tid; a < tot; a += nt) {
+      int lo = 0, hi = H - 1;  // largest r with roff[q][r] <= a (never an empty ring)
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (roff[q][mid] <= a) lo = mid;
+        else hi = mid - 1;
+      }
+      const size_t src = base + rsp[lo] + (a - roff[q][lo]);
+      if (q == 0) d.less_sharp[base + a] = d.edge_tmp[src];
+      else if (q == 1) d.flat[base + a] = d.flat_tmp[src];
+      else d.lflat[base + a] = d.lflat_tmp[src];
+    }
   }
   __syncthreads();
   const float4* loam = d.loam + base;
