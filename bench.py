@@ -21,6 +21,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -500,6 +501,19 @@ def ctypes_sizeof_report() -> int:
     return ctypes.sizeof(_abi.LmReport)
 
 
+def launcher_cmd(argv: list, gpus: int, port: int) -> list:
+    """The torchrun command that runs this script on `gpus` ranks (one process per GPU, RCCL)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -525,8 +539,15 @@ def main():
                     help="configs[4] leg: scans per step split over all ranks (0 = skip)")
     args = ap.parse_args()
 
-    import torch
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # not started by torchrun: launch one rank per GPU as a child process (nothing here has
+        # touched the GPU yet) and exit with its status
+        sys.exit(subprocess.call(launcher_cmd(sys.argv[1:], args.gpus, free_port())))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+
+    import torch
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None

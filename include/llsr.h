@@ -148,8 +148,12 @@ int32_t llsr_process_scan(llsr_handle* h, const float* xyzi, int32_t n, llsr_sca
 
 /* Batched, device-resident: scans b = 0..B-1 are d_xyzi[d_offsets[b] .. d_offsets[b+1]),
  * float4 records in HBM (B+1 int64 offsets, also in device memory). Slot b uses FA carry-over
- * state b. Enqueued on `hip_stream` (hipStream_t, NULL = default stream); returns after
- * enqueue. Results stay in the handle until the next call. */
+ * state b. Enqueued on `hip_stream` (hipStream_t); NULL selects the handle's own stream, which is
+ * created non-blocking — it does NOT synchronise with the legacy default stream, so a caller that
+ * filled d_xyzi on the default stream must pass that stream (or synchronise) itself. Returns after
+ * enqueue. Batches of one handle are ordered even across streams (each waits for the previous
+ * one's completion event), because they share the slot buffers and the FA carry-over state.
+ * Results stay in the handle until the next call. */
 int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const int64_t* d_offsets,
                            int32_t B, void* hip_stream);
 
@@ -203,7 +207,7 @@ typedef struct llsr_s2s_batch {
 /* Size the scan-to-scan buffers (problems per batch, points per cloud). */
 int32_t llsr_scan2scan_reserve(llsr_handle* h, int32_t max_problems, int32_t max_sharp, int32_t max_flat,
                                int32_t max_corner_last, int32_t max_surf_last);
-/* Enqueue a batch on `hip_stream` (NULL: the handle's stream); fully asynchronous: every
+/* Enqueue a batch on `hip_stream` (NULL: the handle's own non-blocking stream); fully asynchronous: every
  * iteration runs inside one kernel. LLSR_ERANGE is reported by a later call's check of the
  * device error flag (llsr_scan2scan_check) when a cloud exceeded the reservation. */
 int32_t llsr_scan2scan_batch(llsr_handle* h, const llsr_s2s_batch* batch, void* hip_stream);
@@ -238,7 +242,7 @@ typedef struct llsr_s2m_batch {
  * points per cloud. Replaces MO's per-scan kd-tree allocation (MO:1575-1576). */
 int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t max_problems, int32_t max_corner_map,
                               int32_t max_surf_map, int32_t max_corner_q, int32_t max_surf_q);
-/* Run the batch on `hip_stream` (NULL: the handle's stream). The LM's iteration count is data
+/* Run the batch on `hip_stream` (NULL: the handle's own non-blocking stream). The LM's iteration count is data
  * dependent, so the call waits on the stream every few iterations to stop once every problem
  * has converged or reached iterCountThres; it returns when the batch is complete.
  * LLSR_ERANGE: a cloud exceeds the reserved capacity (nothing written for that problem). */

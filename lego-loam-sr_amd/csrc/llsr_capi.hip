@@ -63,6 +63,7 @@ struct llsr_handle {
   int64_t* d_off = nullptr;
   hipStream_t stream = nullptr;
   hipStream_t last_stream = nullptr;
+  hipEvent_t last_done = nullptr;  // recorded after each batch: the next one (any stream) waits on it
   int last_B = 0;
   const float4* last_pts = nullptr;  // inputs of the last batch (diagnostic re-launches only)
   const int64_t* last_off = nullptr;
@@ -86,6 +87,7 @@ struct llsr_handle {
     llsr_s2m_stats stats{};
     S2MArgs sh{};                // the open split-correspondence batch (llsr_scan2map_shard_*)
     bool sh_live = false;
+    hipStream_t last = nullptr;  // stream of the last scan-to-map launch
   } mo;
   // scan-to-scan (llsr_scan2scan_*)
   struct {
@@ -204,6 +206,10 @@ static T* carve(char*& p, size_t n) {
   return r;
 }
 
+// Wait for every stream this handle has launched work on (before its buffers are re-allocated):
+// stream-scoped, so other handles' streams on the device keep running.
+static hipError_t sync_handle_streams(llsr_handle* h);
+
 // boost::mt19937 seeded with 12345 (PCL 1.10 SampleConsensusModel's rng_alg_, IP:716-721), state
 // after the seeding recurrence and the first twist: every scan's RANSAC starts its draws here, so
 // the device loads 624 words instead of running 1248 serial steps on one lane per scan.
@@ -300,6 +306,10 @@ extern "C" int32_t llsr_create(const llsr_config* cfg, int32_t hip_device, int32
   for (auto& set : h->ev)
     for (auto& e : set)
       if (hipEventCreate(&e) != hipSuccess) { llsr_destroy(h); return LLSR_ENODEV; }
+  if (hipEventCreateWithFlags(&h->last_done, hipEventDisableTiming) != hipSuccess) {
+    llsr_destroy(h);
+    return LLSR_ENODEV;
+  }
   if (h->dc.ccl_lds) {
     if (hipFuncSetAttribute((const void*)k_label<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             h->dc.HW * (int)sizeof(int)) != hipSuccess ||
@@ -319,9 +329,11 @@ extern "C" void llsr_destroy(llsr_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->last_stream) (void)hipStreamSynchronize(h->last_stream);
   for (auto& set : h->ev)
     for (auto& e : set)
       if (e) (void)hipEventDestroy(e);
+  if (h->last_done) (void)hipEventDestroy(h->last_done);
   if (h->pool) (void)hipFree(h->pool);
   if (h->mo.pool) (void)hipFree(h->mo.pool);
   if (h->s2s.pool) (void)hipFree(h->s2s.pool);
@@ -342,6 +354,15 @@ extern "C" void llsr_destroy(llsr_handle* h) {
   if (h->d_off) (void)hipFree(h->d_off);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
+}
+
+static hipError_t sync_handle_streams(llsr_handle* h) {
+  for (hipStream_t st : {h->stream, h->last_stream, h->s2s.last, h->mo.last}) {
+    if (!st) continue;
+    const hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 extern "C" const char* llsr_last_error(const llsr_handle* h) { return h ? h->err.c_str() : "null handle"; }
@@ -393,6 +414,9 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   if (B < 1 || B > h->max_batch) return fail(h, LLSR_ERANGE, "batch size outside [1, max_batch]");
   HIP_OK(h, hipSetDevice(h->device));
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+  // the slot buffers and the FA carry-over state are shared by every batch of this handle: a
+  // batch on another stream than the previous one starts after it
+  if (h->last_stream && h->last_stream != s) HIP_OK(h, hipStreamWaitEvent(s, h->last_done, 0));
   const DevCfg& c = h->dc;
   const float4* pts = reinterpret_cast<const float4*>(d_xyzi);
   int k = 0;
@@ -440,6 +464,7 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   else k_dbscan_merge<2048><<<B, 64, 0, s>>>(c, h->d);
   mark();
   HIP_OK(h, hipGetLastError());
+  HIP_OK(h, hipEventRecord(h->last_done, s));
   if (h->profiling) {
     h->ring_head = (h->ring_head + 1) % llsr_handle::kRing;
     h->ring_used += 1;
@@ -607,7 +632,7 @@ extern "C" int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t P, int32_t mc, 
   auto& m = h->mo;
   if (m.pool && P <= m.P && mc <= m.mc && ms <= m.ms && qc <= m.qc && qs <= m.qs) return LLSR_OK;
   if (m.pool) {
-    HIP_OK(h, hipDeviceSynchronize());
+    HIP_OK(h, sync_handle_streams(h));
     HIP_OK(h, hipFree(m.pool));
     m.pool = nullptr;
   }
@@ -702,6 +727,7 @@ extern "C" int32_t llsr_scan2map_batch(llsr_handle* h, const llsr_s2m_batch* b, 
   if (h->profiling && m.pool) HIP_OK(h, hipEventRecord(m.p0, s));
   S2MArgs a{};
   m.sh_live = false;  // one scan-to-map batch per handle at a time: this one replaces a shard batch
+  m.last = s;
   int32_t rc = s2m_prepare(h, b, s, a);
   if (rc != LLSR_OK) return rc;
   const int P = a.P;
@@ -749,6 +775,7 @@ extern "C" int32_t llsr_scan2map_shard_begin(llsr_handle* h, const llsr_s2m_batc
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
   auto& m = h->mo;
   m.sh_live = false;
+  m.last = s;
   int32_t rc = s2m_prepare(h, b, s, m.sh);
   if (rc != LLSR_OK) return rc;
   m.sh_live = true;
@@ -789,7 +816,9 @@ extern "C" int32_t llsr_scan2map_shard_step(llsr_handle* h, const int64_t* d_ne,
   if (n_active) {
     HIP_OK(h, hipMemcpyAsync(m.host_flags, a.n_active, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_OK(h, hipStreamSynchronize(s));
-    if (m.host_flags[1]) return fail(h, LLSR_ERANGE, "a scan2map cloud exceeds the reserved capacity or has bad offsets");
+    if (m.host_flags[1] & 1) return fail(h, LLSR_ERANGE, "a scan2map cloud exceeds the reserved capacity or has bad offsets");
+    if (m.host_flags[1] & 2)
+      return fail(h, LLSR_ERANGE, "a normal-equation term is non-finite or outside the fixed-point range (|v| >= 2^32)");
     *n_active = m.host_flags[0];
   }
   return LLSR_OK;
@@ -904,7 +933,7 @@ extern "C" int32_t llsr_scan2scan_reserve(llsr_handle* h, int32_t P, int32_t ms,
   auto& m = h->s2s;
   if (m.pool && P <= m.P && ms <= m.ms && f <= m.f && nc <= m.nc && ns <= m.ns) return LLSR_OK;
   if (m.pool) {
-    HIP_OK(h, hipDeviceSynchronize());
+    HIP_OK(h, sync_handle_streams(h));
     HIP_OK(h, hipFree(m.pool));
     m.pool = nullptr;
   }
@@ -913,7 +942,7 @@ extern "C" int32_t llsr_scan2scan_reserve(llsr_handle* h, int32_t P, int32_t ms,
   const size_t Tc = (size_t)1 << lc, Ts = (size_t)1 << ls;
   const size_t capq = (size_t)(ms > f ? ms : f) + 1;
   const size_t bytes = sizeof(CellSlot) * P * (Tc + Ts) + (sizeof(float4) + sizeof(int2)) * P * ((size_t)nc + ns) +
-                       sizeof(int) * 2 * P + (3 * sizeof(int) + sizeof(float4)) * P * capq + 64 + 12 * 256;
+                       sizeof(int) * 2 * P + (3 * sizeof(int) + sizeof(float4) + 1) * P * capq + 64 + 13 * 256;
   if (hipMalloc(&m.pool, bytes) != hipSuccess) {
     m.pool = nullptr;
     m.P = 0;
@@ -936,6 +965,7 @@ extern "C" int32_t llsr_scan2scan_reserve(llsr_handle* h, int32_t P, int32_t ms,
   gc.log2T = lc; gs.log2T = ls;
   a.idx = carve<int>(q, 3 * (size_t)P * capq);
   a.rows = carve<float4>(q, (size_t)P * capq);
+  a.valid = carve<uint8_t>(q, (size_t)P * capq);
   a.error = carve<int>(q, 1);
   a.cap_sharp = ms;
   a.cap_flat = f;
@@ -1201,6 +1231,7 @@ extern "C" int32_t llsr_odometry_batch(llsr_handle* h, const float* d_xyzi, cons
   if (rc != LLSR_OK) return rc;
   k_odo_finish<<<B, 256, 0, s>>>(a);
   HIP_OK(h, hipGetLastError());
+  HIP_OK(h, hipEventRecord(h->last_done, s));
   o.cur = nxt;
   h->last_stream = s;
   return LLSR_OK;

@@ -352,6 +352,7 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
   __shared__ float sums[12];
   __shared__ int isDeg, stop, n_corr[2], iters[2];
   __shared__ float4 lrows[kLdsRows];
+  __shared__ uint8_t lvalid[kLdsRows];
   __shared__ float4 lcl[kLdsCorner];
   __shared__ int fbq[kFbMax], nfb, nvalid;
   __shared__ float red_d[kMulti][kThreads / 64];
@@ -387,12 +388,14 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
     const int capq = a.cap_sharp > a.cap_flat ? a.cap_sharp : a.cap_flat;
     int* idx = a.idx + (size_t)p * capq * 3;
     float4* grows = a.rows + (size_t)p * capq;
+    uint8_t* gvalid = a.valid + (size_t)p * capq;
     for (int phase = 0; phase < 2; ++phase) {  // 0: surf (FA:2508-2516), 1: corner (FA:2519-2527)
       const bool surf = phase == 0;
       const float4* qry = surf ? a.flat + f0 : a.sharp + ms0;
       const int Q = surf ? F : Ms;
       // the rows of this phase: LDS when they fit (phase B re-reads them serially every iteration)
       float4* rows = Q <= kLdsRows ? lrows : grows;
+      uint8_t* vf = Q <= kLdsRows ? lvalid : gvalid;  // row q holds a correspondence (laserCloudOri order)
       if (tid == 0)
         for (int k = 0; k < 9; ++k) matP[k] = (k % 4 == 0) ? 1.0f : 0.0f;
       __syncthreads();
@@ -530,6 +533,7 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
             }
           }
           rows[q] = row;
+          vf[q] = valid ? 1 : 0;
           nval += valid ? 1 : 0;
         }
         if (nval) atomicAdd(&nvalid, nval);
@@ -537,25 +541,37 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
         if (it % 5 == 0 && surf) LLSR_STAMP(tAks);
         else if (it % 5 == 0) LLSR_STAMP(tAkc);
         else LLSR_STAMP(tA);
-        // ---- B: AtA / AtB summed in correspondence order, one lane per entry ----
+        // ---- B: AtA / AtB as Eigen evaluates matAt * matA and matAt * matB (FA:1953-1955) ----
+        // Lane r + 3c sums AtA(r, c), lanes 9..11 AtB: the products of two components of each
+        // correspondence's row in correspondence order. matAt * matA is Eigen's GEMM: each depth
+        // block of kc rows (llsr_eigen::gemm_kc) is summed from zero and added to the result; below
+        // N + 6 < 20 it is the lazy coefficient product, and matAt * matB always is (a sum that
+        // starts from the first product). Rows without a correspondence are skipped.
         if (tid < 12) {
-          // lane r + 3c sums AtA(r, c), lanes 9..11 AtB: the products of two components of each
-          // row in correspondence order (FA:1915-1923 / 2064-2072). A row without a correspondence
-          // is all zeros, and adding +0 leaves the sum bit-identical (a sum started at +0 is never
-          // -0), so the loop needs no test; rows are read 8 at a time.
           const int ra = tid < 9 ? tid % 3 : tid - 9, rb = tid < 9 ? tid / 3 : 3;
           const float* rf = reinterpret_cast<const float*>(rows);
-          float acc = 0.0f;
-          int q = 0;
-          for (; q + 8 <= Q; q += 8) {
-            float u0[8], u1[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) { u0[u] = rf[4 * (q + u) + ra]; u1[u] = rf[4 * (q + u) + rb]; }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) acc += u0[u] * u1[u];
+          const int N = nvalid;
+          const bool lazy = tid >= 9 || N + 6 < 20;
+          const int kc = lazy ? 0x7fffffff : llsr_eigen::gemm_kc(N, 3, 3);
+          float tot = 0.0f, c = 0.0f;
+          int cnt = 0;
+          bool first = true;
+          for (int q = 0; q < Q; ++q) {
+            if (!vf[q]) continue;
+            const float pr = rf[4 * q + ra] * rf[4 * q + rb];
+            if (lazy) {
+              c = first ? pr : c + pr;
+              first = false;
+            } else {
+              c = c + pr;
+              if (++cnt == kc) {
+                tot = tot + 1.0f * c;
+                c = 0.0f;
+                cnt = 0;
+              }
+            }
           }
-          for (; q < Q; ++q) acc += rf[4 * q + ra] * rf[4 * q + rb];
-          sums[tid] = acc;
+          sums[tid] = lazy ? c : (cnt ? tot + 1.0f * c : tot);
         }
         __syncthreads();
         LLSR_STAMP(tB);
@@ -584,16 +600,13 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
                 }
               }
               isDeg = deg;
-              for (int r = 0; r < 3; ++r)  // matV.inverse() * matV2, V orthonormal: V^T * V2
-                for (int c = 0; c < 3; ++c) {
-                  float acc = 0;
-                  for (int k = 0; k < 3; ++k) acc += V[k + 3 * r] * V2[k + 3 * c];
-                  matP[r + 3 * c] = acc;
-                }
+              float Vi[9];
+              llsr_eigen::inverse3(V, Vi);         // matV.inverse(): cofactors (FA:1983 / 2118)
+              llsr_eigen::prod33(Vi, V2, matP);    // matP = matV.inverse() * matV2
             }
-            if (isDeg) {
+            if (isDeg) {  // matX = matP * matX2 (FA:1986-1990 / 2121-2125)
               const float X2[3] = {X[0], X[1], X[2]};
-              for (int r = 0; r < 3; ++r) X[r] = matP[r] * X2[0] + matP[r + 3] * X2[1] + matP[r + 6] * X2[2];
+              llsr_eigen::prod31(matP, X2, X);
             }
             const float r2d = (float)(180.0 / 3.14159265358979323846);  // FA:56
             double dR, dT;

@@ -114,24 +114,26 @@ __global__ __launch_bounds__(256) void k_project(DevCfg c, const float4* __restr
                                                  const int64_t* __restrict__ off, DevBufs d) {
   const int b = blockIdx.y;
   const int64_t o0 = off[b], n = off[b + 1] - o0;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if ((int64_t)blockIdx.x * blockDim.x >= n) return;
-  bool fin = false;
-  if (i < n) {
-    const float4 p = pts[o0 + i];
-    fin = finite3(p);
-    if (fin) {
-      const int cell = project_cell_any(c, p, 1.0f / c.ip_resY, 1.0f / c.ip_resX);
-      if (cell >= 0) atomicMax(&d.cell_pt[(size_t)b * c.HW + cell], i);
+  // grid-stride over the scan: every raw point is projected whatever the grid's width
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = base + threadIdx.x;
+    bool fin = false;
+    if (i < n) {
+      const float4 p = pts[o0 + i];
+      fin = finite3(p);
+      if (fin) {
+        const int cell = project_cell_any(c, p, 1.0f / c.ip_resY, 1.0f / c.ip_resX);
+        if (cell >= 0) atomicMax(&d.cell_pt[(size_t)b * c.HW + cell], (int)i);
+      }
     }
-  }
-  const unsigned long long m = __ballot(fin);
-  if (lane_id() == 0 && m) {
-    int* cnt = d.counts + b * kCnt;
-    atomicAdd(&cnt[C_NPTS], (int)__popcll(m));
-    const int base = blockIdx.x * blockDim.x + (threadIdx.x & ~63);
-    atomicMin(&cnt[C_FIRST], base + (int)__ffsll((long long)m) - 1);
-    atomicMax(&cnt[C_LAST], base + 63 - (int)__clzll((long long)m));
+    const unsigned long long m = __ballot(fin);
+    if (lane_id() == 0 && m) {
+      int* cnt = d.counts + b * kCnt;
+      atomicAdd(&cnt[C_NPTS], (int)__popcll(m));
+      const int wb = (int)(base + (threadIdx.x & ~63));
+      atomicMin(&cnt[C_FIRST], wb + (int)__ffsll((long long)m) - 1);
+      atomicMax(&cnt[C_LAST], wb + 63 - (int)__clzll((long long)m));
+    }
   }
 }
 

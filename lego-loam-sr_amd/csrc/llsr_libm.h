@@ -9,6 +9,19 @@
 // produce identical bits on the host (g++ -ffp-contract=off) and on gfx950 (hipcc
 // -ffp-contract=off, correctly-rounded f32 divide/sqrt — hipcc's default).
 //
+// The float ports below follow fdlibm as shipped in glibc's sysdeps/ieee754/flt-32 (e_asinf.c,
+// e_acosf.c, e_atan2f.c, s_atanf.c, k_tanf.c, s_tanf.c: "Conversion to float by Ian Lance Taylor,
+// Cygnus Support, ian@cygnus.com"), whose notice is preserved as its licence requires:
+//
+//   ====================================================
+//   Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+//
+//   Developed at SunPro, a Sun Microsystems, Inc. business.
+//   Permission to use, copy, modify, and distribute this
+//   software is freely granted, provided that this notice
+//   is preserved.
+//   ====================================================
+//
 // Validation: oracle/libm_check.cpp compares every function against the host glibc over all
 // 2^32 float inputs (asinf, acosf, atanf; tanf, sinf, cosf on |x| < 120) and over dense
 // random/structured pairs for atan2f. See DESIGN.md §2.

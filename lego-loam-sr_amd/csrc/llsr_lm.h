@@ -1,9 +1,7 @@
-// llsr_lm.h — LMOptimization's solve / degeneracy / pose update / stop test (MO:1453-1568) on
+// llsr_lm.h — LMOptimization's solve / degeneracy / pose update / stop test (MO:1505-1568) on
 // already-summed normal equations, and the int64 fixed-point words that the split-correspondence
-// scan-to-map sums across GPUs.
-//
-// Shared by the device (llsr_mo.hip: every scan-to-map path) and the oracle's split-sum
-// restatement (oracle/oracle_mo.cpp), so the step after the sums is one piece of code.
+// scan-to-map sums across GPUs. Device code (llsr_mo.hip); the oracle restates the
+// same step independently (oracle/oracle_mo.cpp mo_lm_solve / ofx).
 #pragma once
 #include <stdint.h>
 
@@ -13,20 +11,26 @@
 namespace llsr_lm {
 
 // Words per problem of the reduced normal equations: AtA upper triangle (21, row-major r <= c),
-// AtB (6), sum |coeff.intensity| (1), #corner, #surf correspondences (2), 2 spare.
+// AtB (6), sum |coeff.intensity| (1), #corner, #surf correspondences (2), 1 spare, and word 31 =
+// the number of terms that were out of the fixed-point range (non-finite or |v| >= 2^32).
 constexpr int kNeWords = 32;
 constexpr int kRed = 30;
+constexpr int kNeOverflow = 31;
 
 // Fixed point for the exchanged sums: every per-correspondence term is rounded once to a
 // multiple of 2^-30 and the sums are plain int64 additions — associative, so any split of the
-// correspondences over blocks / GPUs and any all-reduce order give identical words. Headroom:
-// sum |term| < 2^33 (e.g. 20k correspondences with |J|^2 up to 4e5, points ~600 m away).
+// correspondences over blocks / GPUs and any all-reduce order give identical words. Range: a
+// term with |v| < 2^32 is at most 2^62 in the word; the sums are exact while the total stays below
+// 2^63, i.e. sum |term| < 2^33 (e.g. 20k correspondences with |J|^2 up to 4e5, points ~600 m
+// away). A term outside |v| < 2^32 (or NaN / inf) contributes 0 and is counted in word 31, which
+// the solve step turns into an error instead of a silently wrong pose.
 constexpr double kNeScale = 1073741824.0;  // 2^30
-
-LLSR_HD long long ne_fix(float v) { return (long long)__builtin_rint((double)v * kNeScale); }
+LLSR_HD bool ne_in_range(float v) { return llsr_libm::fabs_(v) < 4294967296.0f; }  // false for NaN
+LLSR_HD long long ne_fix(float v) { return ne_in_range(v) ? (long long)__builtin_rint((double)v * kNeScale) : 0; }
 LLSR_HD float ne_unfix(long long w) { return (float)((double)w / kNeScale); }
 // Word k of one correspondence: the counts (28, 29) stay plain integers.
 LLSR_HD long long ne_term(int k, float v) { return k >= 28 ? (long long)v : ne_fix(v); }
+LLSR_HD int ne_bad(int k, float v) { return (k < 28 && !ne_in_range(v)) ? 1 : 0; }
 
 // Summed words -> the float reduction vector lm_update consumes.
 LLSR_HD void ne_to_red(const long long* w, float* red) {
@@ -35,10 +39,11 @@ LLSR_HD void ne_to_red(const long long* w, float* red) {
   red[29] = (float)w[29];
 }
 
-// One LMOptimization after the Jacobian build (MO:1453-1568) for a problem whose N = nc + ns
+// One LMOptimization after the Jacobian build (MO:1505-1568) for a problem whose N = nc + ns
 // >= 50 (the caller checks MO:1453). St provides pose[6], cR/sR/cP/sP/cY/sY (cached cos / sin
-// of pose[0..2]), matP[36], matX0[6], min_lambda, cf_mean, degenerate. `red`: AtA upper
-// triangle (21), AtB (6), sum |d|, #corner, #surf. Returns the stop test (MO:1562-1566).
+// of pose[0..2]), matP[36], matX0[6], min_lambda, cf_mean, degenerate — matP and degenerate are
+// MapOptimization members (mapOptimization.h:279-281): set at iteration 0 and reused after.
+// `red`: AtA upper triangle (21), AtB (6), sum |d|, #corner, #surf. Returns the stop test.
 template <class St>
 LLSR_HD bool lm_update(St& st, const float* red, int iterCount, bool applied, float stop_thres) {
   using llsr_libm::cosf_;
@@ -50,9 +55,9 @@ LLSR_HD bool lm_update(St& st, const float* red, int iterCount, bool applied, fl
     for (int c = r; c < 6; ++c, ++q) { AtA[r + 6 * c] = red[q]; AtA[c + 6 * r] = red[q]; }
   for (int c = 0; c < 6; ++c) AtB[c] = red[21 + c];
   float X[6];
-  llsr_eigen::colpiv_qr_solve<6, 6>(AtA, AtB, X);
-  if (iterCount == 0) {  // MO:1507-1537
-    float E[6], V[36], V2[36];
+  llsr_eigen::colpiv_qr_solve<6, 6>(AtA, AtB, X);  // matAtA.colPivHouseholderQr().solve(matAtB)
+  if (iterCount == 0) {  // MO:1507-1531
+    float E[6], V[36], V2[36], Vi[36];
     llsr_eigen::eig_sym<6>(AtA, E, V);
     st.min_lambda = E[0];
     for (int k = 0; k < 36; ++k) V2[k] = V[k];
@@ -66,22 +71,14 @@ LLSR_HD bool lm_update(St& st, const float* red, int iterCount, bool applied, fl
       }
     }
     st.degenerate = deg ? 1 : 0;
-    for (int r = 0; r < 6; ++r)  // matV.inverse() * matV2, V orthonormal: V^T * V2
-      for (int c = 0; c < 6; ++c) {
-        float acc = 0;
-        for (int k = 0; k < 6; ++k) acc += V[k + 6 * r] * V2[k + 6 * c];
-        st.matP[r + 6 * c] = acc;
-      }
+    llsr_eigen::inverse_lu<6>(V, Vi);      // matV.inverse() (PartialPivLU)
+    llsr_eigen::prod66(Vi, V2, st.matP);   // matP = matV.inverse() * matV2
     for (int k = 0; k < 6; ++k) st.matX0[k] = X[k];
   }
-  if (st.degenerate) {
+  if (st.degenerate) {  // MO:1533-1536
     float X2[6];
     for (int k = 0; k < 6; ++k) X2[k] = X[k];
-    for (int r = 0; r < 6; ++r) {
-      float acc = 0;
-      for (int k = 0; k < 6; ++k) acc += st.matP[r + 6 * k] * X2[k];
-      X[r] = acc;
-    }
+    llsr_eigen::prod61(st.matP, X2, X);
   }
   if (applied) {  // MO:1539-1545 (commented out in the reference: faithful mode skips it)
     for (int k = 0; k < 6; ++k) st.pose[k] += X[k];

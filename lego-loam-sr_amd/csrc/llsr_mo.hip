@@ -321,21 +321,28 @@ template <bool kCorner>
 __device__ __forceinline__ void s2m_block_fx(const S2MArgs& a, int p, int qb) {
   const S2MProb& st = a.prob[p];
   if (!st.active) return;
-  __shared__ long long wsum[4][kRed];
+  __shared__ long long wsum[4][kRed + 1];
   float v[kRed];
   query_terms<kCorner>(a, st, p, qb * 256 + threadIdx.x, v);
   const int w = threadIdx.x >> 6;
+  int bad = 0;  // terms outside the fixed-point range: contribute 0, counted in word 31
 #pragma unroll
   for (int k = 0; k < kRed; ++k) {
+    bad += llsr_lm::ne_bad(k, v[k]);
     const long long s = wave_reduce_add(llsr_lm::ne_term(k, v[k]));
     if (lane_id() == 0) wsum[w][k] = s;
   }
+  {
+    const long long s = wave_reduce_add((long long)bad);
+    if (lane_id() == 0) wsum[w][kRed] = s;
+  }
   __syncthreads();
-  if (threadIdx.x < kRed) {
+  if (threadIdx.x <= kRed) {
     const int k = threadIdx.x;
     const long long t = wsum[0][k] + wsum[1][k] + wsum[2][k] + wsum[3][k];
+    const int word = k < kRed ? k : llsr_lm::kNeOverflow;
     if (t != 0)
-      atomicAdd(reinterpret_cast<unsigned long long*>(a.ne + (size_t)p * llsr_lm::kNeWords + k),
+      atomicAdd(reinterpret_cast<unsigned long long*>(a.ne + (size_t)p * llsr_lm::kNeWords + word),
                 (unsigned long long)t);
   }
 }
@@ -357,8 +364,10 @@ __global__ __launch_bounds__(64) void k_s2m_solve_fx(S2MArgs a) {
   if (p >= a.P) return;
   S2MProb& st = a.prob[p];
   if (!st.active) return;
+  const long long* w = a.ne + (size_t)p * llsr_lm::kNeWords;
+  if (w[llsr_lm::kNeOverflow] != 0) atomicOr(a.error, 2);  // reported by llsr_scan2map_shard_step
   float red[kRed];
-  llsr_lm::ne_to_red(a.ne + (size_t)p * llsr_lm::kNeWords, red);
+  llsr_lm::ne_to_red(w, red);
   lm_step(a, st, red);
 }
 

@@ -64,7 +64,7 @@ void oracle_transform_to_end(const float* transform_cur, float* xyzi, int32_t n)
 void oracle_integrate_transformation(float* transform_sum, const float* transform_cur);
 /* GenerateShadowPoint (FA:412-439). */
 void oracle_shadow_points(float* out_xyzi);
-/* Test hooks for the Eigen restatements (llsr_eigen.h): column-major inputs. */
+/* Test hooks for the oracle's Eigen 3.3.7 restatement (oracle_eigen.h): column-major inputs. */
 int32_t oracle_eig3(const float* A, float* evals, float* evecs);
 int32_t oracle_eig6(const float* A, float* evals, float* evecs);
 void oracle_qr_solve_5x3(const float* A, const float* b, float* x);

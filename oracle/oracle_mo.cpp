@@ -8,8 +8,8 @@
 // matter: a correspondence is kept only when the 5th nearest squared distance is < 1.0, so the
 // search is a 1 m uniform grid over the 27 neighbouring cells; squared distances accumulate as
 // ((0 + dx^2) + dy^2) + dz^2 (nanoflann.hpp:431-439, L2_Simple_Adaptor behind the SO3_Adaptor of
-// nanoflann_pcl.h) and equal distances keep the lower index. Eigen calls use
-// lego-loam-sr_amd/csrc/llsr_eigen.h.
+// nanoflann_pcl.h) and equal distances keep the lower index. Eigen calls go through the oracle's
+// own restatement (oracle_eigen.h), independent of the device's.
 //
 // Built a second time by oracle/Makefile with -DLLSR_ORACLE_NANOFLANN against the reference's
 // own vendored kd-tree (LeGO-LOAM/include/lego_loam/nanoflann.hpp, included by path, std-only;
@@ -23,9 +23,8 @@
 #include <vector>
 
 #include "../include/llsr.h"
-#include "../lego-loam-sr_amd/csrc/llsr_eigen.h"
-#include "../lego-loam-sr_amd/csrc/llsr_lm.h"
 #include "oracle.h"
+#include "oracle_eigen.h"
 #ifdef LLSR_ORACLE_NANOFLANN
 #include "nanoflann.hpp"
 #endif
@@ -118,7 +117,6 @@ struct Coeff { P4 ori; float cx, cy, cz, ci; };
 // cornerOptimization body (MO:1274-1375) for one map-frame query point; false when rejected.
 bool corner_coeff(const Knn& gc, const P4* cornerM, const P4& sel_p, float& la_, float& lb_, float& lc_,
                   float& ld_) {
-  using namespace llsr_eigen;
   int idx[5];
   float d2[5];
   if (gc.knn5(sel_p, idx, d2) < 5) return false;
@@ -133,7 +131,7 @@ bool corner_coeff(const Knn& gc, const P4* cornerM, const P4& sel_p, float& la_,
   a11 /= 5; a12 /= 5; a13 /= 5; a22 /= 5; a23 /= 5; a33 /= 5;
   const float A1[9] = {a11, a12, a13, a12, a22, a23, a13, a23, a33};  // column-major
   float D1[3], V1[9];
-  eig3(A1, D1, V1);
+  oeig::eig_sym3(A1, D1, V1);
   if (!(D1[2] > 3 * D1[1])) return false;
   const float x0 = sel_p.x, y0 = sel_p.y, z0 = sel_p.z;
   // ROW 0 of matV1: V(0,0), V(0,1), V(0,2) (column-major: [0], [3], [6])
@@ -158,7 +156,6 @@ bool corner_coeff(const Knn& gc, const P4* cornerM, const P4& sel_p, float& la_,
 
 // surfOptimization body (MO:1383-1440) for one map-frame query point; false when rejected.
 bool surf_coeff(const Knn& gs, const P4* surfM, const P4& sel_p, float& la_, float& lb_, float& lc_, float& ld_) {
-  using namespace llsr_eigen;
   int idx[5];
   float d2[5];
   if (gs.knn5(sel_p, idx, d2) < 5) return false;
@@ -166,7 +163,7 @@ bool surf_coeff(const Knn& gs, const P4* surfM, const P4& sel_p, float& la_, flo
   for (int j = 0; j < 5; ++j) { A0[j] = surfM[idx[j]].x; A0[5 + j] = surfM[idx[j]].y; A0[10 + j] = surfM[idx[j]].z; }
   const float B0[5] = {-1, -1, -1, -1, -1};
   float X0[3];
-  colpiv_qr_solve<5, 3>(A0, B0, X0);
+  oeig::colpiv_qr_solve(A0, 5, 3, B0, X0);  // matA0.colPivHouseholderQr().solve(matB0)
   float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1;
   const float ps = std::sqrt(pa * pa + pb * pb + pc * pc);
   pa /= ps; pb /= ps; pc /= ps; pd /= ps;
@@ -218,13 +215,57 @@ void jacobian_row(const float* t, const Coeff& co, float* a) {
   a[5] = co.cz;
 }
 
+// LMOptimization from the solve to the degeneracy projection (MO:1505-1537), on the assembled
+// normal equations. matP / isDegenerate are MapOptimization members (mapOptimization.h:279-281,
+// zeroed at construction MO:285-286): set at iteration 0, reused by the later iterations.
+struct MoLm {
+  bool isDegenerate = false;
+  float matP[36] = {0};
+  float min_lambda = 0.0f;
+  float matX0[6] = {0};
+};
+void mo_lm_solve(MoLm& s, const float* AtA, const float* AtB, int iterCount, float* X) {
+  oeig::colpiv_qr_solve(AtA, 6, 6, AtB, X);
+  if (iterCount == 0) {
+    float E[6], V[36], V2[36], Vi[36];
+    oeig::eig_sym_n(AtA, 6, E, V);
+    s.min_lambda = E[0];
+    std::memcpy(V2, V, sizeof V2);
+    s.isDegenerate = false;
+    const float eignThre[6] = {100, 100, 100, 100, 100, 100};
+    for (int i = 5; i >= 0; --i) {
+      if (E[i] < eignThre[i]) {
+        for (int j = 0; j < 6; ++j) V2[i + 6 * j] = 0;  // matV2(i, j): row i (MO:1522-1524)
+        s.isDegenerate = true;
+      } else {
+        break;
+      }
+    }
+    oeig::inverse_lu(V, 6, Vi);       // matV.inverse(): PartialPivLU
+    oeig::prod66(Vi, V2, s.matP);     // matP = matV.inverse() * matV2 (MO:1530)
+    std::memcpy(s.matX0, X, sizeof s.matX0);
+  }
+  if (s.isDegenerate) {
+    float X2[6];
+    std::memcpy(X2, X, sizeof X2);
+    oeig::prod61(s.matP, X2, X);      // matX = matP * matX2 (MO:1533-1536)
+  }
+}
+
+// The stop test (MO:1546-1553): pcl::rad2deg(float), std::pow(float, int) in double.
+bool mo_converged(const float* X, float stop_thres) {
+  const float r2d = 57.29577951308232f;
+  const float deltaR = (float)std::sqrt(std::pow(X[0] * r2d, 2) + std::pow(X[1] * r2d, 2) + std::pow(X[2] * r2d, 2));
+  const float deltaT = (float)std::sqrt(std::pow(X[3] * 100, 2) + std::pow(X[4] * 100, 2) + std::pow(X[5] * 100, 2));
+  return deltaR < stop_thres && deltaT < stop_thres;
+}
+
 }  // namespace
 
 extern "C" int32_t ORACLE_FN(scan2map)(const llsr_config* cfg, const float* cq, int32_t Qc, const float* sq,
                                    int32_t Qs, const float* cm, int32_t Mc, const float* sm, int32_t Ms,
                                    float* pose, llsr_lm_report* rep) {
   if (!cfg || !pose || !rep || Qc < 0 || Qs < 0 || Mc < 0 || Ms < 0) return LLSR_EINVAL;
-  using namespace llsr_eigen;
   const P4* cornerQ = reinterpret_cast<const P4*>(cq);
   const P4* surfQ = reinterpret_cast<const P4*>(sq);
   const P4* cornerM = reinterpret_cast<const P4*>(cm);
@@ -241,11 +282,11 @@ extern "C" int32_t ORACLE_FN(scan2map)(const llsr_config* cfg, const float* cq, 
   gc.build(cornerM, Mc);
   gs.build(surfM, Ms);
   const bool applied = cfg->mode == LLSR_MODE_LM_APPLIED;
-  bool isDegenerate = false;
-  float matP[36] = {0};
-  float min_lambda = 0.0f, CF_mean = 0.0f;
+  MoLm lm;
+  float CF_mean = 0.0f;
   int iters = 0, converged = 0, nc = 0, ns = 0;
   std::vector<Coeff> sel;
+  std::vector<float> rows, bv;
   for (int iterCount = 0; iterCount < cfg->iterCountThres; ++iterCount) {
     sel.clear();
     ++iters;
@@ -265,61 +306,26 @@ extern "C" int32_t ORACLE_FN(scan2map)(const llsr_config* cfg, const float* cq, 
     // ---- LMOptimization (MO:1444-1570) ----
     const int N = (int)sel.size();
     if (N < 50) continue;  // returns false: not converged, no update
-    float AtA[36] = {0}, AtB[6] = {0};
+    rows.resize((size_t)6 * N);
+    bv.resize(N);
     for (int i = 0; i < N; ++i) {
-      float a[6];
-      jacobian_row(t, sel[i], a);
-      const float bb = -cfg->step_size * sel[i].ci;
-      for (int c = 0; c < 6; ++c) {
-        for (int r = 0; r < 6; ++r) AtA[r + 6 * c] += a[r] * a[c];
-        AtB[c] += a[c] * bb;
-      }
+      jacobian_row(t, sel[i], &rows[(size_t)6 * i]);
+      bv[i] = -cfg->step_size * sel[i].ci;  // matB(i, 0) = -step_size * coeff.intensity
     }
-    float X[6];
-    colpiv_qr_solve<6, 6>(AtA, AtB, X);
-    if (iterCount == 0) {
-      float E[6], V[36];
-      eig_sym<6>(AtA, E, V);
-      min_lambda = E[0];
-      float V2[36];
-      std::memcpy(V2, V, sizeof V2);
-      isDegenerate = false;
-      for (int i = 5; i >= 0; --i) {
-        if (E[i] < 100) {
-          for (int j = 0; j < 6; ++j) V2[i + 6 * j] = 0;  // matV2(i, j): row i (MO:1522-1524)
-          isDegenerate = true;
-        } else {
-          break;
-        }
-      }
-      // matP = matV.inverse() * matV2; V is orthonormal up to rounding: inverse ~ transpose
-      for (int r = 0; r < 6; ++r)
-        for (int c = 0; c < 6; ++c) {
-          float acc = 0;
-          for (int k = 0; k < 6; ++k) acc += V[k + 6 * r] * V2[k + 6 * c];
-          matP[r + 6 * c] = acc;
-        }
-      std::memcpy(rep->matX0, X, sizeof X);
-    }
-    if (isDegenerate) {
-      float X2[6];
-      std::memcpy(X2, X, sizeof X2);
-      for (int r = 0; r < 6; ++r) {
-        float acc = 0;
-        for (int k = 0; k < 6; ++k) acc += matP[r + 6 * k] * X2[k];
-        X[r] = acc;
-      }
-    }
+    float AtA[36], AtB[6], X[6];
+    oeig::gemm_ata(rows.data(), N, 6, AtA);  // matAtA = matAt * matA (GEMM)
+    oeig::gemv_atb(rows.data(), bv.data(), N, 6, AtB);
+    mo_lm_solve(lm, AtA, AtB, iterCount, X);
+    if (iterCount == 0) std::memcpy(rep->matX0, lm.matX0, sizeof lm.matX0);
     if (applied)
       for (int k = 0; k < 6; ++k) t[k] += X[k];
-    const float r2d = 57.29577951308232f;  // pcl::rad2deg(float)
-    const float deltaR = (float)std::sqrt(std::pow(X[0] * r2d, 2) + std::pow(X[1] * r2d, 2) + std::pow(X[2] * r2d, 2));
-    const float deltaT = (float)std::sqrt(std::pow(X[3] * 100, 2) + std::pow(X[4] * 100, 2) + std::pow(X[5] * 100, 2));
     float CF_all = 0;
     for (int i = 0; i < N; ++i) CF_all += std::fabs(sel[i].ci);
     CF_mean = CF_all / N;
-    if (deltaR < cfg->stop_thres && deltaT < cfg->stop_thres) { converged = 1; break; }
+    if (mo_converged(X, cfg->stop_thres)) { converged = 1; break; }
   }
+  const bool isDegenerate = lm.isDegenerate;
+  const float min_lambda = lm.min_lambda;
   auto t1 = std::chrono::steady_clock::now();
   rep->iterations = iters;
   rep->converged = converged;
@@ -335,23 +341,33 @@ extern "C" int32_t ORACLE_FN(scan2map)(const llsr_config* cfg, const float* cq, 
 }
 
 // ---- split-correspondence scan-to-map, int64 fixed-point sums (llsr_scan2map_shard_*) -------
-// The CPU statement of what the device's split mode computes: per LM iteration every rank sums
-// the fixed-point terms (llsr_lm::ne_term) of its 256-query blocks (block b of each kind goes to
-// rank b % world), the ranks' words are added, and llsr_lm::lm_update — the device's own step —
-// runs on the total. Used by the gloo tests as a rank's engine and by the GPU tests as the
-// bit-exact reference for the device's split mode.
+// The CPU statement of the split mode, written independently of the
+// device: per LM iteration every rank sums the fixed-point terms of its 256-query blocks (block b
+// of each kind goes to rank b % world), the ranks' words are added, and the LMOptimization tail
+// (mo_lm_solve above: QR, eigen, PartialPivLU inverse, projection) runs on the total. Used by the
+// gloo tests as a rank's engine and by the GPU tests as the bit-exact reference for the device's
+// split mode. Word layout (LLSR_NE_WORDS = 32): AtA upper triangle row-major (21), AtB (6),
+// sum |coeff.intensity|, #corner, #surf, 2 spare. A term is round-to-nearest-even(v * 2^30) as an
+// int64; a non-finite term or one with |v| >= 2^32 is counted in word 31 and contributes 0.
+namespace ofx {
+constexpr int kWords = LLSR_NE_WORDS;
+constexpr double kScale = 1073741824.0;  // 2^30
+inline void add_term(int64_t* ne, int k, float v) {
+  if (k >= 28) { ne[k] += (int64_t)v; return; }
+  if (!(std::fabs(v) < 4294967296.0f)) { ne[31] += 1; return; }
+  ne[k] += (int64_t)std::nearbyint((double)v * kScale);
+}
+inline float word(int64_t w) { return (float)((double)w / kScale); }
+}  // namespace ofx
+
 struct oracle_s2m_shard {
   llsr_config cfg;
   std::vector<P4> cq, sq, cm, sm;
   Knn gc, gs;
-  struct State {
-    float pose[6];
-    float cR, sR, cP, sP, cY, sY;
-    float matP[36];
-    float matX0[6];
-    float min_lambda = 0.0f, cf_mean = 0.0f;
-    int degenerate = 0, iter = 0, active = 0, converged = 0, nc = 0, ns = 0;
-  } st;
+  MoLm lm;
+  float pose[6];
+  float cf_mean = 0.0f;
+  int iter = 0, active = 0, converged = 0, nc = 0, ns = 0;
 };
 
 extern "C" oracle_s2m_shard* ORACLE_FN(s2m_shard_create)(const llsr_config* cfg, const float* cq, int32_t Qc,
@@ -366,15 +382,9 @@ extern "C" oracle_s2m_shard* ORACLE_FN(s2m_shard_create)(const llsr_config* cfg,
   s->sq.assign(p4[1], p4[1] + Qs);
   s->cm.assign(p4[2], p4[2] + Mc);
   s->sm.assign(p4[3], p4[3] + Ms);
-  auto& st = s->st;
-  std::memcpy(st.pose, pose, sizeof st.pose);
-  std::memset(st.matP, 0, sizeof st.matP);
-  std::memset(st.matX0, 0, sizeof st.matX0);
-  st.cR = std::cos(st.pose[0]); st.sR = std::sin(st.pose[0]);
-  st.cP = std::cos(st.pose[1]); st.sP = std::sin(st.pose[1]);
-  st.cY = std::cos(st.pose[2]); st.sY = std::sin(st.pose[2]);
-  st.active = (Mc > 10 && Ms > 100) ? 1 : 0;  // MO:1573
-  if (st.active) {
+  std::memcpy(s->pose, pose, sizeof s->pose);
+  s->active = (Mc > 10 && Ms > 100) ? 1 : 0;  // MO:1573
+  if (s->active) {
     s->gc.build(s->cm.data(), Mc);
     s->gs.build(s->sm.data(), Ms);
   }
@@ -385,21 +395,19 @@ extern "C" void ORACLE_FN(s2m_shard_destroy)(oracle_s2m_shard* s) { delete s; }
 
 // Rank `rank` of `world`: the LLSR_NE_WORDS int64 words of this rank's query blocks.
 extern "C" void ORACLE_FN(s2m_shard_partial)(oracle_s2m_shard* s, int32_t rank, int32_t world, int64_t* ne) {
-  for (int k = 0; k < llsr_lm::kNeWords; ++k) ne[k] = 0;
-  if (!s->st.active || world < 1) return;
-  const float* t = s->st.pose;
+  for (int k = 0; k < ofx::kWords; ++k) ne[k] = 0;
+  if (!s->active || world < 1) return;
+  const float* t = s->pose;
   auto add = [&](const Coeff& co, bool corner) {
     float a[6];
     jacobian_row(t, co, a);
     const float bb = -s->cfg.step_size * co.ci;
-    float v[llsr_lm::kRed] = {0};
     int k = 0;
     for (int r = 0; r < 6; ++r)
-      for (int c = r; c < 6; ++c, ++k) v[k] = a[r] * a[c];
-    for (int c = 0; c < 6; ++c) v[21 + c] = a[c] * bb;
-    v[27] = std::fabs(co.ci);
-    v[corner ? 28 : 29] = 1.0f;
-    for (int q = 0; q < llsr_lm::kRed; ++q) ne[q] += llsr_lm::ne_term(q, v[q]);
+      for (int c = r; c < 6; ++c, ++k) ofx::add_term(ne, k, a[r] * a[c]);
+    for (int c = 0; c < 6; ++c) ofx::add_term(ne, 21 + c, a[c] * bb);
+    ofx::add_term(ne, 27, std::fabs(co.ci));
+    ofx::add_term(ne, corner ? 28 : 29, 1.0f);
   };
   for (int i = 0; i < (int)s->cq.size(); ++i) {
     if ((i / 256) % world != rank) continue;
@@ -415,37 +423,42 @@ extern "C" void ORACLE_FN(s2m_shard_partial)(oracle_s2m_shard* s, int32_t rank, 
 
 // LMOptimization on the summed words of all ranks; returns 1 while the problem is still active.
 extern "C" int32_t ORACLE_FN(s2m_shard_step)(oracle_s2m_shard* s, const int64_t* ne) {
-  auto& st = s->st;
-  if (!st.active) return 0;
-  long long w[llsr_lm::kNeWords];
-  for (int k = 0; k < llsr_lm::kNeWords; ++k) w[k] = (long long)ne[k];
-  float red[llsr_lm::kRed];
-  llsr_lm::ne_to_red(w, red);
-  st.iter += 1;
-  const int iterCount = st.iter - 1;
-  st.nc = (int)red[28];
-  st.ns = (int)red[29];
+  if (!s->active) return 0;
+  s->iter += 1;
+  const int iterCount = s->iter - 1;
+  s->nc = (int)ne[28];
+  s->ns = (int)ne[29];
+  const int N = s->nc + s->ns;
   bool conv = false;
-  if (st.nc + st.ns >= 50)
-    conv = llsr_lm::lm_update(st, red, iterCount, s->cfg.mode == LLSR_MODE_LM_APPLIED, s->cfg.stop_thres);
-  if (conv) st.converged = 1;
-  if (conv || st.iter >= s->cfg.iterCountThres) st.active = 0;
-  return st.active;
+  if (N >= 50) {  // MO:1453
+    float AtA[36], AtB[6], X[6];
+    int k = 0;
+    for (int r = 0; r < 6; ++r)
+      for (int c = r; c < 6; ++c, ++k) AtA[r + 6 * c] = AtA[c + 6 * r] = ofx::word(ne[k]);
+    for (int c = 0; c < 6; ++c) AtB[c] = ofx::word(ne[21 + c]);
+    mo_lm_solve(s->lm, AtA, AtB, iterCount, X);
+    if (s->cfg.mode == LLSR_MODE_LM_APPLIED)
+      for (int q = 0; q < 6; ++q) s->pose[q] += X[q];
+    s->cf_mean = ofx::word(ne[27]) / (float)N;
+    conv = mo_converged(X, s->cfg.stop_thres);
+  }
+  if (conv) s->converged = 1;
+  if (conv || s->iter >= s->cfg.iterCountThres) s->active = 0;
+  return s->active;
 }
 
 extern "C" void ORACLE_FN(s2m_shard_result)(const oracle_s2m_shard* s, float* pose, llsr_lm_report* rep) {
-  const auto& st = s->st;
   std::memset(rep, 0, sizeof *rep);
-  rep->iterations = st.iter;
-  rep->converged = st.converged;
-  rep->degenerate = st.degenerate;
-  rep->min_lambda = st.min_lambda;
-  rep->cf_mean = st.cf_mean;
-  rep->n_corner_corr = st.nc;
-  rep->n_surf_corr = st.ns;
-  std::memcpy(rep->matX0, st.matX0, sizeof st.matX0);
-  std::memcpy(rep->pose, st.pose, sizeof st.pose);
-  std::memcpy(pose, st.pose, sizeof st.pose);
+  rep->iterations = s->iter;
+  rep->converged = s->converged;
+  rep->degenerate = s->lm.isDegenerate ? 1 : 0;
+  rep->min_lambda = s->lm.min_lambda;
+  rep->cf_mean = s->cf_mean;
+  rep->n_corner_corr = s->nc;
+  rep->n_surf_corr = s->ns;
+  std::memcpy(rep->matX0, s->lm.matX0, sizeof s->lm.matX0);
+  std::memcpy(rep->pose, s->pose, sizeof s->pose);
+  std::memcpy(pose, s->pose, sizeof s->pose);
 }
 
 // kNN-5 of Q queries against one map (cross-check hook): idx/d2 [Q][5]; returns #accepted and
@@ -466,8 +479,10 @@ extern "C" int32_t ORACLE_FN(knn5_batch)(const float* map, int32_t M, const floa
 }
 
 #ifndef LLSR_ORACLE_NANOFLANN
-extern "C" int32_t oracle_eig3(const float* A, float* e, float* v) { return llsr_eigen::eig3(A, e, v); }
-extern "C" int32_t oracle_eig6(const float* A, float* e, float* v) { return llsr_eigen::eig_sym<6>(A, e, v); }
-extern "C" void oracle_qr_solve_5x3(const float* A, const float* b, float* x) { llsr_eigen::colpiv_qr_solve<5, 3>(A, b, x); }
-extern "C" void oracle_qr_solve_6x6(const float* A, const float* b, float* x) { llsr_eigen::colpiv_qr_solve<6, 6>(A, b, x); }
+extern "C" int32_t oracle_eig3(const float* A, float* e, float* v) { return oeig::eig_sym3(A, e, v); }
+extern "C" int32_t oracle_eig6(const float* A, float* e, float* v) { return oeig::eig_sym_n(A, 6, e, v); }
+extern "C" void oracle_qr_solve_5x3(const float* A, const float* b, float* x) { oeig::colpiv_qr_solve(A, 5, 3, b, x); }
+extern "C" void oracle_qr_solve_6x6(const float* A, const float* b, float* x) { oeig::colpiv_qr_solve(A, 6, 6, b, x); }
+extern "C" void oracle_inverse3(const float* A, float* inv) { oeig::inverse3(A, inv); }
+extern "C" void oracle_inverse6(const float* A, float* inv) { oeig::inverse_lu(A, 6, inv); }
 #endif

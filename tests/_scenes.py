@@ -1,0 +1,66 @@
+"""Scenes that drive the LMs into their degenerate branch (FA:1959-1990, MO:1507-1537).
+
+The reference scans the eigenvalues from the LARGEST down and stops at the first one above the
+threshold (10 in FA, 100 in MO), so the branch fires only when every eigenvalue of AtA is below
+it: a handful of correspondences on points close to the sensor. Then every row of matV2 is zeroed,
+matP = matV.inverse() * 0 and matX = matP * matX2 are (signed) zeros, the pose does not move and
+the loop stops at iteration 0. These scenes shrink the synthetic street around the sensor (scale
+f) and keep a few queries, which is how the degenerate branch is reached here."""
+import os
+
+import numpy as np
+
+import oracle_py
+from llsr import default_config, synth
+
+FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mo_map_vlp16.npz")
+
+
+def _scaled(a, f):
+    b = np.array(a, np.float32, copy=True)
+    b[:, :3] *= np.float32(f)
+    return b
+
+
+def fa_degenerate_pairs(n=6):
+    """(cfg, [(sharp, flat, corner_last, surf_last, t0)]) whose corner phase is degenerate."""
+    cfg = default_config("vlp16")
+    ora = oracle_py.Oracle(cfg)
+    prev = ora.process(synth.make_scan(1, "vlp16"))
+    cur = ora.process(synth.make_scan(2, "vlp16"))
+    sharp, flat, cl, sl = oracle_py.fa_lm_inputs(prev, cur)
+    out = []
+    for k in range(n):
+        idx = (np.arange(10 + k % 3) * 7 + 3 * k) % len(sharp)
+        t0 = np.array([0.0, 0.03, 0.0, 0.1, 0.0, 0.1], np.float32) * np.float32(k % 2)
+        out.append((_scaled(sharp[idx], 0.1), _scaled(flat, 0.1), _scaled(cl, 0.1), _scaled(sl, 0.1), t0))
+    return cfg, out
+
+
+# (query, offset) pairs of the fixture whose shrunk 10 + 50 query problem is degenerate
+# (found by the oracle; tests/test_degenerate.py re-checks that every one of them is)
+MO_DEGENERATE_CASES = ((0, 0), (0, 12), (1, 16), (1, 20), (2, 4), (2, 8), (3, 12), (3, 28))
+# and a few that are not (the same shrunk scenes): the mix exercises both branches in one batch
+MO_REGULAR_CASES = ((1, 0), (2, 0))
+
+
+def mo_shrunk_problem(z, i, off):
+    tr = z[f"q{i}_true"][3:]
+    cm = np.array(z["corner_map"], np.float32, copy=True)
+    cm[:, :3] = (cm[:, :3] - tr) * np.float32(0.05)
+    sm = np.array(z["surf_map"], np.float32, copy=True)
+    sm[:, :3] = (sm[:, :3] - tr) * np.float32(0.05)
+    cq, sq = _scaled(z[f"q{i}_corner"], 0.05), _scaled(z[f"q{i}_surf"], 0.05)
+    init = np.array(z[f"q{i}_init"], np.float32, copy=True)
+    init[3:] = (init[3:] - tr) * np.float32(0.05)
+    ci = (np.arange(10) * 13 + off) % len(cq)
+    si = (np.arange(50) * 17 + off) % len(sq)
+    return cq[ci], sq[si], cm, sm, init
+
+
+def mo_degenerate_problems(regular=False):
+    """[(corner_q, surf_q, corner_map, surf_map, pose0)]: the committed fixture shrunk 20x around a
+    query's sensor with 10 corner / 50 surf queries (MO_DEGENERATE_CASES, + MO_REGULAR_CASES)."""
+    z = np.load(FIX)
+    cases = MO_DEGENERATE_CASES + (MO_REGULAR_CASES if regular else ())
+    return [mo_shrunk_problem(z, i, off) for i, off in cases]

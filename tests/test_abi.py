@@ -74,3 +74,31 @@ def test_map_create_fails_loudly_without_device():
     assert not llsr.lib().llsr_map_create(None, 0)
     with pytest.raises(llsr.LlsrError):
         llsr.LocalMap(0)
+
+
+@pytest.mark.parametrize("lang,std", [("c", "c99"), ("c++", "c++11")])
+def test_header_is_plain_c_and_cxx(lang, std):
+    """include/llsr.h is the FFI surface (cgo / ctypes / a C++ node): it must parse as strict C99
+    and C++11 with no warnings."""
+    cc = "gcc" if lang == "c" else "g++"
+    subprocess.run([cc, f"-std={std}", "-Wall", "-Wextra", "-pedantic", "-Werror", "-fsyntax-only", "-x", lang,
+                    HEADER], check=True)
+
+
+def test_c99_consumer_compiles_and_links(tmp_path):
+    """A strict-C99 caller links against libllsr.so (tests/native/consumer_c.c; build only)."""
+    exe = str(tmp_path / "consumer_c")
+    libdir = os.path.dirname(llsr.LIB_PATH)
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror", "-I", os.path.join(REPO, "include"),
+                    "-o", exe, os.path.join(REPO, "tests", "native", "consumer_c.c"), "-L", libdir, "-lllsr",
+                    f"-Wl,-rpath,{libdir}"], check=True)
+    assert os.path.exists(exe)
+
+
+def test_cxx_consumer_is_built_in_tree():
+    """The C++ consumer that tests/test_gpu_consumer.py runs on the GPU box is built by build()
+    (lego-loam-sr_amd/Makefile) against the header and resolves libllsr.so."""
+    exe = os.path.join(REPO, "tests", "native", "llsr_consumer")
+    assert os.path.exists(exe)
+    out = subprocess.run(["ldd", exe], check=True, capture_output=True, text=True).stdout
+    assert "libllsr.so" in out and "not found" not in out

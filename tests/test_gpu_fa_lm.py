@@ -119,3 +119,21 @@ def test_scan2scan_capacity_error(require_gpu):
     with pytest.raises(LlsrError):
         pipe.scan2scan_check()
     pipe.close()
+
+
+def test_scan2scan_degenerate_bit_exact(require_gpu):
+    """The degenerate branch (FA:1959-1990: all eigenvalues of the corner phase's AtA below 10,
+    matP = matV.inverse() * matV2 with the cofactor inverse) on shrunk scenes (tests/_scenes.py):
+    device == oracle bit for bit, including the flag."""
+    import _scenes
+    cfg, pairs = _scenes.fa_degenerate_pairs()
+    pipe = Pipeline(cfg)
+    errs, n_deg = [], 0
+    for k, (sharp, flat, cl, sl, t0) in enumerate(pairs):
+        g = pipe.scan2scan(sharp, flat, cl, sl, t0, 0)
+        o = oracle_py.scan2scan(cfg, sharp, flat, cl, sl, t0, 0)
+        n_deg += o["degenerate"]
+        errs += [f"pair {k}: {e}" for e in _same(g, o)]
+    pipe.close()
+    assert n_deg >= 4
+    assert not errs, "\n".join(errs)

@@ -120,3 +120,22 @@ def test_shard_api_errors(require_gpu):
     with pytest.raises(LlsrError):
         pipe.scan2map_shard_step(ne.data_ptr(), True)
     pipe.close()
+
+
+def test_shard_degenerate_bit_exact_vs_oracle(require_gpu):
+    """Split mode on degenerate + regular shrunk problems (tests/_scenes.py): the device's LM step
+    (QR, 6x6 eigen, PartialPivLU inverse, projection — llsr_eigen.h) equals the oracle's independent
+    restatement (oracle_eigen.h) bit for bit, for W = 1 and 3."""
+    import _scenes
+    cfg = default_config("vlp16")
+    cfg.mode = _abi.LLSR_MODE_LM_APPLIED
+    probs = _scenes.mo_degenerate_problems(regular=True)
+    ora = oracle_py.shard_run_local(cfg, probs, 1)
+    assert sum(o["degenerate"] for o in ora) == len(_scenes.MO_DEGENERATE_CASES)
+    errs = []
+    for W in (1, 3):
+        dev = _run_device(cfg, probs, W)
+        for p in range(len(probs)):
+            if not _same(dev[p], ora[p]):
+                errs.append(f"W={W} problem {p}: device {dev[p]} vs oracle split statement {ora[p]}")
+    assert not errs, "\n".join(errs)

@@ -1,5 +1,6 @@
-"""CPU checks of the MapOptimization restatement (oracle/oracle_mo.cpp) and the Eigen 3.3.7
-restatements it shares with the device (lego-loam-sr_amd/csrc/llsr_eigen.h).
+"""CPU checks of the MapOptimization restatement (oracle/oracle_mo.cpp) and the oracle's own
+Eigen 3.3.7 restatement (oracle/oracle_eigen.h; the device's is cross-checked against it bit for
+bit by tests/test_eigen_restatement.py).
 
 Parity status: the reference's scan-to-map cannot run here (ROS2/PCL/GTSAM absent, SURVEY.md
 §8c) and ships no golden vectors for it, so the optimiser itself is "parity unpinned" against
