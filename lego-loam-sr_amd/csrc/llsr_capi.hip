@@ -28,6 +28,7 @@ template <bool kLds> __global__ void k_label(DevCfg, DevBufs);
 __global__ void k_segment(DevCfg, const float4*, const int64_t*, DevBufs);
 __global__ void k_fa_points(DevCfg, DevBufs);
 __global__ void k_select_ring(DevCfg, DevBufs);
+__global__ void k_debug_exact_sort(const float*, int, int*);
 __global__ void k_fa_concat(DevCfg, DevBufs);
 __global__ void k_dbscan_adj(DevCfg, DevBufs);
 template <int kDbL> __global__ void k_dbscan_merge(DevCfg, DevBufs);
@@ -263,6 +264,7 @@ static size_t layout(DevBufs& d, char* p0, int B, int H, int HW) {
   d.db_kz = carve<float>(p, n);
   d.db_adj = carve<uint32_t>(p, (size_t)B * kAdjCap * kAdjWords);
   d.mt0 = carve<uint32_t>(p, 624);
+  d.phantom = carve<int>(p, (size_t)B);
   return (size_t)(p - p0);
 }
 
@@ -382,6 +384,7 @@ extern "C" int32_t llsr_reset_state(llsr_handle* h) {
   const size_t n = (size_t)h->max_batch * h->dc.HW;
   HIP_OK(h, hipMemsetAsync(h->d.picked, 0, n, h->stream));
   HIP_OK(h, hipMemsetAsync(h->d.clabel, 0, n, h->stream));
+  HIP_OK(h, hipMemsetAsync(h->d.phantom, 0, sizeof(int) * (size_t)h->max_batch, h->stream));
   HIP_OK(h, hipStreamSynchronize(h->stream));
   return LLSR_OK;
 }
@@ -490,6 +493,29 @@ extern "C" int32_t llsr_kernel_times_ms(llsr_handle* h, float* out, int32_t cap)
   int n = 0;
   for (int k = 0; k < kNumKernels && n < cap; ++k, ++n) out[n] = (float)(h->ksum[k] / (double)h->kbatches);
   return n;
+}
+
+// Diagnostics (not part of the ABI header): the device's exact libstdc++ std::sort (the per-ring
+// curvature sort's tie path, llsr_fa.hip exact_introsort) on n <= 2048 host values; out[k] = the
+// input position at sorted position k. For tests/test_gpu_features_ties.py.
+extern "C" int32_t llsr_debug_exact_sort(const float* vals, int32_t n, int32_t* out) {
+  if (!vals || !out || n < 0 || n > 2048) return LLSR_EINVAL;
+  if (n == 0) return LLSR_OK;
+  float* dv = nullptr;
+  int* di = nullptr;
+  if (hipMalloc(&dv, sizeof(float) * n) != hipSuccess) return LLSR_ENODEV;
+  if (hipMalloc(&di, sizeof(int) * n) != hipSuccess) { (void)hipFree(dv); return LLSR_ENODEV; }
+  int32_t rc = LLSR_OK;
+  if (hipMemcpy(dv, vals, sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess) rc = LLSR_EIO;
+  if (rc == LLSR_OK) {
+    k_debug_exact_sort<<<1, 64>>>(dv, n, di);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(out, di, sizeof(int) * n, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = LLSR_EIO;
+  }
+  (void)hipFree(dv);
+  (void)hipFree(di);
+  return rc;
 }
 
 // Diagnostics (not part of the ABI header): re-launch kernel k on the last batch's buffers with

@@ -21,6 +21,8 @@ enum : int {
   C_F = 10,        // surfPointsFlat (without shadow points)
   C_L = 11,        // surfPointsLessFlat
   C_HALF = 12,     // adjustDistortion halfPassed split index
+  C_EXACT = 13,    // rings whose curvature sort took the exact libstdc++ path (ties)
+  C_PHOUT = 14,    // rings where the carried cloudSmoothness[4] index fell outside the ring window
   kCnt = 16
 };
 
@@ -78,6 +80,7 @@ struct DevBufs {
   float* db_kz;         // [B][HW]
   uint32_t* db_adj;     // [B][kAdjCap][kAdjWords] eps-neighbourhood bitmask rows
   uint32_t* mt0;        // [624] RANSAC's mt19937 state after seed(12345) and its first twist
+  int* phantom;         // [B] FA carry-over state: cloudSmoothness[4].ind (value is always 0)
 };
 
 // DBSCAN adjacency capacity per scan (edge candidates); larger M falls back to on-the-fly rows.

@@ -240,6 +240,173 @@ __device__ __forceinline__ int pow2_ceil(int n) {
   return n2;
 }
 
+// ---- libstdc++ std::sort, exactly (FA:1172), for rings whose eligible curvatures tie ----------
+// The sort compares values only, so the order of EQUAL values is whatever libstdc++'s introsort
+// leaves, and it decides which of two tied candidates the greedy loop visits first. One wave
+// reproduces it on key[0, n) (value bits << 32 | ind): __introsort_loop (median of
+// (first+1, mid, last-1) to first, __unguarded_partition, depth limit 2*lg(n) -> heap sort),
+// then __final_insertion_sort (threshold 16). Each partition is evaluated in parallel: the k-th
+// stop of the left scan over the original range is L[k] (!(a < pivot)), of the right scan R[k]
+// (!(pivot < a), from last-1 down to the pivot slot); pairs k < k* = #{k : L[k] < R[k]} are
+// swapped and the cut is R[k*-1] when k* > 0 and L[k*] is missing or >= R[k*-1], else L[k*].
+// Sub-ranges are independent (the depth limit travels with each) and the final insertion sort
+// never crosses a leaf boundary, so it runs as one insertion sort per leaf. The serial statement
+// of this formulation is checked against std::sort by tests/native/introsort_check.cpp; the
+// device against the oracle's std::sort by tests/test_gpu_features_ties.py.
+__device__ __forceinline__ bool key_lt(uint64_t a, uint64_t b) {
+  return __uint_as_float((uint32_t)(a >> 32)) < __uint_as_float((uint32_t)(b >> 32));
+}
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+// libstdc++ __adjust_heap (with __push_heap) on key[f, f+len), one lane
+__device__ void heap_adjust(uint64_t* key, int f, int hole, int len, uint64_t val) {
+  const int top = hole;
+  int second = hole;
+  while (second < (len - 1) / 2) {
+    second = 2 * (second + 1);
+    if (key_lt(key[f + second], key[f + second - 1])) second--;
+    key[f + hole] = key[f + second];
+    hole = second;
+  }
+  if ((len & 1) == 0 && second == (len - 2) / 2) {
+    second = 2 * (second + 1);
+    key[f + hole] = key[f + second - 1];
+    hole = second - 1;
+  }
+  int parent = (hole - 1) / 2;
+  while (hole > top && key_lt(key[f + parent], val)) {
+    key[f + hole] = key[f + parent];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  key[f + hole] = val;
+}
+// __partial_sort(first, last, last) = __make_heap + __sort_heap, one lane
+__device__ void heap_sort_range(uint64_t* key, int f, int l) {
+  const int len = l - f;
+  if (len >= 2)
+    for (int parent = (len - 2) / 2;; --parent) {
+      heap_adjust(key, f, parent, len, key[f + parent]);
+      if (parent == 0) break;
+    }
+  for (int last = l; last - f > 1;) {
+    --last;
+    const uint64_t val = key[last];
+    key[last] = key[f];
+    heap_adjust(key, f, 0, last - f, val);
+  }
+}
+constexpr int kSortStack = 64;
+// Executed by one full wave (64 lanes). Lp / Rp: n uint16 each; stk: 3 * kSortStack ints;
+// leaf: (n + 64) / 64 uint64 words. Returns nothing; key[0, n) ends up as std::sort leaves it.
+__device__ void exact_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp, int* stk, uint64_t* leaf) {
+  const int l = lane_id();
+  const unsigned long long ltm = (1ull << l) - 1ull;
+  for (int w = l; w <= (n >> 6); w += 64) leaf[w] = 0ull;
+  wave_sync_lds();
+  if (n <= 1) return;
+  int lg = 31 - __clz(n);
+  int sp = 0;  // stack depth (wave-uniform)
+  int rf = 0, rl = n, rd = 2 * lg;
+  while (true) {
+    while (rl - rf > 16) {
+      if (rd == 0) {
+        if (l == 0) heap_sort_range(key, rf, rl);
+        wave_sync_lds();
+        break;
+      }
+      rd--;
+      const int mid = rf + (rl - rf) / 2;
+      if (l == 0) {  // __move_median_to_first(first, first+1, mid, last-1)
+        const int a = rf + 1, b = mid, c = rl - 1;
+        int m;
+        if (key_lt(key[a], key[b])) m = key_lt(key[b], key[c]) ? b : (key_lt(key[a], key[c]) ? c : a);
+        else m = key_lt(key[a], key[c]) ? a : (key_lt(key[b], key[c]) ? c : b);
+        const uint64_t t = key[rf]; key[rf] = key[m]; key[m] = t;
+      }
+      wave_sync_lds();
+      const uint64_t P = key[rf];
+      int nL = 0, nR = 0;
+      for (int c0 = rf + 1; c0 < rl; c0 += 64) {
+        const int i = c0 + l;
+        const bool f = i < rl && !key_lt(key[i], P);
+        const unsigned long long m = __ballot(f);
+        if (f) Lp[nL + __popcll(m & ltm)] = (uint16_t)i;
+        nL += __popcll(m);
+      }
+      for (int c0 = rl - 1; c0 >= rf; c0 -= 64) {
+        const int j = c0 - l;
+        const bool f = j >= rf && !key_lt(P, key[j]);
+        const unsigned long long m = __ballot(f);
+        if (f) Rp[nR + __popcll(m & ltm)] = (uint16_t)j;
+        nR += __popcll(m);
+      }
+      wave_sync_lds();
+      const int nm = nL < nR ? nL : nR;
+      int ks = nm;  // first k with !(L[k] < R[k]) (monotone)
+      for (int c0 = 0; c0 < nm; c0 += 64) {
+        const int k = c0 + l;
+        const unsigned long long m = __ballot(k < nm && !(Lp[k] < Rp[k]));
+        if (m) { ks = c0 + __ffsll((long long)m) - 1; break; }
+      }
+      const int cut = (ks > 0 && (ks >= nL || Lp[ks] >= Rp[ks - 1])) ? Rp[ks - 1] : Lp[ks];
+      for (int k = l; k < ks; k += 64) {
+        const int a = Lp[k], b = Rp[k];
+        const uint64_t t = key[a]; key[a] = key[b]; key[b] = t;
+      }
+      wave_sync_lds();
+      // the right part waits (at most one entry per level of the current path: <= 2*lg(n) + 1
+      // <= 23 < kSortStack); the left part continues here
+      if (l == 0) { stk[3 * sp] = cut; stk[3 * sp + 1] = rl; stk[3 * sp + 2] = rd; }
+      ++sp;
+      rl = cut;
+    }
+    if (l == 0) leaf[rf >> 6] |= 1ull << (rf & 63);
+    wave_sync_lds();
+    if (sp == 0) break;
+    --sp;
+    rf = stk[3 * sp]; rl = stk[3 * sp + 1]; rd = stk[3 * sp + 2];
+  }
+  // one insertion sort per leaf block: lane w takes the leaves starting in word w, w + 64, ...
+  const int nw = (n + 63) >> 6;
+  for (int w = l; w < nw; w += 64) {
+    uint64_t bits = leaf[w];
+    while (bits) {
+      const int s0 = (w << 6) + __ffsll((long long)bits) - 1;
+      bits &= bits - 1;
+      int e = n;  // next leaf start after s0
+      if (bits) {
+        e = (w << 6) + __ffsll((long long)bits) - 1;
+      } else {
+        for (int w2 = w + 1; w2 < nw; ++w2)
+          if (leaf[w2]) { e = (w2 << 6) + __ffsll((long long)leaf[w2]) - 1; break; }
+      }
+      for (int i = s0 + 1; i < e; ++i) {
+        const uint64_t val = key[i];
+        int j = i;
+        while (j > s0 && key_lt(val, key[j - 1])) { key[j] = key[j - 1]; --j; }
+        key[j] = val;
+      }
+    }
+  }
+  wave_sync_lds();
+}
+
+// Diagnostics (llsr_debug_exact_sort): exact_introsort on one array of n <= kRingMax values; out
+// receives the original positions in sorted order. One wave.
+__global__ __launch_bounds__(64) void k_debug_exact_sort(const float* vals, int n, int* out) {
+  __shared__ uint64_t key[kRingMax];
+  __shared__ uint16_t Lp[kRingMax], Rp[kRingMax];
+  __shared__ int stk[3 * kSortStack];
+  __shared__ uint64_t leafw[kRingMax / 64 + 1];
+  for (int t = threadIdx.x; t < n; t += 64) key[t] = ((uint64_t)__float_as_uint(vals[t]) << 32) | (uint32_t)t;
+  wave_sync_lds();
+  exact_introsort(key, n, Lp, Rp, stk, leafw);
+  for (int t = threadIdx.x; t < n; t += 64) out[t] = (int)(uint32_t)key[t];
+}
+
 // Serial greedy pick (FA:1175-1259) over a candidate list already in visiting order, by one wave:
 // each chunk of 64 candidates reads `picked` once; the first still-alive candidate is selected,
 // candidates inside its suppression interval die, repeat. Steps per chunk = picks in the chunk.
@@ -378,21 +545,102 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
     }
   }
   __syncthreads();
-  // ---- edges: statically eligible sorted-part entries, visited in descending key order ----
+  // ---- the sorted range [sp, ep) of cloudSmoothness (FA:1172) ----
+  // Position 4 (ring 0's sp) holds whatever the previous frame's ring-0 sort left there: value 0
+  // (it is always a minimum) and a carried index `ph` (0 until an exact zero displaces it).
+  const int nRng = ep - sp;
+  const int ph = sp == 4 ? d.phantom[b] : 0;
+  const bool ph_in = ph >= ws && ph - ws < wn;
+  const float ph_curv = ph < 5 ? 0.0f : curv[ph];  // cloudCurvature[0..4] is never written (FA:819)
+  if (sp == 4 && !ph_in && tid == 0) atomicAdd(&d.counts[b * kCnt + C_PHOUT], 1);
+  __shared__ uint64_t leafw[kRingMax / 64 + 1];
+  __shared__ int stk[3 * kSortStack];
+  __shared__ int s_flag, s_exact;
+  // exact-order triggers: ties between eligible keys (found after each fast sort) and, in ring 0, an
+  // exact zero that could take position 4 from the phantom for the next frame
+  if (tid == 0) s_flag = 0;
+  __syncthreads();
+  if (sp == 4) {
 #pragma unroll
-  for (int u = 0; u < kPer; ++u) {  // wave-aggregated append: one LDS atomic per wave
-    const int p = ws + tid + u * 256;
-    const bool in = p >= sp && p < ep;
-    const int ind = p == 4 ? 0 : p;
-    const float v = p == 4 ? 0.0f : cvr[u];
-    const int w = in ? ind - ws : 0;
-    const bool e = in && wpick[w] == 0 && v > c.edge_thr && wgnd[w] == 0;
-    const unsigned long long m = __ballot(e);
-    int wb = 0;
-    if (lane_id() == 0 && m) wb = atomicAdd(&s_cnt, (int)__popcll(m));
-    wb = __shfl(wb, 0, 64);
-    if (e) key[wb + __popcll(m & ((1ull << lane_id()) - 1ull))] = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)ind;
+    for (int u = 0; u < kPer; ++u) {
+      const int p = ws + tid + u * 256;
+      if (p >= 5 && p < ep && cvr[u] == 0.0f) s_flag = 1;
+    }
   }
+  // curvature of an entry's index as the eligibility tests read it (cloudCurvature[ind])
+  auto curv_of = [&](int ind) { return ind < 5 ? 0.0f : curv[ind]; };
+  // key[0, nRng) = the full range sorted exactly as std::sort leaves it; updates the phantom
+  auto exact_sort = [&]() {
+    for (int t = tid; t < nRng; t += nt) {
+      const int p = sp + t;
+      const float v = p == 4 ? 0.0f : curv[p];
+      const int ind = p == 4 ? ph : p;
+      key[t] = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)ind;
+    }
+    __syncthreads();
+    if (tid < 64) exact_introsort(key, nRng, cpos, rstart, stk, leafw);
+    __syncthreads();
+    if (tid == 0) {
+      if (sp == 4) d.phantom[b] = (int)(uint32_t)key[0];
+      atomicAdd(&d.counts[b * kCnt + C_EXACT], 1);
+      s_exact = 1;
+    }
+    __syncthreads();
+  };
+  // compaction of the exactly sorted entries passing `elig`, in visiting order (descending for the
+  // edge loop, ascending for the flat loop), into cpos; wave 0; returns the count
+  auto compact_sorted = [&](bool descending, auto elig) {
+    const int l = lane_id();
+    int cnt = 0;
+    for (int c0 = 0; c0 < nRng; c0 += 64) {
+      const int k = c0 + l;
+      const int t = descending ? nRng - 1 - k : k;
+      const bool e = k < nRng && elig((int)(uint32_t)key[t]);
+      const unsigned long long m = __ballot(e);
+      if (e) cpos[cnt + __popcll(m & ((1ull << l) - 1ull))] = (uint16_t)t;
+      cnt += __popcll(m);
+    }
+    return cnt;
+  };
+  auto edge_elig = [&](int ind) {
+    const int w = ind - ws;
+    return w >= 0 && w < wn && wpick[w] == 0 && curv_of(ind) > c.edge_thr && wgnd[w] == 0;
+  };
+  auto flat_elig = [&](int ind) {
+    const int w = ind - ws;
+    return w >= 0 && w < wn && wpick[w] == 0 && curv_of(ind) < c.surf_thr && wgnd[w] == 1;
+  };
+  // wave-aggregated append of the statically eligible keys of the fast path
+  auto append = [&](bool edge) {
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int p = ws + tid + u * 256;
+      const bool in = p >= sp && p < ep && (p != 4 || ph_in);
+      const int ind = p == 4 ? ph : p;
+      const float v = p == 4 ? 0.0f : cvr[u];          // the sort value
+      const float ve = p == 4 ? ph_curv : cvr[u];     // cloudCurvature[ind]
+      const int w = in ? ind - ws : 0;
+      const bool e = in && wpick[w] == 0 && (edge ? (ve > c.edge_thr && wgnd[w] == 0) : (ve < c.surf_thr && wgnd[w] == 1));
+      const unsigned long long m = __ballot(e);
+      int wb = 0;
+      if (lane_id() == 0 && m) wb = atomicAdd(&s_cnt, (int)__popcll(m));
+      wb = __shfl(wb, 0, 64);
+      if (e) key[wb + __popcll(m & ((1ull << lane_id()) - 1ull))] = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)ind;
+    }
+  };
+  // adjacent equal values in the fast-sorted eligible keys [lo, hi); also reports an earlier trigger
+  auto ties = [&](int lo, int hi) {
+    for (int t = lo + tid; t + 1 < hi; t += nt)
+      if ((uint32_t)(key[t] >> 32) == (uint32_t)(key[t + 1] >> 32)) s_flag = 1;
+    __syncthreads();
+    return s_flag != 0;
+  };
+  if (tid == 0) s_exact = 0;
+  __syncthreads();
+  // ---- edges: eligible entries visited in descending sorted order, the unsorted ep first ----
+  const bool epE = curv[ep] > c.edge_thr && wgnd[ep - ws] == 0;
+  const int e0 = epE ? 1 : 0;
+  append(true);
   __syncthreads();
   if (c.dbg_phase <= 0) return;
   int nE = s_cnt;
@@ -401,43 +649,52 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   __syncthreads();
   bitonic_sort_u64(key, n2);
   if (c.dbg_phase <= 1) return;
-  // visiting order: the unsorted entry at ep first, then descending keys (FA:1175)
-  const bool epE = curv[ep] > c.edge_thr && wgnd[ep - ws] == 0;
-  const int e0 = epE ? 1 : 0;
-  if (tid < 64) {
+  // (n2 - nE zero keys sort first: the eligible keys are key[n2 - nE, n2))
+  if (ties(n2 - nE, n2)) {
+    exact_sort();
+    if (tid < 64) {
+      const int cnt = compact_sorted(true, edge_elig);
+      auto order = [&](int t) { return t < e0 ? ep : (int)(uint32_t)key[cpos[t - e0]]; };
+      const int sel = greedy_wave(order, cnt + e0, ws, wpick, wreach, wlab, (int8_t)1, d.edge_tmp + base + sp);
+      if (tid == 0) { rc[i] = sel; s_cnt = 0; }
+    }
+  } else if (tid < 64) {
     auto order = [&](int t) { return t < e0 ? ep : (int)(uint32_t)key[n2 - 1 - (t - e0)]; };
     const int cnt = greedy_wave(order, nE + e0, ws, wpick, wreach, wlab, (int8_t)1, d.edge_tmp + base + sp);
     if (tid == 0) { rc[i] = cnt; s_cnt = 0; }
   }
   __syncthreads();
   if (c.dbg_phase <= 2) return;
-  // ---- flats: ascending key order, entry ep last ----
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) {  // wave-aggregated append: one LDS atomic per wave
-    const int p = ws + tid + u * 256;
-    const bool in = p >= sp && p < ep;
-    const int ind = p == 4 ? 0 : p;
-    const float v = p == 4 ? 0.0f : cvr[u];
-    const int w = in ? ind - ws : 0;
-    const bool e = in && wpick[w] == 0 && v < c.surf_thr && wgnd[w] == 1;
-    const unsigned long long m = __ballot(e);
-    int wb = 0;
-    if (lane_id() == 0 && m) wb = atomicAdd(&s_cnt, (int)__popcll(m));
-    wb = __shfl(wb, 0, 64);
-    if (e) key[wb + __popcll(m & ((1ull << lane_id()) - 1ull))] = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)ind;
-  }
-  __syncthreads();
-  const int nF = s_cnt;
-  n2 = pow2_ceil(nF);
-  for (int t = nF + tid; t < n2; t += nt) key[t] = ~0ull;
-  __syncthreads();
-  bitonic_sort_u64(key, n2);
-  // visiting order: ascending keys, then the unsorted entry at ep (FA:1211)
+  // ---- flats: eligible entries in ascending sorted order, the unsorted ep last ----
   const bool epF = curv[ep] < c.surf_thr && wgnd[ep - ws] == 1;
-  if (tid < 64) {
-    auto order = [&](int t) { return t < nF ? (int)(uint32_t)key[t] : ep; };
-    const int cnt = greedy_wave(order, nF + (epF ? 1 : 0), ws, wpick, wreach, wlab, (int8_t)-1, d.flat_tmp + base + sp);
-    if (tid == 0) rc[H + i] = cnt;
+  if (s_exact) {
+    if (tid < 64) {
+      const int cnt = compact_sorted(false, flat_elig);
+      auto order = [&](int t) { return t < cnt ? (int)(uint32_t)key[cpos[t]] : ep; };
+      const int sel = greedy_wave(order, cnt + (epF ? 1 : 0), ws, wpick, wreach, wlab, (int8_t)-1, d.flat_tmp + base + sp);
+      if (tid == 0) rc[H + i] = sel;
+    }
+  } else {
+    append(false);
+    __syncthreads();
+    const int nF = s_cnt;
+    n2 = pow2_ceil(nF);
+    for (int t = nF + tid; t < n2; t += nt) key[t] = ~0ull;
+    __syncthreads();
+    bitonic_sort_u64(key, n2);
+    if (ties(0, nF)) {
+      exact_sort();
+      if (tid < 64) {
+        const int cnt = compact_sorted(false, flat_elig);
+        auto order = [&](int t) { return t < cnt ? (int)(uint32_t)key[cpos[t]] : ep; };
+        const int sel = greedy_wave(order, cnt + (epF ? 1 : 0), ws, wpick, wreach, wlab, (int8_t)-1, d.flat_tmp + base + sp);
+        if (tid == 0) rc[H + i] = sel;
+      }
+    } else if (tid < 64) {
+      auto order = [&](int t) { return t < nF ? (int)(uint32_t)key[t] : ep; };
+      const int cnt = greedy_wave(order, nF + (epF ? 1 : 0), ws, wpick, wreach, wlab, (int8_t)-1, d.flat_tmp + base + sp);
+      if (tid == 0) rc[H + i] = cnt;
+    }
   }
   __syncthreads();
   if (c.dbg_phase <= 3) return;

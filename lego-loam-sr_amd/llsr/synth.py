@@ -37,7 +37,10 @@ def beam_layout(lidar: str):
 
 
 class _Scene:
-    def __init__(self, rng: np.random.Generator):
+    def __init__(self, rng: np.random.Generator, ground_ramp: tuple[float, float] | None = None):
+        # ground_ramp = (x0, slope): beyond x = x0 the ground rises with this slope (a second plane
+        # the near-ground RANSAC can lock onto, tests/test_gpu_features_ties.py)
+        self.ramp = ground_ramp
         boxes = []  # (xmin, xmax, ymin, ymax, zmin, zmax)
         # facades: left y in [9, 12], right y in [-14, -11], long along x
         for side, y0, y1 in ((1, 9.0, 12.0), (-1, -14.0, -11.0)):
@@ -85,7 +88,16 @@ class _Scene:
         dz = d[:, 2]
         with np.errstate(divide="ignore", invalid="ignore"):
             tg = (self.ground_z - o[2]) / dz
-        t = np.where((dz < 0) & (tg > 0), tg, t)
+        if self.ramp is None:
+            t = np.where((dz < 0) & (tg > 0), tg, t)
+        else:
+            x0, k = self.ramp
+            flat_ok = (dz < 0) & (tg > 0) & (o[0] + tg * d[:, 0] <= x0)
+            with np.errstate(divide="ignore", invalid="ignore"):  # z = ground_z + k (x - x0)
+                tr = (self.ground_z + k * (o[0] - x0) - o[2]) / (dz - k * d[:, 0])
+            ramp_ok = (tr > 0) & (o[0] + tr * d[:, 0] > x0)
+            t = np.where(flat_ok, tg, t)
+            t = np.where(ramp_ok & (tr < t), tr, t)
         inv = 1.0 / np.where(np.abs(d) < 1e-12, 1e-12, d)
         for b in self.boxes:
             t1 = (b[0::2] - o) * inv  # x/y/z mins
@@ -111,14 +123,14 @@ class _Scene:
 
 def make_scan(seed: int, lidar: str = VLP16, dropout: float = 0.02, noise: float = 0.01,
               max_range: float = 100.0, origin_xy: tuple[float, float] | None = None,
-              scene_id: int | None = None) -> np.ndarray:
+              scene_id: int | None = None, ground_ramp: tuple[float, float] | None = None) -> np.ndarray:
     """One raw scan as float32 [N, 4] (x, y, z, intensity), N = rings * columns (NaNs kept).
 
     The sensor sits at (0.5 * (seed % 64), U(-0.5, 0.5), 0) of scene `seed // 64`; scan-to-map
     fixtures override both (`origin_xy`, `scene_id`) to place keyframes along one street."""
     rng = np.random.default_rng(seed)
     scene_id = seed // 64 if scene_id is None else scene_id  # scenes shared by 64 scans
-    scene = _Scene(np.random.default_rng(1000003 + scene_id))
+    scene = _Scene(np.random.default_rng(1000003 + scene_id), ground_ramp)
     elev, W = beam_layout(lidar)
     H = elev.shape[0]
     res_x = 2.0 * np.pi / W
@@ -142,6 +154,30 @@ def make_scan(seed: int, lidar: str = VLP16, dropout: float = 0.02, noise: float
     pts[:, :3] = (d * r[:, None]).astype(np.float32)
     pts[:, 3] = rng.integers(0, 101, size=t.shape).astype(np.float32)
     return pts
+
+
+def make_symmetric_scan(seed: int, lidar: str = VLP16, quadrants: int = 4) -> np.ndarray:
+    """A scan whose first quarter of azimuth columns is repeated, rotated by 90 degrees about the
+    sensor, in the other quarters (quadrants = 4) or half repeated at 180 degrees (quadrants = 2).
+    The rotations only swap and negate x / y, so every curvature (FA:817-848) repeats EXACTLY in
+    each copy: the per-ring sort (FA:1172) meets ties everywhere and libstdc++'s order of equal
+    values decides the order of the feature lists."""
+    pts = make_scan(seed, lidar)
+    _, W = beam_layout(lidar)
+    H = pts.shape[0] // W
+    step = W // quadrants
+    base = pts[: step * H].copy()
+    out = [base]
+    cur = base
+    for _ in range(quadrants - 1):
+        nxt = cur.copy()
+        if quadrants == 4:   # azimuth(t + W/4) = azimuth(t) - 90 deg: (x, y) -> (y, -x)
+            nxt[:, 0], nxt[:, 1] = cur[:, 1], -cur[:, 0]
+        else:                # 180 deg: (x, y) -> (-x, -y)
+            nxt[:, 0], nxt[:, 1] = -cur[:, 0], -cur[:, 1]
+        out.append(nxt)
+        cur = nxt
+    return np.concatenate(out, axis=0)
 
 
 def make_batch(n_scans: int, lidar: str = VLP16, distinct: int | None = None, seed0: int = 1):

@@ -219,6 +219,19 @@ extern "C" void oracle_stage_ms(const oracle_state* s, double* ip, double* fa) {
   if (fa) *fa = s->fa_ms;
 }
 
+// libstdc++ std::sort by value (the comparator of FA:1172, utility.h:57-61) of n values; out[k] =
+// the input position at sorted position k (test hook for the device's exact tie order).
+extern "C" void oracle_std_sort_by_value(const float* vals, int32_t n, int32_t* out) {
+  std::vector<std::pair<float, size_t>> v((size_t)n);
+  for (int k = 0; k < n; ++k) v[k] = {vals[k], (size_t)k};
+  std::sort(v.begin(), v.end(),
+            [](const std::pair<float, size_t>& a, const std::pair<float, size_t>& b) { return a.first < b.first; });
+  for (int k = 0; k < n; ++k) out[k] = (int32_t)v[k].second;
+}
+
+// cloudSmoothness[4].ind, the entry the next frame's ring-0 sort starts from (test hook)
+extern "C" int32_t oracle_phantom_index(const oracle_state* s) { return (int32_t)s->smooth[4].second; }
+
 extern "C" int32_t oracle_ransac_inliers(oracle_state* s, uint32_t seed, int32_t* out, int32_t cap) {
   PlaneRansac rs(s->near, seed);
   std::vector<int> inl;

@@ -43,6 +43,9 @@ def lib():
         L.oracle_stage_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.oracle_ransac_inliers.restype = C.c_int32
         L.oracle_ransac_inliers.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int32]
+        L.oracle_std_sort_by_value.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
+        L.oracle_phantom_index.restype = C.c_int32
+        L.oracle_phantom_index.argtypes = [C.c_void_p]
         for f in ("oracle_eig3", "oracle_eig6"):
             getattr(L, f).restype = C.c_int32
             getattr(L, f).argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
@@ -141,11 +144,23 @@ class Oracle:
         lib().oracle_stage_ms(self._h, C.byref(a), C.byref(b))
         return a.value, b.value
 
+    def phantom_index(self) -> int:
+        """cloudSmoothness[4].ind after the last scan (the next ring-0 sort's phantom entry)."""
+        return int(lib().oracle_phantom_index(self._h))
+
     def ransac_inliers(self, seed: int) -> np.ndarray:
         cap = self.cfg.num_vertical_scans * self.cfg.num_horizontal_scans
         buf = np.zeros(cap, dtype=np.int32)
         n = lib().oracle_ransac_inliers(self._h, seed, buf.ctypes.data, cap)
         return buf[:n].copy()
+
+
+def std_sort_by_value(vals) -> np.ndarray:
+    """Positions of `vals` in libstdc++ std::sort order under the value-only comparator (FA:1172)."""
+    v = np.ascontiguousarray(vals, dtype=np.float32)
+    out = np.zeros(len(v), dtype=np.int32)
+    lib().oracle_std_sort_by_value(v.ctypes.data, len(v), out.ctypes.data)
+    return out
 
 
 def _f4(a) -> np.ndarray:

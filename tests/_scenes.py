@@ -64,3 +64,29 @@ def mo_degenerate_problems(regular=False):
     z = np.load(FIX)
     cases = MO_DEGENERATE_CASES + (MO_REGULAR_CASES if regular else ())
     return [mo_shrunk_problem(z, i, off) for i, off in cases]
+
+
+def zero_curvature_scan(seed, centers=(900,), q=2.0 ** -8):
+    """A 4-fold symmetric VLP-16 scan (synth.make_symmetric_scan) whose lowest ring (-15 deg) meets
+    the ground, around each raw column c in `centers`, on the line through the ground point P at c
+    perpendicular to its ray: the points at columns c + 5m, m = -5..5 — consecutive in the
+    segmented cloud, since ground cells enter it every 5th column (IP:809-812) — are P +- w_m with P
+    and w_m on a 2^-8 m grid (z too), so the neighbour sums of calculateSmoothnessOurs (FA:826-835)
+    cancel exactly at P: an exact zero curvature in ring 0's sort range per centre. Those tie with
+    the phantom entry cloudSmoothness[4] = {0, ind}, and libstdc++'s order of equal values decides
+    which index position 4 carries into the next frame (its flat loop visits that entry first)."""
+    from llsr import synth
+    pts = synth.make_symmetric_scan(seed)
+    W, Hh = 1800, 16
+    res = 2.0 * np.pi / W
+    z = np.round(-1.3 / q) * q
+    rho = -z / np.tan(np.deg2rad(15.0))
+    for c in centers:
+        phi = (W / 2 - c) * res
+        P = np.round(np.array([rho * np.cos(phi), rho * np.sin(phi)]) / q) * q
+        u = np.array([np.sin(phi), -np.cos(phi)])  # along increasing raw column (decreasing phi)
+        for m in range(-5, 6):
+            w = np.round(rho * np.tan(5 * abs(m) * res) * u / q) * q
+            xy = P + np.sign(m) * w
+            pts[((c + 5 * m) % W) * Hh + 0, :3] = (np.float32(xy[0]), np.float32(xy[1]), np.float32(z))
+    return pts
