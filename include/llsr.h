@@ -382,6 +382,55 @@ int32_t llsr_map_extract(llsr_map* m, const float robot_pos[3], float* d_corner,
 /* surroundingExistingKeyPosesID after the last extract; returns its length. */
 int32_t llsr_map_keyframe_ids(const llsr_map* m, int32_t* out, int32_t cap);
 
+/* ---- Mapping chain: ImageProjection -> FeatureAssociation -> MapOptimization::run ----
+ * (mapOptmization.cpp:1854-1896, one AssociationOut per odometry frame, mapping_frequency_divider
+ * 1, loop closure disabled as in every config block.) Each llsr_mapping_batch call runs
+ * llsr_odometry_batch on the B slots and then, for every slot past its first scan (the first
+ * scan sends no AssociationOut, FA:2781-2784): OdometryToTransform of the published odometry
+ * (tf2 round trip, FA:2612-2625 / utility.h:99-113), transformAssociateToMap (MO:458-581),
+ * extractSurroundingKeyFrames on the slot's keyframe store (MO:1096-1232), downsampleCurrentScan
+ * of the AssociationOut clouds (corner / surf last, the adjustOutlierCloud'ed IP outliers
+ * FA:2600-2610, corner / surf scan; MO:1234-1267), scan2MapOptimization (MO:1572-1610: all slots
+ * in one device batch, isDegenerate / matP carried per slot), transformUpdate (MO:583-589) and
+ * saveKeyFramesAndFactor (MO:1612-1755; every frame is a keyframe there, saveThisKeyFrame is forced
+ * true at MO:1629; the prior / between factors with the initial values as measurements leave
+ * iSAM2's estimate at the initial values, so the key pose is transformTobeMapped for the first
+ * keyframe and transformAftMapped after). Requires the handle's mode LLSR_MODE_LM_APPLIED
+ * (the odometry's); `mo_mode` selects MapOptimization's own LM mode (LLSR_MODE_FAITHFUL: the pose
+ * update at MO:1539-1545 stays commented out, as in the reference). Synchronises per call. */
+typedef struct llsr_mapping_slot {
+  int32_t frames;               /* scans consumed by the slot (odometry frames) */
+  int32_t mo_frames;            /* MapOptimization::run iterations = frames - 1 once frames >= 2 */
+  int32_t keyframes;            /* cloudKeyPoses3D size */
+  int32_t lm_ran;               /* the last frame's map passed MO:1573 (corner > 10, surf > 100) */
+  float transform_sum[6];       /* OdometryToTransform of the last published odometry */
+  float transform_tobe_mapped[6];
+  float transform_bef_mapped[6];
+  float transform_aft_mapped[6];
+  int32_t n_corner_q;           /* laserCloudCornerScanDSNum (the corner queries) */
+  int32_t n_surf_q;             /* laserCloudSurfTotalLastDSNum (the surf queries) */
+  llsr_lm_report lm;            /* the last frame's scan2MapOptimization (iterations 0 when skipped) */
+  llsr_map_report map;          /* the last frame's extractSurroundingKeyFrames */
+} llsr_mapping_slot;
+/* Allocate the per-slot MapOptimization state (max_batch slots, map_cfg NULL = the reference's
+ * leaves and radius) and start every slot over (also resets the odometry). */
+int32_t llsr_mapping_init(llsr_handle* h, int32_t mo_mode, const llsr_map_config* map_cfg);
+int32_t llsr_mapping_batch(llsr_handle* h, const float* d_xyzi, const int64_t* d_offsets, int32_t B,
+                           void* hip_stream);
+int32_t llsr_mapping_fetch(llsr_handle* h, int32_t b, llsr_mapping_slot* out);
+/* cloudKeyPoses6D of slot b: x, y, z, roll, pitch, yaw per keyframe into out[6*cap]; returns the
+ * keyframe count (may exceed cap). */
+int32_t llsr_mapping_keyposes(llsr_handle* h, int32_t b, float* out, int32_t cap);
+/* Start every slot over: odometry, poses, keyframe stores. */
+int32_t llsr_mapping_reset(llsr_handle* h);
+/* Host-only (no device): the pose glue llsr_mapping_batch applies per frame — OdometryToTransform
+ * of FA's transformSum (tf2 round trip) into transform_sum, then transformAssociateToMap with the
+ * given transformBefMapped / transformAftMapped into transform_tobe_mapped (and transform_incre,
+ * may be NULL). */
+int32_t llsr_mapping_associate(const float transform_sum_fa[6], const float transform_bef_mapped[6],
+                               const float transform_aft_mapped[6], float transform_sum[6],
+                               float transform_tobe_mapped[6], float transform_incre[6]);
+
 
 /* ---- Input wire formats (llsr_input.hip) ----
  * sensor_msgs/PointCloud2 (PointField datatype codes, sensor_msgs/msg/PointField.msg) decoded as

@@ -14,6 +14,7 @@
 #include "llsr_device.h"
 #include "llsr_libm.h"
 #include "llsr_grid.h"
+#include "llsr_mapping.h"
 #include "llsr_mo.h"
 #include "llsr_odo.h"
 #include "llsr_s2s.h"
@@ -77,7 +78,7 @@ struct llsr_handle {
   long long kbatches = 0;
   // scan-to-map (llsr_scan2map_*): buffers sized by llsr_scan2map_reserve
   struct {
-    int P = 0, qc = 0, qs = 0, mc = 0, ms = 0, log2T_c = 0, log2T_s = 0, blocks_c = 0, blocks = 0;
+    int P = 0, qc = 0, qs = 0, mc = 0, ms = 0, log2T_c = 0, log2T_s = 0, blocks_c = 0, blocks = 0, red_blocks = 0;
     void* pool = nullptr;
     S2MArgs a{};
     int* host_flags = nullptr;   // pinned: n_active, error
@@ -120,6 +121,31 @@ struct llsr_handle {
     llsr_s2s_report* report = nullptr;  // [B]
     int cur = 0;                  // last_c/s[cur] hold the current last clouds
   } odo;
+  // mapping chain (llsr_mapping_*): MapOptimization's members per slot + the batch buffers
+  struct MapSlot {
+    llsr_mapping::MoPoses pose;
+    llsr_map* map = nullptr;           // keyframe store (cornerCloudKeyFrames etc., cloudKeyPoses6D)
+    float robot[3] = {0, 0, 0};        // currentRobotPosPoint
+    int frames = 0, mo_frames = 0, lm_ran = 0, n_cq = 0, n_sq = 0;
+    llsr_lm_report lm{};
+    llsr_map_report mrep{};
+    std::vector<float> keyposes;       // [keyframes][6]
+  };
+  struct {
+    bool live = false;
+    int mode = LLSR_MODE_LM_APPLIED;   // MapOptimization's LM mode
+    llsr_map_config mcfg{};
+    llsr_map* vg = nullptr;            // VoxelGrid engine of the batched downsample
+    std::vector<MapSlot> slot;
+    float4 *outl = nullptr, *ds = nullptr, *tot = nullptr, *cmap = nullptr, *smap = nullptr;
+    size_t cap_outl = 0, cap_ds = 0, cap_tot = 0, cap_cmap = 0, cap_smap = 0;
+    void* small = nullptr;             // device: pose [B][6], report [B], deg [B], matP [B][36], off [5][B+1]
+    void* hsmall = nullptr;            // pinned host mirror
+    float* d_pose = nullptr; llsr_lm_report* d_rep = nullptr; int* d_deg = nullptr; float* d_matP = nullptr;
+    int64_t* d_off = nullptr;
+    float* h_pose = nullptr; llsr_lm_report* h_rep = nullptr; int64_t* h_off = nullptr; int* h_frames = nullptr;
+    float* h_tsum = nullptr;
+  } mp;
   std::string err;
 };
 
@@ -352,6 +378,13 @@ extern "C" void llsr_destroy(llsr_handle* h) {
   if (h->mo.e1) (void)hipEventDestroy(h->mo.e1);
   for (hipEvent_t e : {h->mo.p0, h->mo.p1, h->mo.p2})
     if (e) (void)hipEventDestroy(e);
+  for (auto& sl : h->mp.slot)
+    if (sl.map) llsr_map_destroy(sl.map);
+  if (h->mp.vg) llsr_map_destroy(h->mp.vg);
+  for (void* p : {(void*)h->mp.outl, (void*)h->mp.ds, (void*)h->mp.tot, (void*)h->mp.cmap, (void*)h->mp.smap,
+                  h->mp.small})
+    if (p) (void)hipFree(p);
+  if (h->mp.hsmall) (void)hipHostFree(h->mp.hsmall);
   if (h->d_in) (void)hipFree(h->d_in);
   if (h->d_off) (void)hipFree(h->d_off);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -652,7 +685,7 @@ extern "C" int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t P, int32_t mc, 
                                          int32_t qs) {
   if (!h) return LLSR_EINVAL;
   if (P < 1 || mc < 0 || ms < 0 || qc < 0 || qs < 0 || mc > (1 << 26) || ms > (1 << 26) ||
-      qc > (1 << 24) || qs > (1 << 24))
+      qc > (1 << 20) || qs > (1 << 20))  // k_s2m_reduce keeps the per-block row prefix in LDS
     return fail(h, LLSR_EINVAL, "scan2map capacities out of range");
   HIP_OK(h, hipSetDevice(h->device));
   auto& m = h->mo;
@@ -668,10 +701,15 @@ extern "C" int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t P, int32_t mc, 
   m.log2T_s = grid_log2_table(ms);
   m.blocks_c = (qc + 255) / 256;
   m.blocks = m.blocks_c + (qs + 255) / 256;
+  // depth blocks of matAt * matA: kc >= 340 rows once N > 680 (llsr_eigen::gemm_kc), + 1 workgroup
+  // for matAt * matB / CF_all
+  m.red_blocks = (qc + qs) / 336 + 3;
   const size_t Tc = (size_t)1 << m.log2T_c, Ts = (size_t)1 << m.log2T_s;
   const size_t bytes = sizeof(S2MProb) * P + sizeof(CellSlot) * P * (Tc + Ts) +
                        sizeof(float4) * P * ((size_t)mc + ms) + sizeof(int2) * P * ((size_t)mc + ms) +
-                       sizeof(int) * 2 * P + sizeof(float) * 32 * (size_t)P * m.blocks + 4096 + 8 * 256;
+                       sizeof(int) * 2 * P + sizeof(float) * 32 * (size_t)P * m.red_blocks +
+                       sizeof(float4) * 2 * 256 * (size_t)P * m.blocks + sizeof(int) * (size_t)P * m.blocks +
+                       4096 + 10 * 256;
   if (hipMalloc(&m.pool, bytes) != hipSuccess) {
     m.pool = nullptr;
     m.P = 0;
@@ -693,7 +731,10 @@ extern "C" int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t P, int32_t mc, 
   gs.cursor = carve<int>(q, (size_t)P);
   gc.cap = mc; gs.cap = ms;
   gc.log2T = m.log2T_c; gs.log2T = m.log2T_s;
-  a.partial = carve<float>(q, 32 * (size_t)P * m.blocks);
+  a.partial = carve<float>(q, 32 * (size_t)P * m.red_blocks);
+  a.rows = carve<float4>(q, 2 * 256 * (size_t)P * m.blocks);
+  a.bcnt = carve<int>(q, (size_t)P * m.blocks);
+  a.red_blocks = m.red_blocks;
   a.n_active = carve<int>(q, 2);
   a.error = a.n_active + 1;
   a.cap_qc = qc; a.cap_qs = qs; a.cap_mc = mc; a.cap_ms = ms;
@@ -710,8 +751,19 @@ extern "C" int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t P, int32_t mc, 
   return LLSR_OK;
 }
 
+// Options of the internal scan-to-map entry (the mapping chain): the MO mode and the optimiser's
+// cross-frame members; the public entries use the handle's mode and a fresh optimiser.
+struct S2MOpts {
+  int mode = -1;  // -1: h->cfg.mode
+  const int* deg_in = nullptr;
+  const float* matP_in = nullptr;
+  int* deg_out = nullptr;
+  float* matP_out = nullptr;
+};
+
 // Validate a scan-to-map batch and enqueue the per-problem setup and both cell-grid builds.
-static int32_t s2m_prepare(llsr_handle* h, const llsr_s2m_batch* b, hipStream_t s, S2MArgs& a) {
+static int32_t s2m_prepare(llsr_handle* h, const llsr_s2m_batch* b, hipStream_t s, S2MArgs& a,
+                           const S2MOpts& opt = S2MOpts{}) {
   auto& m = h->mo;
   if (!m.pool) return fail(h, LLSR_EINVAL, "llsr_scan2map_reserve not called");
   const int P = b->n_problems;
@@ -720,7 +772,9 @@ static int32_t s2m_prepare(llsr_handle* h, const llsr_s2m_batch* b, hipStream_t 
     return fail(h, LLSR_EINVAL, "null batch array");
   a = m.a;
   a.P = P;
-  a.applied = h->cfg.mode == LLSR_MODE_LM_APPLIED;
+  a.applied = (opt.mode >= 0 ? opt.mode : h->cfg.mode) == LLSR_MODE_LM_APPLIED;
+  a.deg_in = opt.deg_in; a.matP_in = opt.matP_in;
+  a.deg_out = opt.deg_out; a.matP_out = opt.matP_out;
   a.iter_max = h->cfg.iterCountThres;
   a.step_size = h->cfg.step_size;
   a.stop_thres = h->cfg.stop_thres;
@@ -745,16 +799,13 @@ static int32_t s2m_prepare(llsr_handle* h, const llsr_s2m_batch* b, hipStream_t 
   return LLSR_OK;
 }
 
-extern "C" int32_t llsr_scan2map_batch(llsr_handle* h, const llsr_s2m_batch* b, void* hip_stream) {
-  if (!h || !b) return fail(h, LLSR_EINVAL, "null argument");
+static int32_t s2m_batch(llsr_handle* h, const llsr_s2m_batch* b, hipStream_t s, const S2MOpts& opt) {
   auto& m = h->mo;
-  HIP_OK(h, hipSetDevice(h->device));
-  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
   if (h->profiling && m.pool) HIP_OK(h, hipEventRecord(m.p0, s));
   S2MArgs a{};
   m.sh_live = false;  // one scan-to-map batch per handle at a time: this one replaces a shard batch
   m.last = s;
-  int32_t rc = s2m_prepare(h, b, s, a);
+  int32_t rc = s2m_prepare(h, b, s, a, opt);
   if (rc != LLSR_OK) return rc;
   const int P = a.P;
   if (h->profiling) HIP_OK(h, hipEventRecord(m.p1, s));
@@ -765,6 +816,7 @@ extern "C" int32_t llsr_scan2map_batch(llsr_handle* h, const llsr_s2m_batch* b, 
     const int n = (a.iter_max - it) < poll ? (a.iter_max - it) : poll;
     for (int k = 0; k < n; ++k) {
       if (m.blocks) k_s2m_iter<<<dim3(m.blocks, P), 256, 0, s>>>(a);
+      k_s2m_reduce<<<dim3(m.red_blocks, P), 256, sizeof(int) * (m.blocks + 1), s>>>(a);
       k_s2m_solve<<<(P + 63) / 64, 64, 0, s>>>(a);
     }
     it += n;
@@ -789,6 +841,13 @@ extern "C" int32_t llsr_scan2map_batch(llsr_handle* h, const llsr_s2m_batch* b, 
     m.stats.iterate_ms += it;
   }
   return LLSR_OK;
+}
+
+extern "C" int32_t llsr_scan2map_batch(llsr_handle* h, const llsr_s2m_batch* b, void* hip_stream) {
+  if (!h || !b) return fail(h, LLSR_EINVAL, "null argument");
+  HIP_OK(h, hipSetDevice(h->device));
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+  return s2m_batch(h, b, s, S2MOpts{});
 }
 
 // ---- split-correspondence scan-to-map (llsr_scan2map_shard_*): the LM loop is the caller's,
@@ -1291,5 +1350,345 @@ extern "C" int32_t llsr_odometry_fetch(llsr_handle* h, int32_t b, llsr_odom_slot
   HIP_OK(h, d2h(surf_last, (const float*)(o.last_s[cur] + hls[b]), 4 * (size_t)out->n_surf_last));
   HIP_OK(h, d2h(corner_scan, (const float*)(o.scan_c + o.h_off[b]), 4 * (size_t)out->n_corner_scan));
   HIP_OK(h, d2h(surf_scan, (const float*)(o.scan_s + o.h_off[nb + b]), 4 * (size_t)out->n_surf_scan));
+  return LLSR_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Mapping chain (MapOptimization::run, MO:1854-1896): the odometry batch, then per slot the pose
+// glue on the host (llsr_mapping.h) around batched device work — adjustOutlierCloud, one
+// segmented VoxelGrid for every slot's downsampleCurrentScan, the slots' local maps, and one
+// scan-to-map batch over all slots.
+
+namespace llsr {
+// adjustOutlierCloud (FA:2600-2610): the IP outlier cloud of slot b (d.outl, [B][HW]) with
+// x, y, z <- y, z, x, packed at off[b].
+__global__ void k_mapping_outliers(const float4* outl, int HW, const int64_t* off, float4* out) {
+  const int b = blockIdx.y;
+  const int64_t o0 = off[b], n = off[b + 1] - o0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 p = outl[(size_t)b * HW + i];
+    out[o0 + i] = make_float4(p.y, p.z, p.x, p.w);
+  }
+}
+}  // namespace llsr
+
+// Grow a device float4 buffer to hold `need` points, keeping its first `keep` points.
+static int32_t mp_grow(llsr_handle* h, float4*& p, size_t& cap, size_t need, size_t keep, hipStream_t s) {
+  if (need <= cap && p) return LLSR_OK;
+  size_t n = cap ? cap : (size_t)1 << 16;
+  while (n < need) n *= 2;
+  float4* q = nullptr;
+  if (hipMalloc(&q, n * sizeof(float4)) != hipSuccess) return fail(h, LLSR_ENOMEM, "mapping buffers");
+  if (p && keep) HIP_OK(h, hipMemcpyAsync(q, p, keep * sizeof(float4), hipMemcpyDeviceToDevice, s));
+  HIP_OK(h, sync_handle_streams(h));
+  HIP_OK(h, hipStreamSynchronize(s));
+  if (p) HIP_OK(h, hipFree(p));
+  p = q;
+  cap = n;
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_mapping_reset(llsr_handle* h) {
+  if (!h) return LLSR_EINVAL;
+  auto& mp = h->mp;
+  if (!mp.live) return fail(h, LLSR_EINVAL, "llsr_mapping_init not called");
+  int32_t rc = llsr_odometry_reset(h);
+  if (rc != LLSR_OK) return rc;
+  for (auto& sl : mp.slot) {
+    llsr_map* m = sl.map;
+    if (llsr_map_reset(m) != LLSR_OK) return fail(h, LLSR_EINVAL, "llsr_map_reset");
+    sl = llsr_handle::MapSlot{};
+    sl.map = m;
+  }
+  const int B = (int)mp.slot.size();
+  HIP_OK(h, hipMemset(mp.d_deg, 0, sizeof(int) * B));      // isDegenerate = false (MO:285)
+  HIP_OK(h, hipMemset(mp.d_matP, 0, sizeof(float) * 36 * B));  // matP zeroed (MO:286)
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_mapping_init(llsr_handle* h, int32_t mo_mode, const llsr_map_config* map_cfg) {
+  if (!h) return LLSR_EINVAL;
+  if (mo_mode != LLSR_MODE_FAITHFUL && mo_mode != LLSR_MODE_LM_APPLIED) return fail(h, LLSR_EINVAL, "mo_mode");
+  if (h->cfg.mode != LLSR_MODE_LM_APPLIED)
+    return fail(h, LLSR_ENOSYS, "the mapping chain runs the odometry, which needs LLSR_MODE_LM_APPLIED");
+  HIP_OK(h, hipSetDevice(h->device));
+  int32_t rc = odo_alloc(h);
+  if (rc != LLSR_OK) return rc;
+  auto& mp = h->mp;
+  mp.mode = mo_mode;
+  if (map_cfg) mp.mcfg = *map_cfg;
+  else llsr_map_config_default(&mp.mcfg);
+  if (!mp.live) {
+    const int B = h->max_batch;
+    mp.slot.resize(B);
+    for (auto& sl : mp.slot)
+      if (!(sl.map = llsr_map_create(&mp.mcfg, h->device))) return fail(h, LLSR_ENOMEM, "llsr_map_create");
+    if (!(mp.vg = llsr_map_create(&mp.mcfg, h->device))) return fail(h, LLSR_ENOMEM, "llsr_map_create");
+    const size_t nb = (size_t)B + 1;
+    const size_t dbytes = sizeof(float) * 6 * B + sizeof(llsr_lm_report) * B + sizeof(int) * B +
+                          sizeof(float) * 36 * B + sizeof(int64_t) * 5 * nb + 8 * 256;
+    const size_t hbytes = sizeof(float) * 6 * B + sizeof(llsr_lm_report) * B + sizeof(int64_t) * 5 * nb +
+                          sizeof(int) * B + sizeof(float) * 6 * B + 8 * 256;
+    if (hipMalloc(&mp.small, dbytes) != hipSuccess) { mp.small = nullptr; return fail(h, LLSR_ENOMEM, "mapping state"); }
+    if (hipHostMalloc(&mp.hsmall, hbytes) != hipSuccess) { mp.hsmall = nullptr; return fail(h, LLSR_ENOMEM, "mapping staging"); }
+    char* q = (char*)mp.small;
+    mp.d_pose = carve<float>(q, 6 * (size_t)B);
+    mp.d_rep = carve<llsr_lm_report>(q, B);
+    mp.d_deg = carve<int>(q, B);
+    mp.d_matP = carve<float>(q, 36 * (size_t)B);
+    mp.d_off = carve<int64_t>(q, 5 * nb);
+    q = (char*)mp.hsmall;
+    mp.h_pose = carve<float>(q, 6 * (size_t)B);
+    mp.h_rep = carve<llsr_lm_report>(q, B);
+    mp.h_off = carve<int64_t>(q, 5 * nb);
+    mp.h_frames = carve<int>(q, B);
+    mp.h_tsum = carve<float>(q, 6 * (size_t)B);
+    mp.live = true;
+  } else {
+    for (auto& sl : mp.slot) {  // a new map config: rebuild the stores
+      llsr_map_destroy(sl.map);
+      if (!(sl.map = llsr_map_create(&mp.mcfg, h->device))) return fail(h, LLSR_ENOMEM, "llsr_map_create");
+    }
+    llsr_map_destroy(mp.vg);
+    if (!(mp.vg = llsr_map_create(&mp.mcfg, h->device))) return fail(h, LLSR_ENOMEM, "llsr_map_create");
+  }
+  return llsr_mapping_reset(h);
+}
+
+extern "C" int32_t llsr_mapping_batch(llsr_handle* h, const float* d_xyzi, const int64_t* d_offsets, int32_t B,
+                                      void* hip_stream) {
+  if (!h) return LLSR_EINVAL;
+  auto& mp = h->mp;
+  if (!mp.live) return fail(h, LLSR_EINVAL, "llsr_mapping_init not called");
+  if (B < 1 || B > h->max_batch) return fail(h, LLSR_ERANGE, "batch size outside [1, max_batch]");
+  HIP_OK(h, hipSetDevice(h->device));
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+  int32_t rc = llsr_odometry_batch(h, d_xyzi, d_offsets, B, s);
+  if (rc != LLSR_OK) return rc;
+  auto& o = h->odo;
+  const int NB = o.B, nb = NB + 1;
+  // this frame's AssociationOut clouds (the batch flipped o.cur to them)
+  const int64_t* hs = o.h_off;                     // cloud_corner_scan (sharp, TransformToEnd)
+  const int64_t* hf = o.h_off + nb;                // cloud_surf_scan (flat + shadow, TransformToEnd)
+  const int64_t* hlc = o.h_off + (2 + o.cur) * nb; // cloud_corner_last
+  const int64_t* hls = o.h_off + (4 + o.cur) * nb; // cloud_surf_last (+ shadow)
+  HIP_OK(h, hipMemcpyAsync(mp.h_frames, o.frames, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+  HIP_OK(h, hipMemcpyAsync(mp.h_tsum, o.tsum, sizeof(float) * 6 * B, hipMemcpyDeviceToHost, s));
+  HIP_OK(h, hipStreamSynchronize(s));
+  rc = llsr_scan2scan_check(h);
+  if (rc != LLSR_OK) return rc;
+  std::vector<char> step(NB, 0);  // slots that receive an AssociationOut this call
+  for (int b = 0; b < B; ++b) {
+    auto& sl = mp.slot[b];
+    sl.frames = mp.h_frames[b];
+    step[b] = sl.frames >= 2;
+    if (!step[b]) continue;
+    llsr_mapping::odometry_roundtrip(mp.h_tsum + 6 * b, sl.pose.transformSum);  // OdometryToTransform
+    llsr_mapping::transform_associate_to_map(sl.pose);
+  }
+  // adjustOutlierCloud of this frame's IP outliers (FA:2720)
+  int64_t* hol = mp.h_off + 4 * (size_t)nb;
+  hol[0] = 0;
+  int maxO = 0;
+  for (int b = 0; b < NB; ++b) {
+    const int n = (b < B && step[b]) ? o.h_counts[(size_t)b * kCnt + C_O] : 0;
+    hol[b + 1] = hol[b] + n;
+    maxO = n > maxO ? n : maxO;
+  }
+  rc = mp_grow(h, mp.outl, mp.cap_outl, (size_t)hol[NB] + 1, 0, s);
+  if (rc != LLSR_OK) return rc;
+  HIP_OK(h, hipMemcpyAsync(mp.d_off + 4 * (size_t)nb, hol, sizeof(int64_t) * nb, hipMemcpyHostToDevice, s));
+  if (maxO > 0) {
+    const int gx = (maxO + 255) / 256 < 64 ? (maxO + 255) / 256 : 64;
+    k_mapping_outliers<<<dim3(gx, B), 256, 0, s>>>(h->d.outl, h->dc.HW, mp.d_off + 4 * (size_t)nb, mp.outl);
+    HIP_OK(h, hipGetLastError());
+  }
+  // downsampleCurrentScan (MO:1234-1258) of every slot in one segmented VoxelGrid; segments by
+  // kind so each kind's per-slot results are contiguous: [corner last][surf last, outlier]...
+  // [corner scan][surf scan]
+  const float lc = mp.mcfg.corner_leaf, lsf = mp.mcfg.surf_leaf, lo = mp.mcfg.outlier_leaf;
+  const int S5 = 5 * NB;
+  std::vector<const float4*> src(S5);
+  std::vector<long long> cnt(S5, 0), dso(S5 + 1), toto(NB + 1);
+  std::vector<float> leaf(S5);
+  long long total = 0;
+  for (int b = 0; b < NB; ++b) {
+    const bool on = b < B && step[b];
+    src[b] = o.last_c[o.cur] + hlc[b];          cnt[b] = on ? hlc[b + 1] - hlc[b] : 0;          leaf[b] = lc;
+    src[NB + 2 * b] = o.last_s[o.cur] + hls[b]; cnt[NB + 2 * b] = on ? hls[b + 1] - hls[b] : 0; leaf[NB + 2 * b] = lsf;
+    src[NB + 2 * b + 1] = mp.outl + hol[b];     cnt[NB + 2 * b + 1] = hol[b + 1] - hol[b];      leaf[NB + 2 * b + 1] = lo;
+    src[3 * NB + b] = o.scan_c + hs[b];         cnt[3 * NB + b] = on ? hs[b + 1] - hs[b] : 0;   leaf[3 * NB + b] = lc;
+    src[4 * NB + b] = o.scan_s + hf[b];         cnt[4 * NB + b] = on ? hf[b + 1] - hf[b] : 0;   leaf[4 * NB + b] = lsf;
+  }
+  for (long long c : cnt) total += c;
+  rc = mp_grow(h, mp.ds, mp.cap_ds, (size_t)total + 1, 0, s);
+  if (rc != LLSR_OK) return rc;
+  rc = llsr_mapping::voxel_multi(mp.vg, src.data(), cnt.data(), leaf.data(), S5, mp.ds, dso.data(), s);
+  if (rc != LLSR_OK) return fail(h, rc, std::string("downsample: ") + llsr_map_last_error(mp.vg));
+  // laserCloudSurfTotalLastDS = surf leaf over SurfLastDS + OutlierLastDS (MO:1260-1266)
+  std::vector<const float4*> tsrc(NB);
+  std::vector<long long> tcnt(NB);
+  std::vector<float> tleaf(NB, lsf);
+  for (int b = 0; b < NB; ++b) {
+    tsrc[b] = mp.ds + dso[NB + 2 * b];
+    tcnt[b] = dso[NB + 2 * b + 2] - dso[NB + 2 * b];
+  }
+  rc = mp_grow(h, mp.tot, mp.cap_tot, (size_t)(dso[3 * NB] - dso[NB]) + 1, 0, s);
+  if (rc != LLSR_OK) return rc;
+  rc = llsr_mapping::voxel_multi(mp.vg, tsrc.data(), tcnt.data(), tleaf.data(), NB, mp.tot, toto.data(), s);
+  if (rc != LLSR_OK) return fail(h, rc, std::string("downsample: ") + llsr_map_last_error(mp.vg));
+  // extractSurroundingKeyFrames (MO:1096-1232) per slot around currentRobotPosPoint
+  int64_t* hcq = mp.h_off;
+  int64_t* hsq = mp.h_off + nb;
+  int64_t* hmc = mp.h_off + 2 * (size_t)nb;
+  int64_t* hms = mp.h_off + 3 * (size_t)nb;
+  hmc[0] = hms[0] = 0;
+  long long mMc = 1, mMs = 1, mQc = 1, mQs = 1;
+  for (int b = 0; b < NB; ++b) {
+    hcq[b] = dso[3 * NB + b];
+    hsq[b] = toto[b];
+    auto& sl = mp.slot[b];
+    long long nc = 0, ns = 0;
+    if (b < B && step[b]) {
+      sl.mrep = llsr_map_report{};
+      if (llsr_map_num_keyframes(sl.map) > 0) {
+        for (int attempt = 0;; ++attempt) {
+          rc = llsr_map_extract(sl.map, sl.robot, (float*)(mp.cmap + hmc[b]), (int64_t)mp.cap_cmap - hmc[b],
+                                (float*)(mp.smap + hms[b]), (int64_t)mp.cap_smap - hms[b], &sl.mrep, s);
+          if (rc == LLSR_ERANGE && attempt == 0) {
+            int32_t g = mp_grow(h, mp.cmap, mp.cap_cmap, (size_t)(hmc[b] + sl.mrep.n_corner_ds), hmc[b], s);
+            if (g == LLSR_OK)
+              g = mp_grow(h, mp.smap, mp.cap_smap, (size_t)(hms[b] + sl.mrep.n_surf_ds), hms[b], s);
+            if (g != LLSR_OK) return g;
+            continue;
+          }
+          if (rc != LLSR_OK) return fail(h, rc, std::string("extract: ") + llsr_map_last_error(sl.map));
+          break;
+        }
+        nc = sl.mrep.n_corner_ds;
+        ns = sl.mrep.n_surf_ds;
+      }
+      sl.n_cq = (int)(dso[3 * NB + b + 1] - dso[3 * NB + b]);
+      sl.n_sq = (int)(toto[b + 1] - toto[b]);
+    }
+    hmc[b + 1] = hmc[b] + nc;
+    hms[b + 1] = hms[b] + ns;
+    mMc = nc > mMc ? nc : mMc;
+    mMs = ns > mMs ? ns : mMs;
+    const long long qc = dso[3 * NB + b + 1] - dso[3 * NB + b], qs = toto[b + 1] - toto[b];
+    mQc = qc > mQc ? qc : mQc;
+    mQs = qs > mQs ? qs : mQs;
+  }
+  hcq[NB] = dso[4 * NB];
+  hsq[NB] = toto[NB];
+  if (!mp.cmap) { rc = mp_grow(h, mp.cmap, mp.cap_cmap, 1, 0, s); if (rc != LLSR_OK) return rc; }
+  if (!mp.smap) { rc = mp_grow(h, mp.smap, mp.cap_smap, 1, 0, s); if (rc != LLSR_OK) return rc; }
+  // scan2MapOptimization (MO:1572-1610): every slot is a problem; slots without a step, or whose
+  // map fails MO:1573, stay inactive and keep their pose and LM members
+  rc = llsr_scan2map_reserve(h, NB, (int32_t)mMc, (int32_t)mMs, (int32_t)mQc, (int32_t)mQs);
+  if (rc != LLSR_OK) return rc;
+  for (int b = 0; b < NB; ++b)
+    for (int k = 0; k < 6; ++k) mp.h_pose[6 * b + k] = mp.slot[b].pose.transformTobeMapped[k];
+  HIP_OK(h, hipMemcpyAsync(mp.d_pose, mp.h_pose, sizeof(float) * 6 * NB, hipMemcpyHostToDevice, s));
+  HIP_OK(h, hipMemcpyAsync(mp.d_off, mp.h_off, sizeof(int64_t) * 4 * nb, hipMemcpyHostToDevice, s));
+  llsr_s2m_batch sb{};
+  sb.n_problems = NB;
+  sb.corner_q = (const float*)mp.ds; sb.corner_q_off = mp.d_off;
+  sb.surf_q = (const float*)mp.tot; sb.surf_q_off = mp.d_off + nb;
+  sb.corner_map = (const float*)mp.cmap; sb.corner_map_off = mp.d_off + 2 * (size_t)nb;
+  sb.surf_map = (const float*)mp.smap; sb.surf_map_off = mp.d_off + 3 * (size_t)nb;
+  sb.pose = mp.d_pose;
+  sb.report = mp.d_rep;
+  S2MOpts opt;
+  opt.mode = mp.mode;
+  opt.deg_in = opt.deg_out = mp.d_deg;
+  opt.matP_in = opt.matP_out = mp.d_matP;
+  rc = s2m_batch(h, &sb, s, opt);
+  if (rc != LLSR_OK) return rc;
+  HIP_OK(h, hipMemcpyAsync(mp.h_pose, mp.d_pose, sizeof(float) * 6 * NB, hipMemcpyDeviceToHost, s));
+  HIP_OK(h, hipMemcpyAsync(mp.h_rep, mp.d_rep, sizeof(llsr_lm_report) * NB, hipMemcpyDeviceToHost, s));
+  HIP_OK(h, hipStreamSynchronize(s));
+  // transformUpdate (MO:1608) and saveKeyFramesAndFactor (MO:1612-1755)
+  for (int b = 0; b < B; ++b) {
+    if (!step[b]) continue;
+    auto& sl = mp.slot[b];
+    auto& P = sl.pose;
+    sl.lm = mp.h_rep[b];
+    sl.lm_ran = (hmc[b + 1] - hmc[b] > 10 && hms[b + 1] - hms[b] > 100) ? 1 : 0;
+    if (sl.lm_ran) {
+      for (int k = 0; k < 6; ++k) P.transformTobeMapped[k] = mp.h_pose[6 * b + k];
+      llsr_mapping::transform_update(P);
+    }
+    for (int k = 0; k < 3; ++k) sl.robot[k] = P.transformAftMapped[3 + k];
+    const bool first = llsr_map_num_keyframes(sl.map) == 0;
+    const float* est = first ? P.transformTobeMapped : P.transformAftMapped;  // iSAM2's latestEstimate
+    const float kp[6] = {est[3], est[4], est[5], est[0], est[1], est[2]};
+    for (int k = 0; k < 6; ++k) {
+      P.transformLast[k] = est[k];
+      if (!first) P.transformTobeMapped[k] = P.transformAftMapped[k];
+    }
+    const int kf = llsr_map_add_keyframe(
+        sl.map, kp, (const float*)(o.scan_c + hs[b]), (int32_t)(hs[b + 1] - hs[b]),
+        (const float*)(mp.ds + dso[NB + 2 * b]), (int32_t)(dso[NB + 2 * b + 1] - dso[NB + 2 * b]),
+        (const float*)(mp.ds + dso[NB + 2 * b + 1]), (int32_t)(dso[NB + 2 * b + 2] - dso[NB + 2 * b + 1]), s);
+    if (kf < 0) return fail(h, kf, std::string("add_keyframe: ") + llsr_map_last_error(sl.map));
+    sl.keyposes.insert(sl.keyposes.end(), kp, kp + 6);
+    sl.mo_frames += 1;
+  }
+  HIP_OK(h, hipEventRecord(h->last_done, s));
+  h->last_stream = s;
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_mapping_fetch(llsr_handle* h, int32_t b, llsr_mapping_slot* out) {
+  if (!h || !out) return LLSR_EINVAL;
+  auto& mp = h->mp;
+  if (!mp.live) return fail(h, LLSR_EINVAL, "llsr_mapping_init not called");
+  if (b < 0 || b >= (int)mp.slot.size()) return fail(h, LLSR_ERANGE, "slot outside [0, max_batch)");
+  const auto& sl = mp.slot[b];
+  std::memset(out, 0, sizeof *out);
+  out->frames = sl.frames;
+  out->mo_frames = sl.mo_frames;
+  out->keyframes = (int32_t)(sl.keyposes.size() / 6);
+  out->lm_ran = sl.lm_ran;
+  for (int k = 0; k < 6; ++k) {
+    out->transform_sum[k] = sl.pose.transformSum[k];
+    out->transform_tobe_mapped[k] = sl.pose.transformTobeMapped[k];
+    out->transform_bef_mapped[k] = sl.pose.transformBefMapped[k];
+    out->transform_aft_mapped[k] = sl.pose.transformAftMapped[k];
+  }
+  out->n_corner_q = sl.n_cq;
+  out->n_surf_q = sl.n_sq;
+  out->lm = sl.lm;
+  out->map = sl.mrep;
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_mapping_keyposes(llsr_handle* h, int32_t b, float* out, int32_t cap) {
+  if (!h) return LLSR_EINVAL;
+  auto& mp = h->mp;
+  if (!mp.live) return fail(h, LLSR_EINVAL, "llsr_mapping_init not called");
+  if (b < 0 || b >= (int)mp.slot.size()) return fail(h, LLSR_ERANGE, "slot outside [0, max_batch)");
+  const auto& kp = mp.slot[b].keyposes;
+  const int n = (int)(kp.size() / 6);
+  if (out && cap > 0) std::memcpy(out, kp.data(), sizeof(float) * 6 * (size_t)(n < cap ? n : cap));
+  return n;
+}
+
+extern "C" int32_t llsr_mapping_associate(const float* ts_fa, const float* bef, const float* aft, float* ts,
+                                          float* tobe, float* incre) {
+  if (!ts_fa || !bef || !aft || !ts || !tobe) return LLSR_EINVAL;
+  llsr_mapping::MoPoses P;
+  for (int k = 0; k < 6; ++k) {
+    P.transformBefMapped[k] = bef[k];
+    P.transformAftMapped[k] = aft[k];
+  }
+  llsr_mapping::odometry_roundtrip(ts_fa, P.transformSum);
+  llsr_mapping::transform_associate_to_map(P);
+  for (int k = 0; k < 6; ++k) {
+    ts[k] = P.transformSum[k];
+    tobe[k] = P.transformTobeMapped[k];
+    if (incre) incre[k] = P.transformIncre[k];
+  }
   return LLSR_OK;
 }

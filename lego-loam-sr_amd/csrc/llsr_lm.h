@@ -44,16 +44,12 @@ LLSR_HD void ne_to_red(const long long* w, float* red) {
 // of pose[0..2]), matP[36], matX0[6], min_lambda, cf_mean, degenerate — matP and degenerate are
 // MapOptimization members (mapOptimization.h:279-281): set at iteration 0 and reused after.
 // `red`: AtA upper triangle (21), AtB (6), sum |d|, #corner, #surf. Returns the stop test.
+// lm_update_full: the same on the full column-major matAtA[36], matAtB[6], CF_all and N.
 template <class St>
-LLSR_HD bool lm_update(St& st, const float* red, int iterCount, bool applied, float stop_thres) {
+LLSR_HD bool lm_update_full(St& st, const float* AtA, const float* AtB, float cf_all, int N, int iterCount,
+                            bool applied, float stop_thres) {
   using llsr_libm::cosf_;
   using llsr_libm::sinf_;
-  const int N = (int)red[28] + (int)red[29];
-  float AtA[36], AtB[6];
-  int q = 0;
-  for (int r = 0; r < 6; ++r)
-    for (int c = r; c < 6; ++c, ++q) { AtA[r + 6 * c] = red[q]; AtA[c + 6 * r] = red[q]; }
-  for (int c = 0; c < 6; ++c) AtB[c] = red[21 + c];
   float X[6];
   llsr_eigen::colpiv_qr_solve<6, 6>(AtA, AtB, X);  // matAtA.colPivHouseholderQr().solve(matAtB)
   if (iterCount == 0) {  // MO:1507-1531
@@ -91,8 +87,18 @@ LLSR_HD bool lm_update(St& st, const float* red, int iterCount, bool applied, fl
   const double t0 = (double)(X[3] * 100), t1 = (double)(X[4] * 100), t2 = (double)(X[5] * 100);
   const float deltaR = (float)__builtin_sqrt(e0 * e0 + e1 * e1 + e2 * e2);
   const float deltaT = (float)__builtin_sqrt(t0 * t0 + t1 * t1 + t2 * t2);
-  st.cf_mean = red[27] / (float)N;
+  st.cf_mean = cf_all / (float)N;
   return deltaR < stop_thres && deltaT < stop_thres;
+}
+
+template <class St>
+LLSR_HD bool lm_update(St& st, const float* red, int iterCount, bool applied, float stop_thres) {
+  const int N = (int)red[28] + (int)red[29];
+  float AtA[36];
+  int q = 0;
+  for (int r = 0; r < 6; ++r)
+    for (int c = r; c < 6; ++c, ++q) { AtA[r + 6 * c] = red[q]; AtA[c + 6 * r] = red[q]; }
+  return lm_update_full(st, AtA, red + 21, red[27], N, iterCount, applied, stop_thres);
 }
 
 }  // namespace llsr_lm

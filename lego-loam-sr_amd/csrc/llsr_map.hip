@@ -33,6 +33,7 @@
 
 #include "../../include/llsr.h"
 #include "llsr_libm.h"
+#include "llsr_mapping.h"
 
 namespace {
 
@@ -475,6 +476,16 @@ extern "C" int32_t llsr_map_downsample_scan(llsr_map* m, const float* cl, int32_
   for (int k = 0; k < 6; ++k) out_off[k] = o[k];
   out_off[6] = o[5] + t[1];
   return LLSR_OK;
+}
+
+// The mapping chain's batched downsampleCurrentScan (llsr_mapping.h): one segmented VoxelGrid over
+// clouds at arbitrary device addresses, all slots at once.
+int32_t llsr_mapping::voxel_multi(llsr_map* m, const float4* const* src, const long long* n, const float* leaf,
+                                  int S, float4* out, long long* out_off, hipStream_t s) {
+  if (!m || S < 1) return LLSR_EINVAL;
+  std::vector<VgCloud> cl(S);
+  for (int k = 0; k < S; ++k) cl[k] = {src[k], n[k], leaf[k]};
+  return vg_run(m, cl, out, out_off, s);
 }
 
 extern "C" int32_t llsr_map_add_keyframe(llsr_map* m, const float pose[6], const float* c, int32_t nc,

@@ -191,7 +191,10 @@ __global__ void k_s2m_setup(S2MArgs a) {
   }
 #pragma unroll
   for (int k = 0; k < 6; ++k) { st.pose[k] = a.pose[6 * p + k]; st.matX0[k] = 0.0f; }
-  st.iter = 0; st.converged = 0; st.degenerate = 0; st.nc = 0; st.ns = 0;
+  st.iter = 0; st.converged = 0; st.nc = 0; st.ns = 0;
+  st.degenerate = a.deg_in ? a.deg_in[p] : 0;
+  if (a.matP_in)
+    for (int k = 0; k < 36; ++k) st.matP[k] = a.matP_in[36 * p + k];
   st.min_lambda = 0.0f; st.cf_mean = 0.0f;
   st.active = (!bad && st.Mc > 10 && st.Ms > 100) ? 1 : 0;  // MO:1573
   st.cR = cosf_(st.pose[0]); st.sR = sinf_(st.pose[0]);
@@ -219,16 +222,14 @@ __device__ void lm_step(const S2MArgs& a, S2MProb& st, const float* red) {
   }
 }
 
-// What one query contributes (cornerOptimization MO:1274-1375 / surfOptimization MO:1383-1440,
-// then the Jacobian row of LMOptimization MO:1465-1490): v[0..20] the AtA upper triangle,
-// v[21..26] AtB, v[27] |coeff.intensity|, v[28] / v[29] = 1 for a corner / surf
-// correspondence; all zero without one.
+// One query of cornerOptimization (MO:1274-1375) / surfOptimization (MO:1383-1440) at the current
+// pose: false without a correspondence, else its Jacobian row (LMOptimization MO:1465-1490), the
+// right-hand side matB = -step_size * coeff.intensity and |coeff.intensity| (MO:1558).
 template <bool kCorner>
-__device__ __forceinline__ void query_terms(const S2MArgs& a, const S2MProb& st, int p, int qi, float* v) {
-#pragma unroll
-  for (int k = 0; k < kRed; ++k) v[k] = 0.0f;
+__device__ __forceinline__ bool query_row(const S2MArgs& a, const S2MProb& st, int p, int qi, float* J, float& bb,
+                                          float& ald) {
   const int Q = kCorner ? st.Qc : st.Qs;
-  if (qi >= Q) return;
+  if (qi >= Q) return false;
   const float4 q = reinterpret_cast<const float4*>(kCorner ? a.cq : a.sq)[(kCorner ? st.qc0 : st.qs0) + qi];
   Assoc as{st.cR, st.sR, st.cP, st.sP, st.cY, st.sY, st.pose[3], st.pose[4], st.pose[5]};
   float x0, y0, z0;
@@ -244,20 +245,32 @@ __device__ __forceinline__ void query_terms(const S2MArgs& a, const S2MProb& st,
     ok = surf_coeff(a.grids.g[1].table(p), a.grids.g[1].log2T, a.grids.g[1].cells(p), mp,
                     x0, y0, z0, la, lb, lc, ld);
   }
-  if (!ok) return;
+  if (!ok) return false;
   // Jacobian row (MO:1465-1490) at the current pose; srx.. are the same sin/cos values
   const float srx = st.sR, crx = st.cR, sry = st.sP, cry = st.cP, srz = st.sY, crz = st.cY;
   const float px = q.x, py = q.y, pz = q.z;
-  const float arx = (crx * sry * srz * px + crx * crz * sry * py - srx * sry * pz) * la +
-                    (-srx * srz * px - crz * srx * py - crx * pz) * lb +
-                    (crx * cry * srz * px + crx * cry * crz * py - cry * srx * pz) * lc;
-  const float ary = ((cry * srx * srz - crz * sry) * px + (sry * srz + cry * crz * srx) * py + crx * cry * pz) * la +
-                    ((-cry * crz - srx * sry * srz) * px + (cry * srz - crz * srx * sry) * py - crx * sry * pz) * lc;
-  const float arz = ((crz * srx * sry - cry * srz) * px + (-cry * crz - srx * sry * srz) * py) * la +
-                    (crx * crz * px - crx * srz * py) * lb +
-                    ((sry * srz + cry * crz * srx) * px + (crz * sry - cry * srx * srz) * py) * lc;
-  const float J[6] = {arx, ary, arz, la, lb, lc};
-  const float bb = -a.step_size * ld;
+  J[0] = (crx * sry * srz * px + crx * crz * sry * py - srx * sry * pz) * la +
+         (-srx * srz * px - crz * srx * py - crx * pz) * lb +
+         (crx * cry * srz * px + crx * cry * crz * py - cry * srx * pz) * lc;
+  J[1] = ((cry * srx * srz - crz * sry) * px + (sry * srz + cry * crz * srx) * py + crx * cry * pz) * la +
+         ((-cry * crz - srx * sry * srz) * px + (cry * srz - crz * srx * sry) * py - crx * sry * pz) * lc;
+  J[2] = ((crz * srx * sry - cry * srz) * px + (-cry * crz - srx * sry * srz) * py) * la +
+         (crx * crz * px - crx * srz * py) * lb +
+         ((sry * srz + cry * crz * srx) * px + (crz * sry - cry * srx * srz) * py) * lc;
+  J[3] = la; J[4] = lb; J[5] = lc;
+  bb = -a.step_size * ld;
+  ald = fabs_(ld);
+  return true;
+}
+
+// The split mode's per-query words: v[0..20] the AtA upper triangle, v[21..26] AtB, v[27]
+// |coeff.intensity|, v[28] / v[29] = 1 for a corner / surf correspondence; all zero without one.
+template <bool kCorner>
+__device__ __forceinline__ void query_terms(const S2MArgs& a, const S2MProb& st, int p, int qi, float* v) {
+#pragma unroll
+  for (int k = 0; k < kRed; ++k) v[k] = 0.0f;
+  float J[6], bb, ald;
+  if (!query_row<kCorner>(a, st, p, qi, J, bb, ald)) return;
   int k = 0;
 #pragma unroll
   for (int r = 0; r < 6; ++r)
@@ -265,29 +278,39 @@ __device__ __forceinline__ void query_terms(const S2MArgs& a, const S2MProb& st,
     for (int c = r; c < 6; ++c, ++k) v[k] = J[r] * J[c];
 #pragma unroll
   for (int c = 0; c < 6; ++c) v[21 + c] = J[c] * bb;
-  v[27] = fabs_(ld);
+  v[27] = ald;
   v[kCorner ? 28 : 29] = 1.0f;
 }
 
-// One block of queries: kCorner = corner queries (partial slots [0, blocks_c)), else surf queries
-// (partial slots [blocks_c, blocks)).
+// ---- the float path (llsr_scan2map_batch): Eigen's summation order ------------------------
+// LMOptimization's matA rows are the correspondences in laserCloudOri order: the corner queries
+// that found one, in query order, then the surf queries (MO:1582-1583). k_s2m_iter writes each
+// 256-query block's rows compacted in that order (a.rows, 8 floats: J[6], matB, |intensity|) and
+// the block's row count; k_s2m_reduce then sums them exactly as the reference's Eigen 3.3.7 build
+// does (llsr_eigen.h, oracle_eigen.h gemm_ata / gemv_atb): matAt * matA per GEMM depth block of kc
+// rows (one workgroup per block, from zero, rows 4-5 x columns 0-3 through gebp's four-accumulator
+// path), matAt * matB and CF_all left to right over all rows (the last workgroup); k_s2m_solve adds
+// the depth blocks in order. The result is bit-identical to the oracle's statement.
 template <bool kCorner>
 __device__ __forceinline__ void s2m_block(const S2MArgs& a, int p, int qb) {
   const S2MProb& st = a.prob[p];
   if (!st.active) return;
-  __shared__ float wsum[4][kRed];
-  float v[kRed];
-  query_terms<kCorner>(a, st, p, qb * 256 + threadIdx.x, v);
-  // fixed-order block reduction: wave butterfly, then waves 0..3 in order
-  const int w = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < kRed; ++k) {
-    const float s = wave_reduce_add(v[k]);
-    if (lane_id() == 0) wsum[w][k] = s;
-  }
+  __shared__ int wcnt[4];
+  float J[6], bb = 0.0f, ald = 0.0f;
+  const bool ok = query_row<kCorner>(a, st, p, qb * 256 + threadIdx.x, J, bb, ald);
+  const unsigned long long m = __ballot(ok);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) wcnt[w] = __popcll(m);
   __syncthreads();
-  float* part = a.partial + ((size_t)p * a.blocks + (kCorner ? 0 : a.blocks_c) + qb) * 32;
-  if (threadIdx.x < kRed) part[threadIdx.x] = ((wsum[0][threadIdx.x] + wsum[1][threadIdx.x]) + wsum[2][threadIdx.x]) + wsum[3][threadIdx.x];
+  const int gb = (kCorner ? 0 : a.blocks_c) + qb;
+  int base = 0;
+  for (int k = 0; k < w; ++k) base += wcnt[k];
+  if (ok) {
+    float4* r = a.rows + (((size_t)p * a.blocks + gb) * 256 + base + __popcll(m & ((1ull << lane) - 1))) * 2;
+    r[0] = make_float4(J[0], J[1], J[2], J[3]);
+    r[1] = make_float4(J[4], J[5], bb, ald);
+  }
+  if (threadIdx.x == 0) a.bcnt[(size_t)p * a.blocks + gb] = (wcnt[0] + wcnt[1]) + (wcnt[2] + wcnt[3]);
 }
 
 // grid (blocks, P): corner blocks first, then surf blocks; the branch is block-uniform.
@@ -298,19 +321,156 @@ __global__ __launch_bounds__(256) void k_s2m_iter(S2MArgs a) {
     s2m_block<false>(a, blockIdx.y, blockIdx.x - a.blocks_c);
 }
 
+namespace {
+constexpr int kMaxKc = 680;     // llsr_eigen::gemm_kc's ceiling with a 32 KiB L1 (rows per depth block)
+constexpr int kRedWords = 29;   // AtA: 21 upper-triangle entries + the 8 of rows 4-5 x columns 0-3
 
-// One thread per problem: block partials summed in block order, then the LM step.
+// Exclusive prefix of the problem's block row counts into pre[0..blocks] (LDS).
+__device__ void block_prefix(const S2MArgs& a, int p, int* pre, int* tmp) {
+  const int nb = a.blocks, t = threadIdx.x;
+  const int per = (nb + 255) / 256, b0 = t * per, b1 = min(nb, b0 + per);
+  const int* cnt = a.bcnt + (size_t)p * nb;
+  int s = 0;
+  for (int b = b0; b < b1; ++b) s += cnt[b];
+  tmp[t] = s;
+  __syncthreads();
+  if (t == 0) {
+    int acc = 0;
+    for (int k = 0; k < 256; ++k) { const int v = tmp[k]; tmp[k] = acc; acc += v; }
+  }
+  __syncthreads();
+  s = tmp[t];
+  for (int b = b0; b < b1; ++b) { pre[b] = s; s += cnt[b]; }
+  if (b1 == nb && b0 < b1) pre[nb] = s;
+  if (nb == 0 && t == 0) pre[0] = 0;
+  __syncthreads();
+}
+
+// Rows [r0, r0 + d) of the problem's matA into lrow (LDS, 2 float4 per row).
+__device__ void gather_rows(const S2MArgs& a, int p, const int* pre, int r0, int d, float4* lrow) {
+  const int nb = a.blocks;
+  for (int i = threadIdx.x; i < d; i += blockDim.x) {
+    const int g = r0 + i;
+    int lo = 0, hi = nb - 1;  // the block b with pre[b] <= g < pre[b + 1]
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pre[mid] <= g) lo = mid;
+      else hi = mid - 1;
+    }
+    const float4* src = a.rows + (((size_t)p * nb + lo) * 256 + (g - pre[lo])) * 2;
+    lrow[2 * i] = src[0];
+    lrow[2 * i + 1] = src[1];
+  }
+}
+}  // namespace
+
+// grid (red_blocks, P), 256 threads: workgroup x < nkb sums depth block x of matAt * matA; the last
+// workgroup sums matAt * matB and CF_all over every row.
+__global__ __launch_bounds__(256) void k_s2m_reduce(S2MArgs a) {
+  const int p = blockIdx.y;
+  const S2MProb& st = a.prob[p];
+  if (!st.active) return;
+  extern __shared__ int sm_pre[];                  // [blocks + 1]
+  __shared__ int tmp[256];
+  __shared__ float4 lrow[2 * kMaxKc];
+  block_prefix(a, p, sm_pre, tmp);
+  const int N = sm_pre[a.blocks];
+  float* part = a.partial + ((size_t)p * a.red_blocks + blockIdx.x) * 32;
+  const int t = threadIdx.x;
+  if ((int)blockIdx.x == a.red_blocks - 1) {
+    // matAtB = matAt * matB (lazy product: from the first product, left to right) and CF_all
+    float acc = 0.0f;
+    for (int r0 = 0; r0 < N; r0 += kMaxKc) {
+      const int d = min(kMaxKc, N - r0);
+      gather_rows(a, p, sm_pre, r0, d, lrow);
+      __syncthreads();
+      if (t < 7) {
+        const float* lr = reinterpret_cast<const float*>(lrow);
+        for (int q = 0; q < d; ++q) {
+          const float* row = lr + 8 * q;
+          if (t < 6) acc = (r0 + q == 0) ? row[t] * row[6] : acc + row[t] * row[6];
+          else acc = acc + row[7];
+        }
+      }
+      __syncthreads();
+    }
+    if (t < 7) part[t] = acc;
+    if (t == 7) part[7] = __int_as_float(sm_pre[a.blocks_c]);  // corner correspondences
+    if (t == 8) part[8] = __int_as_float(N);
+    return;
+  }
+  if (N < 50) return;  // MO:1453: no solve this iteration
+  const int kc = llsr_eigen::gemm_kc(N, 6, 6);
+  const int x = blockIdx.x;
+  const int r0 = x * kc;
+  if (r0 >= N) return;
+  const int d = min(kc, N - r0);
+  gather_rows(a, p, sm_pre, r0, d, lrow);
+  __syncthreads();
+  if (t < kRedWords) {
+    const float* lr = reinterpret_cast<const float*>(lrow);
+    float c;
+    if (t < 21) {  // upper triangle (i <= j), row-major order: c = c + a_i * a_j from zero
+      int i = 0, k = t;
+      while (k >= 6 - i) { k -= 6 - i; ++i; }
+      const int j = i + k;
+      c = 0.0f;
+      for (int q = 0; q < d; ++q) c = c + lr[8 * q + i] * lr[8 * q + j];
+    } else {       // (i, j), i in {4, 5}, j in {0..3}: gebp's swapped 1 x 4 path
+      const int i = 4 + (t - 21) / 4, j = (t - 21) % 4;
+      float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f, C3 = 0.0f;
+      const int endk4 = (d / 4) * 4;
+      int q = 0;
+      for (; q < endk4; q += 4) {
+        C0 = lr[8 * q + j] * lr[8 * q + i] + C0;
+        C1 = lr[8 * (q + 1) + j] * lr[8 * (q + 1) + i] + C1;
+        C2 = lr[8 * (q + 2) + j] * lr[8 * (q + 2) + i] + C2;
+        C3 = lr[8 * (q + 3) + j] * lr[8 * (q + 3) + i] + C3;
+      }
+      c = (C0 + C1) + (C2 + C3);
+      for (; q < d; ++q) c = lr[8 * q + j] * lr[8 * q + i] + c;
+    }
+    part[t] = c;
+  }
+}
+
+// One thread per problem: the depth blocks added in order (res = res + 1.0f * block), then the LM
+// step on the full matAtA (not symmetric in the last bits: rows 4-5 x columns 0-3).
 __global__ __launch_bounds__(64) void k_s2m_solve(S2MArgs a) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= a.P) return;
   S2MProb& st = a.prob[p];
   if (!st.active) return;
-  float red[kRed];
-  for (int k = 0; k < kRed; ++k) red[k] = 0.0f;
-  const float* pp = a.partial + (size_t)p * a.blocks * 32;
-  for (int b = 0; b < a.blocks; ++b)
-    for (int k = 0; k < kRed; ++k) red[k] += pp[(size_t)b * 32 + k];
-  lm_step(a, st, red);
+  const float* last = a.partial + ((size_t)p * a.red_blocks + a.red_blocks - 1) * 32;
+  const int N = __float_as_int(last[8]);
+  const int nc = __float_as_int(last[7]);
+  st.iter += 1;
+  const int iterCount = st.iter - 1;
+  st.nc = nc;
+  st.ns = N - nc;
+  bool conv = false;
+  if (N >= 50) {  // MO:1453
+    const int kc = llsr_eigen::gemm_kc(N, 6, 6);
+    const int nkb = (N + kc - 1) / kc;
+    float w[kRedWords];
+    for (int e = 0; e < kRedWords; ++e) w[e] = 0.0f;
+    for (int x = 0; x < nkb; ++x) {
+      const float* pp = a.partial + ((size_t)p * a.red_blocks + x) * 32;
+      for (int e = 0; e < kRedWords; ++e) w[e] = w[e] + 1.0f * pp[e];
+    }
+    float AtA[36];
+    int e = 0;
+    for (int i = 0; i < 6; ++i)
+      for (int j = i; j < 6; ++j, ++e) { AtA[i + 6 * j] = w[e]; AtA[j + 6 * i] = w[e]; }
+    for (int i = 4; i < 6; ++i)
+      for (int j = 0; j < 4; ++j, ++e) AtA[i + 6 * j] = w[e];
+    conv = llsr_lm::lm_update_full(st, AtA, last, last[6], N, iterCount, a.applied != 0, a.stop_thres);
+  }
+  if (conv) st.converged = 1;
+  if (conv || st.iter >= a.iter_max) {
+    st.active = 0;
+    atomicSub(a.n_active, 1);
+  }
 }
 
 // ---- split-correspondence mode (llsr_scan2map_shard_*) ----------------------
@@ -389,6 +549,9 @@ __global__ void k_s2m_finish(S2MArgs a) {
     a.pose[6 * p + k] = st.pose[k];
   }
   r.ms = 0.0f;
+  if (a.deg_out) a.deg_out[p] = st.degenerate;
+  if (a.matP_out)
+    for (int k = 0; k < 36; ++k) a.matP_out[36 * p + k] = st.matP[k];
 }
 
 }  // namespace llsr

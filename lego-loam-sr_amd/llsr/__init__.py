@@ -41,6 +41,8 @@ EXPORTS = [
     "llsr_map_last_error", "llsr_map_reset", "llsr_map_voxel_grid", "llsr_map_downsample_scan",
     "llsr_map_add_keyframe", "llsr_map_num_keyframes", "llsr_map_extract", "llsr_map_keyframe_ids",
     "llsr_decode_pointcloud2", "llsr_kitti_count", "llsr_kitti_read", "llsr_kitti_load",
+    "llsr_mapping_init", "llsr_mapping_batch", "llsr_mapping_fetch", "llsr_mapping_keyposes", "llsr_mapping_reset",
+    "llsr_mapping_associate",
 ]
 
 
@@ -103,6 +105,12 @@ def lib():
         L.llsr_map_extract.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,
                                        C.POINTER(_abi.MapReport), C.c_void_p]
         L.llsr_map_keyframe_ids.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+        L.llsr_mapping_init.argtypes = [C.c_void_p, C.c_int32, C.POINTER(_abi.MapConfig)]
+        L.llsr_mapping_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
+        L.llsr_mapping_fetch.argtypes = [C.c_void_p, C.c_int32, C.POINTER(_abi.MappingSlot)]
+        L.llsr_mapping_keyposes.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]
+        L.llsr_mapping_reset.argtypes = [C.c_void_p]
+        L.llsr_mapping_associate.argtypes = [C.c_void_p] * 6
         L.llsr_decode_pointcloud2.argtypes = [C.POINTER(_abi.Pc2Layout), C.c_void_p, C.c_void_p, C.c_int32,
                                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.llsr_kitti_count.argtypes = [C.c_char_p]
@@ -312,6 +320,49 @@ class Pipeline:
 
     def odometry_reset(self):
         self._check(lib().llsr_odometry_reset(self._h), "llsr_odometry_reset")
+
+    # ---- mapping chain (FeatureAssociation -> MapOptimization::run) ----------------------------
+    def mapping_init(self, mo_mode: int = _abi.LLSR_MODE_LM_APPLIED, map_cfg: _abi.MapConfig | None = None):
+        """Per-slot MapOptimization state; mo_mode is MapOptimization's LM mode."""
+        self._check(lib().llsr_mapping_init(self._h, mo_mode, C.byref(map_cfg) if map_cfg is not None else None),
+                    "llsr_mapping_init")
+
+    def mapping_batch(self, d_xyzi: int, d_offsets: int, B: int, stream: int = 0):
+        """One device-resident scan per slot through IP + FA + odometry + MapOptimization."""
+        self._check(lib().llsr_mapping_batch(self._h, C.c_void_p(d_xyzi), C.c_void_p(d_offsets), B,
+                                             C.c_void_p(stream)), "llsr_mapping_batch")
+
+    def mapping_fetch(self, b: int) -> dict:
+        st = _abi.MappingSlot()
+        self._check(lib().llsr_mapping_fetch(self._h, b, C.byref(st)), "llsr_mapping_fetch")
+        d = {k: getattr(st, k) for k in ("frames", "mo_frames", "keyframes", "lm_ran", "n_corner_q", "n_surf_q")}
+        for k in ("transform_sum", "transform_tobe_mapped", "transform_bef_mapped", "transform_aft_mapped"):
+            d[k] = np.array(getattr(st, k)[:], np.float32)
+        d["lm"] = st.lm.as_dict()
+        d["map"] = st.map.as_dict()
+        return d
+
+    def mapping_keyposes(self, b: int) -> np.ndarray:
+        n = lib().llsr_mapping_keyposes(self._h, b, None, 0)
+        if n < 0:
+            self._check(n, "llsr_mapping_keyposes")
+        out = np.zeros((max(n, 1), 6), np.float32)
+        lib().llsr_mapping_keyposes(self._h, b, out.ctypes.data, n)
+        return out[:n].copy()
+
+    def mapping_reset(self):
+        self._check(lib().llsr_mapping_reset(self._h), "llsr_mapping_reset")
+
+
+def mapping_associate(transform_sum_fa, bef, aft):
+    """Host-only pose glue of the mapping chain (llsr_mapping_associate): OdometryToTransform then
+    transformAssociateToMap; returns (transform_sum, transform_tobe_mapped, transform_incre)."""
+    a = [np.ascontiguousarray(x, np.float32) for x in (transform_sum_fa, bef, aft)]
+    out = [np.zeros(6, np.float32) for _ in range(3)]
+    rc = lib().llsr_mapping_associate(*(x.ctypes.data for x in a), *(x.ctypes.data for x in out))
+    if rc != 0:
+        raise LlsrError(f"llsr_mapping_associate: {rc}")
+    return tuple(out)
 
 
 def shadow_points() -> np.ndarray:

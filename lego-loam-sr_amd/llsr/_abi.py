@@ -218,6 +218,14 @@ class MapReport(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class MappingSlot(C.Structure):
+    """llsr_mapping_slot (include/llsr.h): one sequence's MapOptimization state after the last call."""
+    _fields_ = [("frames", C.c_int32), ("mo_frames", C.c_int32), ("keyframes", C.c_int32), ("lm_ran", C.c_int32),
+                ("transform_sum", C.c_float * 6), ("transform_tobe_mapped", C.c_float * 6),
+                ("transform_bef_mapped", C.c_float * 6), ("transform_aft_mapped", C.c_float * 6),
+                ("n_corner_q", C.c_int32), ("n_surf_q", C.c_int32), ("lm", LmReport), ("map", MapReport)]
+
+
 PC2_FLOAT32 = 7
 PC2_MAX_FIELDS = 16
 KITTI_MAX_FLOATS = 1000000

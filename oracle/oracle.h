@@ -47,6 +47,17 @@ int32_t oracle_scan2scan(const llsr_config* cfg, const float* sharp, int32_t n_s
                          int32_t n_flat, const float* corner_last, int32_t n_corner_last,
                          const float* surf_last, int32_t n_surf_last, float* transform_cur,
                          int32_t* is_degenerate, llsr_s2s_report* rep);
+/* oracle_scan2map with the optimiser's members carried across calls (mapOptimization.h:279-281):
+ * degenerate / matP[36] (column-major) in/out, as one MapOptimization instance over a sequence. */
+int32_t oracle_scan2map_carry(const llsr_config* cfg, const float* corner_q, int32_t Qc, const float* surf_q,
+                              int32_t Qs, const float* corner_map, int32_t Mc, const float* surf_map, int32_t Ms,
+                              float* pose, int32_t* degenerate, float* matP, llsr_lm_report* rep);
+/* MapOptimization::run's pose glue (oracle_mapping.cpp): publishOdometry -> OdometryToTransform
+ * (FA:2612-2625, utility.h:99-113) and transformAssociateToMap (MO:458-581). */
+void oracle_odometry_to_transform(const float* transform_sum_fa, float* transform_sum_mo);
+void oracle_associate_to_map(const float* transform_sum, const float* transform_bef_mapped,
+                             const float* transform_aft_mapped, float* transform_tobe_mapped,
+                             float* transform_incre);
 /* Split-correspondence scan-to-map with int64 fixed-point normal equations: the CPU statement of
  * llsr_scan2map_shard_* for one problem (see oracle_mo.cpp). partial() writes LLSR_NE_WORDS words
  * for rank/world; step() takes the words summed over every rank and returns 1 while active. */

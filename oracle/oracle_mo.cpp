@@ -262,10 +262,13 @@ bool mo_converged(const float* X, float stop_thres) {
 
 }  // namespace
 
-extern "C" int32_t ORACLE_FN(scan2map)(const llsr_config* cfg, const float* cq, int32_t Qc, const float* sq,
-                                   int32_t Qs, const float* cm, int32_t Mc, const float* sm, int32_t Ms,
-                                   float* pose, llsr_lm_report* rep) {
-  if (!cfg || !pose || !rep || Qc < 0 || Qs < 0 || Mc < 0 || Ms < 0) return LLSR_EINVAL;
+// scan2MapOptimization with the optimiser's members carried in and out: isDegenerate / matP
+// (mapOptimization.h:279-281) keep their values across frames, and an iteration 0 with fewer than
+// 50 correspondences (MO:1453) leaves them untouched for the later iterations of the next frames.
+extern "C" int32_t ORACLE_FN(scan2map_carry)(const llsr_config* cfg, const float* cq, int32_t Qc, const float* sq,
+                                         int32_t Qs, const float* cm, int32_t Mc, const float* sm, int32_t Ms,
+                                         float* pose, int32_t* degenerate, float* matP, llsr_lm_report* rep) {
+  if (!cfg || !pose || !rep || !degenerate || !matP || Qc < 0 || Qs < 0 || Mc < 0 || Ms < 0) return LLSR_EINVAL;
   const P4* cornerQ = reinterpret_cast<const P4*>(cq);
   const P4* surfQ = reinterpret_cast<const P4*>(sq);
   const P4* cornerM = reinterpret_cast<const P4*>(cm);
@@ -283,6 +286,8 @@ extern "C" int32_t ORACLE_FN(scan2map)(const llsr_config* cfg, const float* cq, 
   gs.build(surfM, Ms);
   const bool applied = cfg->mode == LLSR_MODE_LM_APPLIED;
   MoLm lm;
+  lm.isDegenerate = *degenerate != 0;
+  std::memcpy(lm.matP, matP, sizeof lm.matP);
   float CF_mean = 0.0f;
   int iters = 0, converged = 0, nc = 0, ns = 0;
   std::vector<Coeff> sel;
@@ -337,7 +342,18 @@ extern "C" int32_t ORACLE_FN(scan2map)(const llsr_config* cfg, const float* cq, 
   rep->ms = (float)std::chrono::duration<double, std::milli>(t1 - t0).count();
   std::memcpy(rep->pose, t, sizeof t);
   std::memcpy(pose, t, sizeof t);
+  *degenerate = isDegenerate ? 1 : 0;
+  std::memcpy(matP, lm.matP, sizeof lm.matP);
   return LLSR_OK;
+}
+
+// One scan2MapOptimization call of a freshly constructed MapOptimization (members zeroed, MO:285-286).
+extern "C" int32_t ORACLE_FN(scan2map)(const llsr_config* cfg, const float* cq, int32_t Qc, const float* sq,
+                                   int32_t Qs, const float* cm, int32_t Mc, const float* sm, int32_t Ms,
+                                   float* pose, llsr_lm_report* rep) {
+  int32_t deg = 0;
+  float matP[36] = {0};
+  return ORACLE_FN(scan2map_carry)(cfg, cq, Qc, sq, Qs, cm, Mc, sm, Ms, pose, &deg, matP, rep);
 }
 
 // ---- split-correspondence scan-to-map, int64 fixed-point sums (llsr_scan2map_shard_*) -------

@@ -30,7 +30,7 @@ def lib():
     if _LIB is None:
         path = os.path.join(_HERE, "_build", "liboracle.so")
         srcs = [os.path.join(_HERE, f) for f in ("oracle_ipfa.cpp", "oracle_mo.cpp", "oracle_fa_lm.cpp",
-                                                        "oracle_map.cpp", "oracle_voxel.h")]
+                                                        "oracle_map.cpp", "oracle_mapping.cpp", "oracle_voxel.h")]
         if not os.path.exists(path) or os.path.getmtime(path) < max(map(os.path.getmtime, srcs)):
             build()
         L = C.CDLL(path)
@@ -75,6 +75,11 @@ def lib():
         L.oracle_map_extract.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p,
                                          C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p,
                                          C.c_void_p]
+        L.oracle_scan2map_carry.restype = C.c_int32
+        L.oracle_scan2map_carry.argtypes = [C.POINTER(_abi.Config)] + [C.c_void_p, C.c_int32] * 4 + \
+            [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(_abi.LmReport)]
+        L.oracle_odometry_to_transform.argtypes = [C.c_void_p, C.c_void_p]
+        L.oracle_associate_to_map.argtypes = [C.c_void_p] * 5
         _LIB = L
     return _LIB
 
@@ -498,3 +503,91 @@ def kitti_read(path: str) -> np.ndarray:
     buf = np.fromfile(path, dtype=np.float32, count=1000000)
     n = len(buf) // 4
     return buf[:4 * n].reshape(n, 4).copy()
+
+
+def odometry_to_transform(transform_sum_fa) -> np.ndarray:
+    """publishOdometry -> OdometryToTransform (FA:2612-2625, utility.h:99-113): the tf2 round trip."""
+    t = np.ascontiguousarray(transform_sum_fa, np.float32)
+    out = np.zeros(6, np.float32)
+    lib().oracle_odometry_to_transform(t.ctypes.data, out.ctypes.data)
+    return out
+
+
+class OracleMapping:
+    """MapOptimization::run (MO:1854-1896) fed by OracleOdometry, one sequence: the CPU statement of
+    llsr_mapping_batch. `stable` sums each VoxelGrid voxel in input order (the device's order);
+    False follows PCL's std::sort order (float rounding only, DESIGN.md)."""
+
+    def __init__(self, cfg: _abi.Config, mo_mode: int, radius=50.0, keypose_leaf=1.0, corner_leaf=0.2,
+                 surf_leaf=0.4, outlier_leaf=0.4, stable: bool = True):
+        import copy
+        self.odo = OracleOdometry(cfg)
+        self.cfg_mo = copy.copy(cfg)
+        self.cfg_mo.mode = mo_mode
+        self.map = OracleMap(radius, keypose_leaf, corner_leaf, surf_leaf, stable=stable)
+        self.leaf = (corner_leaf, surf_leaf, outlier_leaf)
+        self.stable = stable
+        z = lambda: np.zeros(6, np.float32)  # noqa: E731
+        self.transform_sum, self.bef, self.aft, self.tobe, self.incre, self.last = z(), z(), z(), z(), z(), z()
+        self.robot = np.zeros(3, np.float32)
+        self.deg = C.c_int32(0)
+        self.matP = np.zeros(36, np.float32)
+        self.keyposes = []
+        self.mo_frames = 0
+
+    def _vg(self, a, leaf):
+        return voxel_grid(a, leaf, self.stable) if len(a) else np.zeros((0, 4), np.float32)
+
+    def process(self, xyzi: np.ndarray) -> dict:
+        o = self.odo.process(xyzi)
+        out = {"odo": o, "step": False, "frames": o["frames"]}
+        if o["lm"] is None:  # checkSystemInitialization: no AssociationOut (FA:2781-2784)
+            return out
+        lc, ls, lo = self.leaf
+        # OdometryToTransform + transformAssociateToMap (MO:1878-1880)
+        self.transform_sum = odometry_to_transform(o["transform_sum"])
+        lib().oracle_associate_to_map(self.transform_sum.ctypes.data, self.bef.ctypes.data, self.aft.ctypes.data,
+                                      self.tobe.ctypes.data, self.incre.ctypes.data)
+        # extractSurroundingKeyFrames (MO:1096-1232)
+        cmap = smap = np.zeros((0, 4), np.float32)
+        mrep = None
+        if self.keyposes:
+            cmap, smap, _, mrep = self.map.extract(self.robot)
+        # downsampleCurrentScan (MO:1234-1267); outliers after adjustOutlierCloud (FA:2600-2610)
+        outlier = np.ascontiguousarray(o["features"]["outlier_xyzi"][:, [1, 2, 0, 3]])
+        cl_ds = self._vg(o["corner_last"], lc)
+        sl_ds = self._vg(o["surf_last"], ls)
+        cs_ds = self._vg(o["corner_scan"], lc)
+        ss_ds = self._vg(o["surf_scan"], ls)
+        ol_ds = self._vg(outlier, lo)
+        tot_ds = self._vg(np.concatenate([sl_ds, ol_ds]), ls)
+        # scan2MapOptimization (MO:1572-1610) with the members carried across frames
+        rep = _abi.LmReport()
+        pose = self.tobe.copy()
+        cq, sq, cm, sm = (_f4(a) for a in (cs_ds, tot_ds, cmap, smap))
+        rc = lib().oracle_scan2map_carry(C.byref(self.cfg_mo), cq.ctypes.data, len(cq), sq.ctypes.data, len(sq),
+                                         cm.ctypes.data, len(cm), sm.ctypes.data, len(sm), pose.ctypes.data,
+                                         C.byref(self.deg), self.matP.ctypes.data, C.byref(rep))
+        if rc != 0:
+            raise RuntimeError(f"oracle_scan2map_carry: {rc}")
+        lm_ran = len(cm) > 10 and len(sm) > 100
+        if lm_ran:  # transformUpdate (MO:583-589)
+            self.tobe = pose.copy()
+            self.bef = self.transform_sum.copy()
+            self.aft = self.tobe.copy()
+        # saveKeyFramesAndFactor (MO:1612-1755): iSAM2 returns its initial values
+        self.robot = self.aft[3:6].copy()
+        first = not self.keyposes
+        est = (self.tobe if first else self.aft).copy()
+        self.last = est.copy()
+        if not first:
+            self.tobe = self.aft.copy()
+        kp = np.array([est[3], est[4], est[5], est[0], est[1], est[2]], np.float32)
+        self.map.add_keyframe(kp, o["corner_scan"], sl_ds, ol_ds)
+        self.keyposes.append(kp)
+        self.mo_frames += 1
+        out.update(step=True, lm=rep.as_dict(), lm_ran=lm_ran, map=mrep, n_corner_q=len(cq), n_surf_q=len(sq),
+                   n_corner_map=len(cm), n_surf_map=len(sm), transform_sum=self.transform_sum.copy(),
+                   transform_tobe_mapped=self.tobe.copy(), transform_bef_mapped=self.bef.copy(),
+                   transform_aft_mapped=self.aft.copy(), keyframes=len(self.keyposes))
+        return out

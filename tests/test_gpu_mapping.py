@@ -1,0 +1,115 @@
+"""GPU parity of the mapping chain (llsr_mapping_*: IP -> FA -> odometry -> MapOptimization::run,
+MO:1854-1896) against the oracle's sequence restatement (oracle_py.OracleMapping).
+
+B independent VLP-16 drives advance one scan per call; after every call each slot's MapOptimization
+state is compared with the oracle's: frame / keyframe counts, whether scan-to-map ran (MO:1573),
+the query and local-map sizes, the LM report, transformSum / TobeMapped / BefMapped / AftMapped,
+and at the end the key poses (cloudKeyPoses6D).
+
+Bar: counts equal; poses within 1e-4. The chain is not bit-exact end to end for one documented
+reason: PCL's VoxelGrid sums a voxel's points in std::sort's tie order, the device in input order
+(the oracle's VoxelGrids run in the device order here, stable=True, but the
+odometry's per-ring less-flat VoxelGrid in the oracle follows PCL), so the LM inputs may differ in
+the last bits of a centroid.
+"""
+import numpy as np
+import pytest
+
+import oracle_py
+from llsr import Pipeline, _abi, default_config, synth
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+POSES = ("transform_sum", "transform_tobe_mapped", "transform_bef_mapped", "transform_aft_mapped")
+
+
+def _drive(mode, seeds, frames, iters=None):
+    import torch
+    cfg = default_config("vlp16")
+    cfg.mode = _abi.LLSR_MODE_LM_APPLIED
+    if iters is not None:
+        cfg.iterCountThres = iters
+    H, W = cfg.num_vertical_scans, cfg.num_horizontal_scans
+    pipe = Pipeline(cfg, max_batch=len(seeds), max_points=H * W)
+    pipe.mapping_init(mode)
+    oras = [oracle_py.OracleMapping(cfg, mode) for _ in seeds]
+    errs = []
+    for k in range(frames):
+        scans = [synth.make_scan(s0 + k, "vlp16") for s0 in seeds]
+        off = np.zeros(len(scans) + 1, np.int64)
+        off[1:] = np.cumsum([len(s) for s in scans])
+        d_pts = torch.from_numpy(np.concatenate(scans)).cuda()
+        d_off = torch.from_numpy(off).cuda()
+        torch.cuda.synchronize()
+        pipe.mapping_batch(d_pts.data_ptr(), d_off.data_ptr(), len(scans))
+        for b, ora in enumerate(oras):
+            o = ora.process(scans[b])
+            g = pipe.mapping_fetch(b)
+            tag = f"mode {mode} slot {b} frame {k}"
+            if g["frames"] != o["frames"]:
+                errs.append(f"{tag}: frames {g['frames']} vs {o['frames']}")
+            if not o["step"]:
+                if g["mo_frames"] != 0 or g["keyframes"] != 0:
+                    errs.append(f"{tag}: first scan stepped MapOptimization")
+                continue
+            for key in ("keyframes", "n_corner_q", "n_surf_q"):
+                if g[key] != o[key]:
+                    errs.append(f"{tag}: {key} {g[key]} vs {o[key]}")
+            if bool(g["lm_ran"]) != bool(o["lm_ran"]):
+                errs.append(f"{tag}: lm_ran {g['lm_ran']} vs {o['lm_ran']}")
+            if o["map"] is not None:
+                for key, ok in (("n_corner_ds", "n_corner_map"), ("n_surf_ds", "n_surf_map")):
+                    if g["map"][key] != o[ok]:
+                        errs.append(f"{tag}: map {key} {g['map'][key]} vs {o[ok]}")
+            if o["lm_ran"]:
+                for key in ("iterations", "converged", "degenerate", "n_corner_corr", "n_surf_corr"):
+                    if g["lm"][key] != o["lm"][key]:
+                        errs.append(f"{tag}: lm {key} {g['lm'][key]} vs {o['lm'][key]}")
+            for key in POSES:
+                d = np.abs(g[key] - o[key]).max()
+                if d > TOL:
+                    errs.append(f"{tag}: {key} {g[key]} vs {o[key]} (max |d| {d:.3g})")
+    for b, ora in enumerate(oras):
+        kg = pipe.mapping_keyposes(b)
+        ko = np.array(ora.keyposes, np.float32).reshape(-1, 6)
+        if kg.shape != ko.shape:
+            errs.append(f"slot {b}: keyposes {kg.shape} vs {ko.shape}")
+        elif kg.size and np.abs(kg - ko).max() > TOL:
+            errs.append(f"slot {b}: keyposes max |d| {np.abs(kg - ko).max():.3g}")
+    pipe.close()
+    return errs
+
+
+def test_mapping_chain_lm_applied(require_gpu):
+    errs = _drive(_abi.LLSR_MODE_LM_APPLIED, [1, 65, 130], 6)
+    assert not errs, "\n".join(errs)
+
+
+def test_mapping_chain_faithful(require_gpu):
+    errs = _drive(_abi.LLSR_MODE_FAITHFUL, [3, 200], 5, iters=50)
+    assert not errs, "\n".join(errs)
+
+
+def test_mapping_reset_repeats(require_gpu):
+    """llsr_mapping_reset starts every slot over: a second pass over the same scans repeats the first."""
+    import torch
+    cfg = default_config("vlp16")
+    cfg.mode = _abi.LLSR_MODE_LM_APPLIED
+    pipe = Pipeline(cfg, max_batch=1, max_points=28800)
+    pipe.mapping_init(_abi.LLSR_MODE_LM_APPLIED)
+    runs = []
+    for _ in range(2):
+        pipe.mapping_reset()
+        for k in range(4):
+            pts = synth.make_scan(9 + k, "vlp16")
+            d_pts = torch.from_numpy(pts).cuda()
+            d_off = torch.tensor([0, len(pts)], dtype=torch.int64).cuda()
+            torch.cuda.synchronize()
+            pipe.mapping_batch(d_pts.data_ptr(), d_off.data_ptr(), 1)
+        runs.append((pipe.mapping_fetch(0), pipe.mapping_keyposes(0)))
+    (a, ka), (b, kb) = runs
+    assert a["keyframes"] == b["keyframes"] == 3
+    assert np.array_equal(ka, kb)
+    for key in POSES:
+        assert np.array_equal(a[key], b[key]), key
+    pipe.close()

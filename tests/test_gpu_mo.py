@@ -3,13 +3,11 @@
 HIP path through the C-ABI (llsr_scan2map / llsr_scan2map_batch) against the oracle
 (oracle/oracle_mo.cpp) on the committed ~76k-point map fixture (tests/golden/make_mo_fixture.py).
 
-The bar:
-  * correspondences are bit-exact — checked where the pose is identical on both sides:
-    faithful mode (the reference's commented-out update, MO:1539-1545) evaluates every
-    iteration at the input pose, so the corner / surf correspondence counts must be equal;
-  * the normal equations are summed in a different order (block tree vs the reference's Eigen
-    GEMM / the oracle's sequential sum), so matX / min_lambda / cf_mean are compared with a
-    relative tolerance of 1e-4 and the final pose with north_star's 1e-4 absolute.
+The bar is bit-exactness: the correspondences and Jacobian rows repeat the reference's float /
+double operations one for one, and the normal equations are summed in the order of the
+reference's Eigen 3.3.7 build (matAt * matA per GEMM depth block, rows 4-5 x columns 0-3 through
+gebp's four-accumulator path, matAt * matB and CF_all left to right; k_s2m_reduce), so the final
+pose, iteration count, matX0, min_lambda, cf_mean and correspondence counts equal the oracle's.
 """
 import os
 
@@ -22,7 +20,6 @@ from llsr import Pipeline, _abi, default_config
 pytestmark = pytest.mark.gpu
 
 FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mo_map_vlp16.npz")
-POSE_TOL = 1e-4
 
 
 @pytest.fixture(scope="module")
@@ -40,11 +37,6 @@ def _inputs(fix, i):
     return fix[f"q{i}_corner"], fix[f"q{i}_surf"], fix["corner_map"], fix["surf_map"], fix[f"q{i}_init"]
 
 
-def _close(a, b, rel=1e-4, atol=1e-6):
-    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
-    return np.all(np.abs(a - b) <= atol + rel * np.abs(b))
-
-
 @pytest.mark.parametrize("mode", [_abi.LLSR_MODE_LM_APPLIED, _abi.LLSR_MODE_FAITHFUL])
 def test_scan2map_matches_oracle(require_gpu, fix, mode):
     cfg = _cfg(mode)
@@ -56,27 +48,12 @@ def test_scan2map_matches_oracle(require_gpu, fix, mode):
         g = pipe.scan2map(*args)
         o = oracle_py.scan2map(cfg, *args)
         tag = f"query {i} mode {mode}"
-        if np.abs(g["pose"] - o["pose"]).max() > POSE_TOL:
-            errs.append(f"{tag}: pose {g['pose']} vs {o['pose']}")
-        for k in ("converged", "degenerate"):
-            if g[k] != o[k]:
+        for k in ("pose", "matX0", "min_lambda", "cf_mean", "iterations", "converged", "degenerate",
+                  "n_corner_corr", "n_surf_corr"):
+            if not np.array_equal(np.asarray(g[k]), np.asarray(o[k])):
                 errs.append(f"{tag}: {k} {g[k]} vs {o[k]}")
-        if abs(g["iterations"] - o["iterations"]) > (0 if mode == _abi.LLSR_MODE_FAITHFUL else 1):
-            errs.append(f"{tag}: iterations {g['iterations']} vs {o['iterations']}")
-        if not _close(g["matX0"], o["matX0"], atol=1e-6):
-            errs.append(f"{tag}: matX0 {g['matX0']} vs {o['matX0']}")
-        if not _close(g["min_lambda"], o["min_lambda"]):
-            errs.append(f"{tag}: min_lambda {g['min_lambda']} vs {o['min_lambda']}")
-        if not _close(g["cf_mean"], o["cf_mean"]):
-            errs.append(f"{tag}: cf_mean {g['cf_mean']} vs {o['cf_mean']}")
         if mode == _abi.LLSR_MODE_FAITHFUL:
             np.testing.assert_array_equal(g["pose"], args[4])
-            if (g["n_corner_corr"], g["n_surf_corr"]) != (o["n_corner_corr"], o["n_surf_corr"]):
-                errs.append(f"{tag}: correspondences {g['n_corner_corr']}/{g['n_surf_corr']} vs "
-                            f"{o['n_corner_corr']}/{o['n_surf_corr']}")
-        elif abs(g["n_corner_corr"] - o["n_corner_corr"]) + abs(g["n_surf_corr"] - o["n_surf_corr"]) > 2:
-            errs.append(f"{tag}: correspondences {g['n_corner_corr']}/{g['n_surf_corr']} vs "
-                        f"{o['n_corner_corr']}/{o['n_surf_corr']}")
     pipe.close()
     assert not errs, "\n".join(errs)
 
@@ -118,9 +95,10 @@ def test_scan2map_batch_matches_single(require_gpu, fix):
     pipe.close()
     for p, pr in enumerate(probs):
         o = oracle_py.scan2map(cfg, *pr)
-        assert np.abs(poses[p] - o["pose"]).max() <= POSE_TOL, (p, poses[p], o["pose"])
+        np.testing.assert_array_equal(poses[p], o["pose"])
         np.testing.assert_array_equal(reps[p].pose[:], poses[p])
-        assert abs(reps[p].iterations - o["iterations"]) <= 1 and reps[p].converged == o["converged"], p
+        assert reps[p].iterations == o["iterations"] and reps[p].converged == o["converged"], p
+        assert (reps[p].n_corner_corr, reps[p].n_surf_corr) == (o["n_corner_corr"], o["n_surf_corr"]), p
 
 
 def C_sizeof_report():
@@ -150,7 +128,7 @@ def test_scan2map_guard_and_empty(require_gpu, fix):
     # corners only
     g = pipe.scan2map(cq, sq[:0], cm, sm, pose)
     o = oracle_py.scan2map(cfg, cq, sq[:0], cm, sm, pose)
-    assert np.abs(g["pose"] - o["pose"]).max() <= POSE_TOL and g["iterations"] == o["iterations"]
+    assert np.array_equal(g["pose"], o["pose"]) and g["iterations"] == o["iterations"]
     pipe.close()
 
 
@@ -178,27 +156,19 @@ def test_scan2map_capacity_error(require_gpu, fix):
 @pytest.mark.parametrize("mode", [_abi.LLSR_MODE_LM_APPLIED, _abi.LLSR_MODE_FAITHFUL])
 def test_scan2map_degenerate(require_gpu, mode):
     """The degenerate branch (MO:1507-1537: every eigenvalue of the 6x6 AtA below 100, matP =
-    matV.inverse() * matV2 through PartialPivLU) on shrunk scenes (tests/_scenes.py): same flag,
-    iteration count and (frozen) pose as the oracle. (The shrunk scenes' regular problems are
-    ill-conditioned — smallest eigenvalue just above the threshold — so two float summation orders
-    of AtA land up to ~1e-3 apart there; they are compared bit for bit in split mode instead,
-    test_gpu_shard.py::test_shard_degenerate_bit_exact_vs_oracle.)"""
+    matV.inverse() * matV2 through PartialPivLU) and the shrunk scenes' regular, ill-conditioned
+    problems (tests/_scenes.py, smallest eigenvalue just above the threshold): bit-exact, like
+    every other problem, now that AtA is summed in Eigen's order."""
     import _scenes
     cfg = _cfg(mode)
     pipe = Pipeline(cfg)
     errs = []
-    for k, pr in enumerate(_scenes.mo_degenerate_problems()):
+    for k, pr in enumerate(_scenes.mo_degenerate_problems(regular=True)):
         g = pipe.scan2map(*pr)
         o = oracle_py.scan2map(cfg, *pr)
-        for key in ("degenerate", "converged") + (("n_corner_corr", "n_surf_corr") if o["degenerate"] else ()):
-            if g[key] != o[key]:
+        for key in ("pose", "degenerate", "converged", "iterations", "n_corner_corr", "n_surf_corr", "min_lambda"):
+            if not np.array_equal(np.asarray(g[key]), np.asarray(o[key])):
                 errs.append(f"problem {k}: {key} {g[key]} vs {o[key]}")
-        # the regular shrunk problems converge slowly (ill-conditioned), so where the float sums'
-        # order differs (block tree vs Eigen's GEMM) the stop iteration may move; the pose may not
-        if o["degenerate"] and g["iterations"] != o["iterations"]:
-            errs.append(f"problem {k}: iterations {g['iterations']} vs {o['iterations']}")
-        if np.abs(g["pose"] - o["pose"]).max() > POSE_TOL:
-            errs.append(f"problem {k}: pose {g['pose']} vs {o['pose']}")
         if o["degenerate"] and not np.array_equal(g["pose"], pr[4]):
             errs.append(f"problem {k}: a degenerate problem moved the pose")
     pipe.close()
