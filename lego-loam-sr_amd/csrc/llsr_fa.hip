@@ -256,17 +256,25 @@ __device__ __forceinline__ int pow2_ceil(int n) {
 __device__ __forceinline__ bool key_lt(uint64_t a, uint64_t b) {
   return __uint_as_float((uint32_t)(a >> 32)) < __uint_as_float((uint32_t)(b >> 32));
 }
+// the comparators: cloudSmoothness by value (FA:1172), PCL's cloud_point_index_idx by voxel id
+struct CurvLess {
+  __device__ bool operator()(uint64_t a, uint64_t b) const { return key_lt(a, b); }
+};
+struct VoxLess {
+  __device__ bool operator()(uint64_t a, uint64_t b) const { return (uint32_t)(a >> 32) < (uint32_t)(b >> 32); }
+};
 __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
 // libstdc++ __adjust_heap (with __push_heap) on key[f, f+len), one lane
-__device__ void heap_adjust(uint64_t* key, int f, int hole, int len, uint64_t val) {
+template <class Lt>
+__device__ void heap_adjust(uint64_t* key, int f, int hole, int len, uint64_t val, Lt lt) {
   const int top = hole;
   int second = hole;
   while (second < (len - 1) / 2) {
     second = 2 * (second + 1);
-    if (key_lt(key[f + second], key[f + second - 1])) second--;
+    if (lt(key[f + second], key[f + second - 1])) second--;
     key[f + hole] = key[f + second];
     hole = second;
   }
@@ -276,7 +284,7 @@ __device__ void heap_adjust(uint64_t* key, int f, int hole, int len, uint64_t va
     hole = second - 1;
   }
   int parent = (hole - 1) / 2;
-  while (hole > top && key_lt(key[f + parent], val)) {
+  while (hole > top && lt(key[f + parent], val)) {
     key[f + hole] = key[f + parent];
     hole = parent;
     parent = (hole - 1) / 2;
@@ -284,24 +292,26 @@ __device__ void heap_adjust(uint64_t* key, int f, int hole, int len, uint64_t va
   key[f + hole] = val;
 }
 // __partial_sort(first, last, last) = __make_heap + __sort_heap, one lane
-__device__ void heap_sort_range(uint64_t* key, int f, int l) {
+template <class Lt>
+__device__ void heap_sort_range(uint64_t* key, int f, int l, Lt lt) {
   const int len = l - f;
   if (len >= 2)
     for (int parent = (len - 2) / 2;; --parent) {
-      heap_adjust(key, f, parent, len, key[f + parent]);
+      heap_adjust(key, f, parent, len, key[f + parent], lt);
       if (parent == 0) break;
     }
   for (int last = l; last - f > 1;) {
     --last;
     const uint64_t val = key[last];
     key[last] = key[f];
-    heap_adjust(key, f, 0, last - f, val);
+    heap_adjust(key, f, 0, last - f, val, lt);
   }
 }
 constexpr int kSortStack = 64;
 // Executed by one full wave (64 lanes). Lp / Rp: n uint16 each; stk: 3 * kSortStack ints;
 // leaf: (n + 64) / 64 uint64 words. Returns nothing; key[0, n) ends up as std::sort leaves it.
-__device__ void exact_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp, int* stk, uint64_t* leaf) {
+template <class Lt>
+__device__ void exact_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp, int* stk, uint64_t* leaf, Lt lt) {
   const int l = lane_id();
   const unsigned long long ltm = (1ull << l) - 1ull;
   for (int w = l; w <= (n >> 6); w += 64) leaf[w] = 0ull;
@@ -313,7 +323,7 @@ __device__ void exact_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp
   while (true) {
     while (rl - rf > 16) {
       if (rd == 0) {
-        if (l == 0) heap_sort_range(key, rf, rl);
+        if (l == 0) heap_sort_range(key, rf, rl, lt);
         wave_sync_lds();
         break;
       }
@@ -322,8 +332,8 @@ __device__ void exact_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp
       if (l == 0) {  // __move_median_to_first(first, first+1, mid, last-1)
         const int a = rf + 1, b = mid, c = rl - 1;
         int m;
-        if (key_lt(key[a], key[b])) m = key_lt(key[b], key[c]) ? b : (key_lt(key[a], key[c]) ? c : a);
-        else m = key_lt(key[a], key[c]) ? a : (key_lt(key[b], key[c]) ? c : b);
+        if (lt(key[a], key[b])) m = lt(key[b], key[c]) ? b : (lt(key[a], key[c]) ? c : a);
+        else m = lt(key[a], key[c]) ? a : (lt(key[b], key[c]) ? c : b);
         const uint64_t t = key[rf]; key[rf] = key[m]; key[m] = t;
       }
       wave_sync_lds();
@@ -331,14 +341,14 @@ __device__ void exact_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp
       int nL = 0, nR = 0;
       for (int c0 = rf + 1; c0 < rl; c0 += 64) {
         const int i = c0 + l;
-        const bool f = i < rl && !key_lt(key[i], P);
+        const bool f = i < rl && !lt(key[i], P);
         const unsigned long long m = __ballot(f);
         if (f) Lp[nL + __popcll(m & ltm)] = (uint16_t)i;
         nL += __popcll(m);
       }
       for (int c0 = rl - 1; c0 >= rf; c0 -= 64) {
         const int j = c0 - l;
-        const bool f = j >= rf && !key_lt(P, key[j]);
+        const bool f = j >= rf && !lt(P, key[j]);
         const unsigned long long m = __ballot(f);
         if (f) Rp[nR + __popcll(m & ltm)] = (uint16_t)j;
         nR += __popcll(m);
@@ -386,7 +396,7 @@ __device__ void exact_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp
       for (int i = s0 + 1; i < e; ++i) {
         const uint64_t val = key[i];
         int j = i;
-        while (j > s0 && key_lt(val, key[j - 1])) { key[j] = key[j - 1]; --j; }
+        while (j > s0 && lt(val, key[j - 1])) { key[j] = key[j - 1]; --j; }
         key[j] = val;
       }
     }
@@ -403,7 +413,7 @@ __global__ __launch_bounds__(64) void k_debug_exact_sort(const float* vals, int 
   __shared__ uint64_t leafw[kRingMax / 64 + 1];
   for (int t = threadIdx.x; t < n; t += 64) key[t] = ((uint64_t)__float_as_uint(vals[t]) << 32) | (uint32_t)t;
   wave_sync_lds();
-  exact_introsort(key, n, Lp, Rp, stk, leafw);
+  exact_introsort(key, n, Lp, Rp, stk, leafw, CurvLess{});
   for (int t = threadIdx.x; t < n; t += 64) out[t] = (int)(uint32_t)key[t];
 }
 
@@ -578,7 +588,7 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
       key[t] = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)ind;
     }
     __syncthreads();
-    if (tid < 64) exact_introsort(key, nRng, cpos, rstart, stk, leafw);
+    if (tid < 64) exact_introsort(key, nRng, cpos, rstart, stk, leafw, CurvLess{});
     __syncthreads();
     if (tid == 0) {
       if (sp == 4) d.phantom[b] = (int)(uint32_t)key[0];
@@ -770,59 +780,37 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
     vk[t] = (uint32_t)(i0 + i1 * mul1 + i2 * mul2);
   }
   __syncthreads();
-  // runs of equal voxel id in ring order -> one sort key per run: (voxel id, run index). Position
-  // t = u * 256 + tid in slot u of a lane; run indices from per-(slot, wave) ballot counts scanned in
-  // (slot, wave) = ring order.
+  // std::sort(index_vector) by voxel id alone (PCL 1.10 voxel_grid.hpp): equal ids keep the order
+  // libstdc++'s introsort leaves them in, and each centroid sums its points in that order.
+  for (int t = tid; t < L; t += nt) key[t] = ((uint64_t)vk[t] << 32) | (uint32_t)t;
+  __syncthreads();
+  if (c.dbg_phase <= 5) return;
+  // Lp = rstart, Rp = the (dead) voxel-id words
+  if (tid < 64) exact_introsort(key, L, rstart, reinterpret_cast<uint16_t*>(win_raw), stk, leafw, VoxLess{});
+  __syncthreads();
+  if (c.dbg_phase <= 6) return;
+  // voxel heads in sorted order; sorted position t = u * 256 + tid sits in slot u of a lane, so a
+  // wave's heads of one slot are consecutive voxels and their centroids are stored contiguously;
+  // output positions come from per-(slot, wave) ballot counts scanned in (slot, wave) = sorted order.
   __shared__ int scnt[kLp * 4 + 1];
   const int wv = tid >> 6, ln = lane_id();
   const unsigned long long ltm = (1ull << ln) - 1ull;
-  auto slot_scan = [&]() {  // exclusive scan of scnt[0 .. kLp*4) in place, total in scnt[kLp*4]
-    __syncthreads();
-    if (wv == 0) {
-      const int v = ln < kLp * 4 ? scnt[ln] : 0;
-      const int incl = wave_incl_scan_add(v);
-      if (ln < kLp * 4) scnt[ln] = incl - v;
-      if (ln == 63) scnt[kLp * 4] = incl;
-    }
-    __syncthreads();
-  };
-  unsigned long long mR[kLp];
-#pragma unroll
-  for (int u = 0; u < kLp; ++u) {
-    const int t = u * 256 + tid;
-    mR[u] = __ballot(t < L && (t == 0 || vk[t] != vk[t - 1]));
-    if (ln == 0) scnt[u * 4 + wv] = (int)__popcll(mR[u]);
-  }
-  slot_scan();
-  const int R = scnt[kLp * 4];
-#pragma unroll
-  for (int u = 0; u < kLp; ++u) {
-    if (!((mR[u] >> ln) & 1ull)) continue;
-    const int t = u * 256 + tid;
-    const int ro = scnt[u * 4 + wv] + (int)__popcll(mR[u] & ltm);
-    rstart[ro] = (uint16_t)t;
-    key[ro] = ((uint64_t)vk[t] << 32) | (uint32_t)ro;
-  }
-  if (tid == 0) rstart[R] = (uint16_t)L;
-  const int R2 = pow2_ceil(R);
-  for (int t = R + tid; t < R2; t += nt) key[t] = ~0ull;
-  __syncthreads();
-  if (c.dbg_phase <= 5) return;
-  bitonic_sort_u64(key, R2);
-  if (c.dbg_phase <= 6) return;
-  // voxels = groups of sorted runs with equal id; sum members in (run start, position) order.
-  // Sorted run t = u * 256 + tid sits in slot u of a lane, so a wave's voxel heads of one slot are
-  // consecutive voxels and their centroids are stored contiguously; output positions come from
-  // per-(slot, wave) ballot counts scanned in (slot, wave) = sorted order.
   unsigned long long mH[kLp];
 #pragma unroll
   for (int u = 0; u < kLp; ++u) {
     const int t = u * 256 + tid;
-    const bool head = t < R && (t == 0 || (key[t] >> 32) != (key[t - 1] >> 32));
+    const bool head = t < L && (t == 0 || (key[t] >> 32) != (key[t - 1] >> 32));
     mH[u] = __ballot(head);
     if (ln == 0) scnt[u * 4 + wv] = (int)__popcll(mH[u]);
   }
-  slot_scan();
+  __syncthreads();
+  if (wv == 0) {  // exclusive scan of scnt[0 .. kLp*4) in place, total in scnt[kLp*4]
+    const int v = ln < kLp * 4 ? scnt[ln] : 0;
+    const int incl = wave_incl_scan_add(v);
+    if (ln < kLp * 4) scnt[ln] = incl - v;
+    if (ln == 63) scnt[kLp * 4] = incl;
+  }
+  __syncthreads();
   const int V = scnt[kLp * 4];
 #pragma unroll
   for (int u = 0; u < kLp; ++u) {
@@ -830,16 +818,12 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
     if (!((mH[u] >> ln) & 1ull)) continue;
     const uint32_t vid = (uint32_t)(key[t] >> 32);
     float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
-    int cntp = 0;
-    for (int e = t; e < R && (uint32_t)(key[e] >> 32) == vid; ++e) {
-      const int run = (int)(uint32_t)key[e];
-      for (int q = rstart[run]; q < rstart[run + 1]; ++q) {
-        const float4 p = lp[cpos[q]];
-        sx += p.x; sy += p.y; sz += p.z; si += p.w;
-        ++cntp;
-      }
+    int e = t;
+    for (; e < L && (uint32_t)(key[e] >> 32) == vid; ++e) {
+      const float4 p = lp[cpos[(uint32_t)key[e]]];
+      sx += p.x; sy += p.y; sz += p.z; si += p.w;
     }
-    const float nn = (float)cntp;
+    const float nn = (float)(e - t);
     const int vo = scnt[u * 4 + wv] + (int)__popcll(mH[u] & ltm);
     out[vo] = make_float4(sx / nn, sy / nn, sz / nn, si / nn);
   }

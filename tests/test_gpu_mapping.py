@@ -66,15 +66,14 @@ def _drive(mode, seeds, frames, iters=None):
                     if g["lm"][key] != o["lm"][key]:
                         errs.append(f"{tag}: lm {key} {g['lm'][key]} vs {o['lm'][key]}")
             for key in POSES:
-                d = np.abs(g[key] - o[key]).max()
-                if d > TOL:
-                    errs.append(f"{tag}: {key} {g[key]} vs {o[key]} (max |d| {d:.3g})")
+                if not np.array_equal(g[key], o[key]):
+                    errs.append(f"{tag}: {key} {g[key]} vs {o[key]} (max |d| {np.abs(g[key] - o[key]).max():.3g})")
     for b, ora in enumerate(oras):
         kg = pipe.mapping_keyposes(b)
         ko = np.array(ora.keyposes, np.float32).reshape(-1, 6)
         if kg.shape != ko.shape:
             errs.append(f"slot {b}: keyposes {kg.shape} vs {ko.shape}")
-        elif kg.size and np.abs(kg - ko).max() > TOL:
+        elif not np.array_equal(kg, ko):
             errs.append(f"slot {b}: keyposes max |d| {np.abs(kg - ko).max():.3g}")
     pipe.close()
     return errs

@@ -4,10 +4,9 @@ B independent sequences advance one scan per call through IP + features + scan-t
 integrateTransformation + publishCloudsLast on the device; each slot is compared after every
 scan with the oracle's sequence restatement (oracle_py.OracleOdometry).
 
-Bar: frame counts, LM skip flag and cloud sizes equal; transformCur / transformSum and the last /
-scan clouds within 1e-4 (the surf-last cloud carries the VoxelGrid centroids, which may differ in
-the last bits because PCL sums a voxel in std::sort's tie order — tests/_compare.py — so the LM
-inputs are not always bit-identical; every other input is).
+Bar: bit-exact — frame counts, LM skip flag, transformCur / transformSum and the last / scan
+clouds equal the oracle's (the features are bit-exact, tests/_compare.py, and the scan-to-scan LM
+sums its normal equations in Eigen's order, llsr_fa_lm.hip).
 """
 import numpy as np
 import pytest
@@ -16,7 +15,6 @@ import oracle_py
 from llsr import Pipeline, _abi, default_config, synth
 
 pytestmark = pytest.mark.gpu
-TOL = 1e-4
 
 
 def _sequence(lidar, horizontal, slots, frames):
@@ -44,13 +42,13 @@ def _sequence(lidar, horizontal, slots, frames):
             if (g["lm"]["skipped"] == 1) != (o["lm"] is None):
                 errs.append(f"{tag}: skipped {g['lm']['skipped']} vs oracle lm {o['lm'] is not None}")
             for key in ("transform_cur", "transform_sum"):
-                if np.abs(g[key] - o[key]).max() > TOL:
-                    errs.append(f"{tag}: {key} {g[key]} vs {o[key]}")
+                if not np.array_equal(g[key], o[key]):
+                    errs.append(f"{tag}: {key} {g[key]} vs {o[key]} (max |d| {np.abs(g[key] - o[key]).max():.3g})")
             for key in ("corner_last", "surf_last", "corner_scan", "surf_scan"):
                 ref = o[key] if o[key] is not None else np.zeros((0, 4), np.float32)
                 if g[key].shape != ref.shape:
                     errs.append(f"{tag}: {key} shape {g[key].shape} vs {ref.shape}")
-                elif g[key].size and np.abs(g[key] - ref).max() > TOL * max(1.0, np.abs(ref).max()):
+                elif not np.array_equal(g[key], ref):
                     errs.append(f"{tag}: {key} max |d| {np.abs(g[key] - ref).max():.3g}")
     pipe.close()
     return errs
