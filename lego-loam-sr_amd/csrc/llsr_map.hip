@@ -32,11 +32,13 @@
 #include <vector>
 
 #include "../../include/llsr.h"
+#include "llsr_isort.h"
 #include "llsr_libm.h"
 #include "llsr_mapping.h"
 
 namespace {
 
+using namespace llsr;
 using llsr_libm::cosf_;
 using llsr_libm::sinf_;
 
@@ -128,8 +130,9 @@ __global__ void k_vg_params(const VgSeg* segs, const unsigned* mm, VgPar* par, i
   par[s] = q;
 }
 
+// PCL's index_vector entry of each point: (voxel id << 32 | point index), in input order.
 __global__ __launch_bounds__(256) void k_vg_keys(const Chunk* ch, const VgSeg* segs, const VgPar* par,
-                                                 const long long* base, unsigned long long* key, int* val) {
+                                                 const long long* base, unsigned long long* kk) {
   const Chunk c = ch[blockIdx.x];
   const float4* p = segs[c.seg].src;
   const float inv = segs[c.seg].inv;
@@ -146,8 +149,156 @@ __global__ __launch_bounds__(256) void k_vg_keys(const Chunk* ch, const VgSeg* s
       const int i2 = (int)(floorf(v.z * inv) - (float)q.minb[2]);
       idx = (unsigned)i0 + (unsigned)i1 * q.mul1 + (unsigned)i2 * q.mul2;
     }
-    key[o + i] = ((unsigned long long)c.seg << 32) | idx;
-    val[o + i] = (int)i;
+    kk[o + i] = ((unsigned long long)idx << 32) | (unsigned)i;
+  }
+}
+
+// ---- std::sort(index_vector) by voxel id, exactly as libstdc++ leaves equal ids ----------------
+// Every segment is sorted on its own (llsr_isort.h): ranges above kIsLeaf are partitioned in
+// global memory, one 1024-thread workgroup per range and level (k_is_level: the same parallel
+// statement of __unguarded_partition as the wave version, with the stop lists in Lb / Rb); ranges
+// of at most kIsLeaf elements finish in LDS, one wave each, with the depth limit they inherited
+// (k_is_leaf). A range whose depth limit runs out above kIsLeaf is heap-sorted by one lane (the
+// median-of-3 killer case; never met by point clouds).
+struct IsRange {
+  long long f, l;  // [f, l) in the packed key array
+  int d, pad;      // remaining depth limit
+};
+constexpr int kIsLeaf = 2048;
+constexpr int kIsT = 1024;       // threads of k_is_level
+constexpr int kIsE = 4;          // elements per lane per tile
+
+__device__ void is_push(IsRange r, IsRange* nxt, int* n_nxt, IsRange* leaves, int* n_leaves) {
+  const long long n = r.l - r.f;
+  if (n <= 1) return;
+  if (n > kIsLeaf) nxt[atomicAdd(n_nxt, 1)] = r;
+  else leaves[atomicAdd(n_leaves, 1)] = r;
+}
+
+__global__ __launch_bounds__(kIsT) void k_is_level(unsigned long long* kk, const IsRange* in, int n_in, IsRange* nxt,
+                                                   int* n_nxt, IsRange* leaves, int* n_leaves, int* Lb, int* Rb) {
+  if ((int)blockIdx.x >= n_in) return;
+  const IsRange r = in[blockIdx.x];
+  unsigned long long* a = kk + r.f;
+  int* Lp = Lb + r.f;
+  int* Rp = Rb + r.f;
+  const int n = (int)(r.l - r.f);
+  const int t = threadIdx.x, w = t >> 6, ln = t & 63;
+  const unsigned long long ltm = (1ull << ln) - 1ull;
+  const VoxLess lt;
+  if (r.d == 0) {  // __partial_sort(first, last, last)
+    if (t == 0) heap_sort_range(reinterpret_cast<uint64_t*>(a), 0, n, lt);
+    return;
+  }
+  if (t == 0) {  // __move_median_to_first(first, first + 1, mid, last - 1)
+    const int x = 1, y = n / 2, z = n - 1;
+    int m;
+    if (lt(a[x], a[y])) m = lt(a[y], a[z]) ? y : (lt(a[x], a[z]) ? z : x);
+    else m = lt(a[x], a[z]) ? x : (lt(a[y], a[z]) ? z : y);
+    const unsigned long long v = a[0]; a[0] = a[m]; a[m] = v;
+  }
+  __syncthreads();
+  const unsigned long long P = a[0];
+  __shared__ int wcnt[kIsT / 64];
+  __shared__ int s_first;
+  // stop lists: L = ascending positions in [1, n) with !(a < P); R = descending positions in
+  // [0, n) with !(P < a)
+  int nL = 0, nR = 0;
+  for (int side = 0; side < 2; ++side) {
+    int tot_all = 0;
+    for (int t0 = 0; t0 < n; t0 += kIsT * kIsE) {
+      unsigned long long m[kIsE];
+      int cnt = 0;
+#pragma unroll
+      for (int e = 0; e < kIsE; ++e) {
+        const int k = t0 + (w * kIsE + e) * 64 + ln;  // k-th position in scan order
+        bool f;
+        if (side == 0) f = k + 1 < n && !lt(a[k + 1], P);
+        else f = k < n && !lt(P, a[n - 1 - k]);
+        m[e] = __ballot(f);
+        cnt += (int)__popcll(m[e]);
+      }
+      if (ln == 0) wcnt[w] = cnt;
+      __syncthreads();
+      int off = 0, tot = 0;
+      for (int q = 0; q < kIsT / 64; ++q) {
+        off += q < w ? wcnt[q] : 0;
+        tot += wcnt[q];
+      }
+      off += tot_all;
+#pragma unroll
+      for (int e = 0; e < kIsE; ++e) {
+        const int k = t0 + (w * kIsE + e) * 64 + ln;
+        if ((m[e] >> ln) & 1ull) {
+          const int pos = off + (int)__popcll(m[e] & ltm);
+          if (side == 0) Lp[pos] = k + 1;
+          else Rp[pos] = n - 1 - k;
+        }
+        off += (int)__popcll(m[e]);
+      }
+      tot_all += tot;
+      __syncthreads();
+    }
+    if (side == 0) nL = tot_all;
+    else nR = tot_all;
+  }
+  // k* = first k < min(nL, nR) with !(L[k] < R[k]) (monotone): kIsT-ary search
+  const int nm = nL < nR ? nL : nR;
+  int lo = 0, hi = nm;  // good below lo, bad from hi
+  while (hi > lo) {
+    const int step = (hi - lo + kIsT - 1) / kIsT;
+    if (t == 0) s_first = kIsT;
+    __syncthreads();
+    const int k = lo + t * step;
+    if (k < hi && !(Lp[k] < Rp[k])) atomicMin(&s_first, t);
+    __syncthreads();
+    const int tb = s_first;
+    __syncthreads();
+    if (tb < kIsT) {
+      const int nlo = tb > 0 ? lo + (tb - 1) * step + 1 : lo;
+      hi = lo + tb * step;
+      lo = nlo;
+    } else {
+      const int tlast = min(kIsT - 1, (hi - 1 - lo) / step);
+      lo = lo + tlast * step + 1;
+    }
+  }
+  const int ks = lo;
+  const int cut = (ks > 0 && (ks >= nL || Lp[ks] >= Rp[ks - 1])) ? Rp[ks - 1] : Lp[ks];
+  for (int k = t; k < ks; k += kIsT) {
+    const int x = Lp[k], y = Rp[k];
+    const unsigned long long v = a[x]; a[x] = a[y]; a[y] = v;
+  }
+  if (t == 0) {
+    is_push(IsRange{r.f, r.f + cut, r.d - 1, 0}, nxt, n_nxt, leaves, n_leaves);
+    is_push(IsRange{r.f + cut, r.l, r.d - 1, 0}, nxt, n_nxt, leaves, n_leaves);
+  }
+}
+
+// One wave per range of at most kIsLeaf elements: the rest of its introsort, in LDS.
+__global__ __launch_bounds__(64) void k_is_leaf(unsigned long long* kk, const IsRange* leaves) {
+  __shared__ uint64_t key[kIsLeaf];
+  __shared__ uint16_t Lp[kIsLeaf], Rp[kIsLeaf];
+  __shared__ int stk[3 * kSortStack];
+  __shared__ uint64_t leafw[kIsLeaf / 64 + 1];
+  const IsRange r = leaves[blockIdx.x];
+  const int n = (int)(r.l - r.f);
+  for (int k = threadIdx.x; k < n; k += 64) key[k] = kk[r.f + k];
+  wave_sync_lds();
+  exact_introsort(key, n, Lp, Rp, stk, leafw, VoxLess{}, r.d);
+  for (int k = threadIdx.x; k < n; k += 64) kk[r.f + k] = key[k];
+}
+
+// Sorted index_vector -> the (segment << 32 | voxel id, point index) pairs the head / centroid
+// passes read.
+__global__ __launch_bounds__(256) void k_vg_unpack(const Chunk* ch, const long long* base,
+                                                   const unsigned long long* kk, unsigned long long* key, int* val) {
+  const Chunk c = ch[blockIdx.x];
+  const long long o = base[c.seg];
+  for (long long i = c.b + threadIdx.x; i < c.e; i += blockDim.x) {
+    const unsigned long long v = kk[o + i];
+    key[o + i] = ((unsigned long long)c.seg << 32) | (v >> 32);
+    val[o + i] = (int)(unsigned)(v & 0xffffffffull);
   }
 }
 
@@ -225,11 +376,6 @@ hipError_t grow(T*& p, size_t& cap, size_t need) {
   return e;
 }
 
-int ceil_log2(int s) {
-  int b = 0;
-  while ((1 << b) < s) ++b;
-  return b;
-}
 
 }  // namespace
 
@@ -269,6 +415,9 @@ struct llsr_map {
   size_t cap_hstage = 0;
   char* dxf = nullptr;         // device chunk table of k_map_transform
   size_t cap_dxf = 0;
+  char* isbuf = nullptr;       // exact introsort: range lists + counters
+  size_t cap_isbuf = 0;
+  int* hcnt = nullptr;         // pinned counters
 };
 
 static int32_t mfail(llsr_map* m, int32_t code, const std::string& msg) {
@@ -351,24 +500,73 @@ int32_t vg_run(llsr_map* m, const std::vector<VgCloud>& cl, float4* d_out, long 
   MAP_OK(m, grow(m->rank, m->cap_rank, N));
   MAP_OK(m, grow(m->mm, m->cap_mm, 6 * (size_t)S));
   MAP_OK(m, grow(m->par, m->cap_par, (size_t)S));
-  const int end_bit = 32 + ceil_log2(S);
-  size_t tb_sort = 0, tb_scan = 0;
-  MAP_OK(m, hipcub::DeviceRadixSort::SortPairs(nullptr, tb_sort, m->key, m->key2, m->val, m->val2, (int)N, 0,
-                                                end_bit, s));
+  size_t tb_scan = 0;
   MAP_OK(m, hipcub::DeviceScan::ExclusiveSum(nullptr, tb_scan, m->flag, m->rank, (int)N, s));
-  MAP_OK(m, grow(reinterpret_cast<char*&>(m->tmp), m->cap_tmp, std::max(tb_sort, tb_scan)));
+  MAP_OK(m, grow(reinterpret_cast<char*&>(m->tmp), m->cap_tmp, tb_scan));
   const int nch = (int)ch.size();
   k_vg_init<<<(S + 63) / 64, 64, 0, s>>>(m->mm, S);
   k_vg_minmax<<<nch, 256, 0, s>>>(dch, dseg, m->mm);
   k_vg_params<<<(S + 63) / 64, 64, 0, s>>>(dseg, m->mm, m->par, S);
-  k_vg_keys<<<nch, 256, 0, s>>>(dch, dseg, m->par, dbase, m->key, m->val);
+  k_vg_keys<<<nch, 256, 0, s>>>(dch, dseg, m->par, dbase, m->key);
   MAP_OK(m, hipGetLastError());
-  size_t tb = m->cap_tmp;
-  MAP_OK(m, hipcub::DeviceRadixSort::SortPairs(m->tmp, tb, m->key, m->key2, m->val, m->val2, (int)N, 0, end_bit,
-                                                s));
+  // std::sort of every segment's index_vector (m->key), the stop lists in flag / rank
+  {
+    std::vector<IsRange> big, small;
+    for (int k = 0; k < S; ++k) {
+      const long long n = cl[k].n;
+      if (n < 2) continue;
+      int lg = 0;
+      while ((2ll << lg) <= n) ++lg;  // std::__lg
+      const IsRange r{base[k], base[k] + n, 2 * lg, 0};
+      (n > kIsLeaf ? big : small).push_back(r);
+    }
+    const size_t capA = (size_t)(N / kIsLeaf) + S + 2;
+    const size_t capL = 84 * ((size_t)(N / kIsLeaf) + 1) + S + 2;
+    const size_t o_b = align256(capA * sizeof(IsRange)), o_l = o_b + o_b,
+                 o_c = o_l + align256(capL * sizeof(IsRange)), bytes_is = o_c + 256;
+    MAP_OK(m, grow(m->isbuf, m->cap_isbuf, bytes_is));
+    if (!m->hcnt) MAP_OK(m, hipHostMalloc((void**)&m->hcnt, 4 * sizeof(int)));
+    IsRange* lA = reinterpret_cast<IsRange*>(m->isbuf);
+    IsRange* lB = reinterpret_cast<IsRange*>(m->isbuf + o_b);
+    IsRange* lL = reinterpret_cast<IsRange*>(m->isbuf + o_l);
+    int* dcnt = reinterpret_cast<int*>(m->isbuf + o_c);
+    // the host tables above were uploaded from htab asynchronously: stage the ranges after them
+    const size_t o_h = align256(bytes) , hneed = o_h + align256(std::max(big.size(), small.size()) * sizeof(IsRange) + 1);
+    MAP_OK(m, hipStreamSynchronize(s));
+    MAP_OK(m, host_grow(m->htab, m->cap_htab, hneed + align256((S + 1) * sizeof(long long))));
+    // (host_grow may have moved htab: re-stage the offsets area after the sort, below)
+    if (!big.empty()) {
+      std::memcpy(m->htab + o_h, big.data(), big.size() * sizeof(IsRange));
+      MAP_OK(m, hipMemcpyAsync(lA, m->htab + o_h, big.size() * sizeof(IsRange), hipMemcpyHostToDevice, s));
+      MAP_OK(m, hipStreamSynchronize(s));
+    }
+    if (!small.empty()) {
+      std::memcpy(m->htab + o_h, small.data(), small.size() * sizeof(IsRange));
+      MAP_OK(m, hipMemcpyAsync(lL, m->htab + o_h, small.size() * sizeof(IsRange), hipMemcpyHostToDevice, s));
+    }
+    m->hcnt[0] = 0;
+    m->hcnt[1] = (int)small.size();
+    MAP_OK(m, hipMemcpyAsync(dcnt, m->hcnt, 2 * sizeof(int), hipMemcpyHostToDevice, s));
+    MAP_OK(m, hipStreamSynchronize(s));
+    int nA = (int)big.size();
+    while (nA > 0) {
+      MAP_OK(m, hipMemsetAsync(dcnt, 0, sizeof(int), s));
+      k_is_level<<<nA, kIsT, 0, s>>>(m->key, lA, nA, lB, dcnt, lL, dcnt + 1, m->flag, m->rank);
+      MAP_OK(m, hipGetLastError());
+      MAP_OK(m, hipMemcpyAsync(m->hcnt, dcnt, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+      MAP_OK(m, hipStreamSynchronize(s));
+      nA = m->hcnt[0];
+      if ((size_t)nA > capA || (size_t)m->hcnt[1] > capL) return mfail(m, LLSR_EIO, "voxel grid: introsort range lists overflow");
+      std::swap(lA, lB);
+    }
+    const int nLeaves = m->hcnt[1];
+    if (nLeaves > 0) k_is_leaf<<<nLeaves, 64, 0, s>>>(m->key, lL);
+    k_vg_unpack<<<nch, 256, 0, s>>>(dch, dbase, m->key, m->key2, m->val2);
+    MAP_OK(m, hipGetLastError());
+  }
   const int nb = (int)((N + 255) / 256);
   k_vg_heads<<<nb, 256, 0, s>>>(m->key2, m->flag, N);
-  tb = m->cap_tmp;
+  size_t tb = m->cap_tmp;
   MAP_OK(m, hipcub::DeviceScan::ExclusiveSum(m->tmp, tb, m->flag, m->rank, (int)N, s));
   k_vg_centroid<<<nb, 256, 0, s>>>(m->key2, m->val2, m->flag, m->rank, dseg, d_out, N);
   k_vg_offsets<<<(S + 64) / 64, 64, 0, s>>>(dbase, m->flag, m->rank, N, S, doff);
@@ -414,11 +612,12 @@ extern "C" void llsr_map_destroy(llsr_map* m) {
   (void)hipSetDevice(m->device);
   (void)hipStreamSynchronize(m->stream);
   void* dev[] = {m->store, m->key, m->key2, m->val, m->val2, m->flag, m->rank, m->tmp, m->mm, m->par, m->dtab,
-                 m->mapbuf, m->dsbuf, m->poses, m->dxf};
+                 m->mapbuf, m->dsbuf, m->poses, m->dxf, m->isbuf};
   for (void* p : dev)
     if (p) (void)hipFree(p);
   if (m->htab) (void)hipHostFree(m->htab);
   if (m->hstage) (void)hipHostFree(m->hstage);
+  if (m->hcnt) (void)hipHostFree(m->hcnt);
   (void)hipStreamDestroy(m->stream);
   delete m;
 }

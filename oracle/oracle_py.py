@@ -515,11 +515,11 @@ def odometry_to_transform(transform_sum_fa) -> np.ndarray:
 
 class OracleMapping:
     """MapOptimization::run (MO:1854-1896) fed by OracleOdometry, one sequence: the CPU statement of
-    llsr_mapping_batch. `stable` sums each VoxelGrid voxel in input order (the device's order);
-    False follows PCL's std::sort order (float rounding only, DESIGN.md)."""
+    llsr_mapping_batch. Every VoxelGrid follows PCL (std::sort's order of equal voxel ids), as the
+    device does; `stable` = True would sum each voxel in input order instead (diagnostics)."""
 
     def __init__(self, cfg: _abi.Config, mo_mode: int, radius=50.0, keypose_leaf=1.0, corner_leaf=0.2,
-                 surf_leaf=0.4, outlier_leaf=0.4, stable: bool = True):
+                 surf_leaf=0.4, outlier_leaf=0.4, stable: bool = False):
         import copy
         self.odo = OracleOdometry(cfg)
         self.cfg_mo = copy.copy(cfg)

@@ -6,11 +6,9 @@ state is compared with the oracle's: frame / keyframe counts, whether scan-to-ma
 the query and local-map sizes, the LM report, transformSum / TobeMapped / BefMapped / AftMapped,
 and at the end the key poses (cloudKeyPoses6D).
 
-Bar: counts equal; poses within 1e-4. The chain is not bit-exact end to end for one documented
-reason: PCL's VoxelGrid sums a voxel's points in std::sort's tie order, the device in input order
-(the oracle's VoxelGrids run in the device order here, stable=True, but the
-odometry's per-ring less-flat VoxelGrid in the oracle follows PCL), so the LM inputs may differ in
-the last bits of a centroid.
+Bar: bit-exact end to end — counts, LM reports, every pose and the key poses equal the oracle's.
+Every VoxelGrid on both sides sums a voxel in the order libstdc++'s std::sort leaves PCL's
+index_vector, and both LMs sum their normal equations in Eigen's order.
 """
 import numpy as np
 import pytest
@@ -19,7 +17,6 @@ import oracle_py
 from llsr import Pipeline, _abi, default_config, synth
 
 pytestmark = pytest.mark.gpu
-TOL = 1e-4
 POSES = ("transform_sum", "transform_tobe_mapped", "transform_bef_mapped", "transform_aft_mapped")
 
 
