@@ -370,6 +370,127 @@ def odometry_leg(dev, lidar: str, B: int, seqs: int, frames: int, steps: int, wa
     return out
 
 
+def _mapping_cpu_worker(args):
+    """One CPU process of the mapping leg's multi-core baseline: the oracle chain over one sequence,
+    timing frames >= `skip` only (the same frame indices the device leg times)."""
+    seed0, frames, skip, mo_mode, budget = args
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle_py
+    from llsr import _abi, synth
+    cfg = _abi.config_for("vlp16")
+    cfg.mode = _abi.LLSR_MODE_LM_APPLIED
+    om = oracle_py.OracleMapping(cfg, mo_mode)
+    n, t = 0, 0.0
+    for k in range(frames):
+        scan = synth.make_scan(seed0 + k, "vlp16")
+        t1 = time.perf_counter()
+        om.process(scan)
+        if k >= skip:
+            t += time.perf_counter() - t1
+            n += 1
+        if t > budget:
+            break
+    return n, t
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def mapping_leg(dev, B: int, seqs: int, warmup: int, steps: int, dist, check: bool, cpu_seconds: float,
+                mo_mode_name: str = "lm_applied") -> dict:
+    """The mapping chain (llsr_mapping_batch): B independent VLP-16 drives, one scan each per step,
+    through ImageProjection + features + scan-to-scan LM + OdometryToTransform +
+    transformAssociateToMap + extractSurroundingKeyFrames + downsampleCurrentScan + scan-to-map LM +
+    transformUpdate + keyframe, all slots batched on the device. `seqs` distinct drives (0.5 m
+    between scans) are tiled over the slots; the timed steps are frames warmup .. warmup+steps-1
+    of every drive (the local map keeps growing: every frame is a keyframe, MO:1629)."""
+    import torch
+    from llsr import Pipeline, _abi, default_config, synth
+    from llsr.dist import max_over_ranks
+    mo_mode = {"lm_applied": _abi.LLSR_MODE_LM_APPLIED, "faithful": _abi.LLSR_MODE_FAITHFUL}[mo_mode_name]
+    cfg = default_config("vlp16")
+    cfg.mode = _abi.LLSR_MODE_LM_APPLIED
+    H, W = cfg.num_vertical_scans, cfg.num_horizontal_scans
+    rank = dist.get_rank() if dist else 0
+    frames = warmup + steps
+    seeds = [1 + 64 * (q + 4 * rank) for q in range(seqs)]
+    seq_scans = [[synth.make_scan(s0 + k, "vlp16") for k in range(frames)] for s0 in seeds]
+    batches = []
+    for k in range(frames):
+        scans = [seq_scans[b % seqs][k] for b in range(B)]
+        off = np.zeros(B + 1, np.int64)
+        off[1:] = np.cumsum([len(a) for a in scans])
+        batches.append((torch.from_numpy(np.concatenate(scans)).to(dev), torch.from_numpy(off).to(dev)))
+    pipe = Pipeline(cfg, device=dev, max_batch=B, max_points=H * W)
+    pipe.mapping_init(mo_mode)
+    torch.cuda.synchronize(dev)
+    for k in range(warmup):
+        pipe.mapping_batch(batches[k][0].data_ptr(), batches[k][1].data_ptr(), B)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(warmup, frames):
+        pipe.mapping_batch(batches[k][0].data_ptr(), batches[k][1].data_ptr(), B)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    el = max_over_ranks(time.perf_counter() - t0, dev)
+    world = dist.get_world_size() if dist else 1
+    s0 = pipe.mapping_fetch(0)
+    out = {"workload": f"VLP-16 mapping chain: IP + features + scan-to-scan LM + MapOptimization::run "
+                       f"(local map, downsample, scan-to-map LM mode {mo_mode_name}, keyframes), {B} drives per "
+                       f"GPU, frames {warmup}..{frames - 1} of each (every frame a keyframe)",
+           "value": round(B * steps * world / el, 1), "unit": "scans/s", "scaling": "weak", "steps": steps,
+           "drives_per_gpu": B, "ms_per_step": round(el / steps * 1e3, 3),
+           "slot0": {"keyframes": s0["keyframes"], "lm_iterations": s0["lm"]["iterations"],
+                     "corner_map_ds": s0["map"]["n_corner_ds"], "surf_map_ds": s0["map"]["n_surf_ds"],
+                     "corner_q": s0["n_corner_q"], "surf_q": s0["n_surf_q"]}}
+    if check:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle_py
+        om = oracle_py.OracleMapping(cfg, mo_mode)
+        t_cpu = 0.0
+        for k in range(frames):
+            t1 = time.perf_counter()
+            o = om.process(seq_scans[0][k])
+            if k >= warmup:
+                t_cpu += time.perf_counter() - t1
+        out["bit_exact_slot0"] = bool(all(np.array_equal(s0[key], o[key]) for key in
+                                          ("transform_sum", "transform_tobe_mapped", "transform_aft_mapped")))
+        n1 = steps
+        out["cpu_baseline"] = {"value": round(n1 / t_cpu, 2), "unit": "scans/s", "cores": 1, "kind": "port",
+                               "cpu": cpu_model(),
+                               "sample": f"frames {warmup}..{frames - 1} of drive 0 through the oracle chain "
+                                         f"(oracle_py.OracleMapping), 1 thread, {t_cpu:.1f} s"}
+        # every host core the box grants this job (16 on the GPU pool): one drive per process
+        import multiprocessing as mp
+        nproc = min(16, os.cpu_count() or 1)
+        jobs = [(1 + 64 * (q + 4 * rank) + 256 * (q // seqs), frames, warmup, mo_mode, cpu_seconds)
+                for q in range(nproc)]
+        t1 = time.perf_counter()
+        with mp.get_context("spawn").Pool(nproc) as pool:
+            res = pool.map(_mapping_cpu_worker, jobs)
+        wall = time.perf_counter() - t1
+        nf = sum(r[0] for r in res)
+        busy = max(r[1] for r in res)
+        out["cpu_baseline_all_cores"] = {
+            "value": round(nf / busy, 2), "unit": "scans/s", "cores": nproc, "kind": "port", "cpu": cpu_model(),
+            "sample": f"{nproc} processes, one drive each, frames {warmup}..{frames - 1} timed ({nf} frames, "
+                      f"slowest process {busy:.1f} s busy, {wall:.1f} s wall incl. start-up and untimed frames)"}
+        out["speedup_vs_cpu"] = round(out["value"] / world / out["cpu_baseline"]["value"], 1)
+        out["speedup_vs_cpu_all_cores"] = round(out["value"] / world / out["cpu_baseline_all_cores"]["value"], 1)
+    pipe.close()
+    return out
+
+
 def local_map_leg(dev, K: int, steps: int, warmup: int, dist, check: bool, cpu_seconds: float) -> dict:
     """MapOptimization local map (llsr_map_extract, MO:1096-1232): a store of K synthetic keyframes
     (VLP-16-sized clouds: 200 corner, 6000 surf, 1500 outlier points) along an out-and-back path;
@@ -535,6 +656,8 @@ def main():
     ap.add_argument("--map-keyframes", type=int, default=200,
                     help="local-map leg: keyframes in the store (0 = skip)")
     ap.add_argument("--pc2", type=int, default=1, help="PointCloud2 decode leg (0 = skip)")
+    ap.add_argument("--mapping", default="256:8:8",
+                    help="mapping-chain leg drives_per_gpu:warmup_frames:timed_frames (empty = skip)")
     ap.add_argument("--allreduce-scans", type=int, default=8,
                     help="configs[4] leg: scans per step split over all ranks (0 = skip)")
     args = ap.parse_args()
@@ -667,6 +790,12 @@ def main():
         lmap = local_map_leg(dev, args.map_keyframes, args.s2m_steps * 4, 2, dist,
                              rank == 0 and not args.no_cpu and world == 1, min(args.cpu_seconds, 8.0))
 
+    mapping = None
+    if args.mapping:
+        mb, mw, ms_ = (int(x) for x in args.mapping.split(":"))
+        mapping = mapping_leg(dev, mb, 4, mw, ms_, dist, rank == 0 and not args.no_cpu and world == 1,
+                              min(args.cpu_seconds, 20.0))
+
     allred = None
     if args.allreduce_scans > 0:
         allred = scan2map_allreduce_leg(dev, args.allreduce_scans, args.s2m_steps, 1, dist,
@@ -703,6 +832,7 @@ def main():
             "scan2map_allreduce": allred,
             "odometry": odo,
             "local_map": lmap,
+            "mapping": mapping,
             "pointcloud2_decode": pc2,
         }
         if not args.no_cpu and world == 1:

@@ -2,6 +2,7 @@
 // pool, the per-batch launch sequence and result fetch. No C++ exception crosses the ABI.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <climits>
 #include <cmath>
@@ -137,8 +138,8 @@ struct llsr_handle {
     llsr_map_config mcfg{};
     llsr_map* vg = nullptr;            // VoxelGrid engine of the batched downsample
     std::vector<MapSlot> slot;
-    float4 *outl = nullptr, *ds = nullptr, *tot = nullptr, *cmap = nullptr, *smap = nullptr;
-    size_t cap_outl = 0, cap_ds = 0, cap_tot = 0, cap_cmap = 0, cap_smap = 0;
+    float4 *outl = nullptr, *ds = nullptr, *tot = nullptr, *cmap = nullptr;  // cmap: empty-map base
+    size_t cap_outl = 0, cap_ds = 0, cap_tot = 0, cap_cmap = 0;
     void* small = nullptr;             // device: pose [B][6], report [B], deg [B], matP [B][36], off [5][B+1]
     void* hsmall = nullptr;            // pinned host mirror
     float* d_pose = nullptr; llsr_lm_report* d_rep = nullptr; int* d_deg = nullptr; float* d_matP = nullptr;
@@ -381,8 +382,7 @@ extern "C" void llsr_destroy(llsr_handle* h) {
   for (auto& sl : h->mp.slot)
     if (sl.map) llsr_map_destroy(sl.map);
   if (h->mp.vg) llsr_map_destroy(h->mp.vg);
-  for (void* p : {(void*)h->mp.outl, (void*)h->mp.ds, (void*)h->mp.tot, (void*)h->mp.cmap, (void*)h->mp.smap,
-                  h->mp.small})
+  for (void* p : {(void*)h->mp.outl, (void*)h->mp.ds, (void*)h->mp.tot, (void*)h->mp.cmap, h->mp.small})
     if (p) (void)hipFree(p);
   if (h->mp.hsmall) (void)hipHostFree(h->mp.hsmall);
   if (h->d_in) (void)hipFree(h->d_in);
@@ -1537,52 +1537,64 @@ extern "C" int32_t llsr_mapping_batch(llsr_handle* h, const float* d_xyzi, const
   if (rc != LLSR_OK) return rc;
   rc = llsr_mapping::voxel_multi(mp.vg, tsrc.data(), tcnt.data(), tleaf.data(), NB, mp.tot, toto.data(), s);
   if (rc != LLSR_OK) return fail(h, rc, std::string("downsample: ") + llsr_map_last_error(mp.vg));
-  // extractSurroundingKeyFrames (MO:1096-1232) per slot around currentRobotPosPoint
+  // extractSurroundingKeyFrames (MO:1096-1232) around currentRobotPosPoint, every slot with
+  // keyframes in one pass (a slot without keyframes keeps an empty local map, MO:1097)
+  std::vector<llsr_map*> emaps;
+  std::vector<int> eslot;
+  std::vector<float> epos;
+  for (int b = 0; b < B; ++b) {
+    auto& sl = mp.slot[b];
+    if (!step[b]) continue;
+    sl.mrep = llsr_map_report{};
+    sl.n_cq = (int)(dso[3 * NB + b + 1] - dso[3 * NB + b]);
+    sl.n_sq = (int)(toto[b + 1] - toto[b]);
+    if (llsr_map_num_keyframes(sl.map) == 0) continue;
+    emaps.push_back(sl.map);
+    eslot.push_back(b);
+    epos.insert(epos.end(), sl.robot, sl.robot + 3);
+  }
+  const int nE = (int)emaps.size();
+  std::vector<llsr_map_report> ereps(nE > 0 ? nE : 1);
+  std::vector<long long> eoc(nE + 1, 0), eos(nE + 1, 0);
+  const float4* lmap = nullptr;
+  if (nE > 0) {
+    rc = llsr_mapping::extract_multi(mp.vg, emaps.data(), nE, epos.data(), ereps.data(), &lmap, eoc.data(),
+                                     eos.data(), s);
+    if (rc != LLSR_OK) return fail(h, rc, std::string("extract: ") + llsr_map_last_error(mp.vg));
+  } else {
+    rc = mp_grow(h, mp.cmap, mp.cap_cmap, 1, 0, s);  // a valid (empty) map base for the batch
+    if (rc != LLSR_OK) return rc;
+    lmap = mp.cmap;
+  }
   int64_t* hcq = mp.h_off;
   int64_t* hsq = mp.h_off + nb;
   int64_t* hmc = mp.h_off + 2 * (size_t)nb;
   int64_t* hms = mp.h_off + 3 * (size_t)nb;
-  hmc[0] = hms[0] = 0;
   long long mMc = 1, mMs = 1, mQc = 1, mQs = 1;
-  for (int b = 0; b < NB; ++b) {
-    hcq[b] = dso[3 * NB + b];
-    hsq[b] = toto[b];
-    auto& sl = mp.slot[b];
-    long long nc = 0, ns = 0;
-    if (b < B && step[b]) {
-      sl.mrep = llsr_map_report{};
-      if (llsr_map_num_keyframes(sl.map) > 0) {
-        for (int attempt = 0;; ++attempt) {
-          rc = llsr_map_extract(sl.map, sl.robot, (float*)(mp.cmap + hmc[b]), (int64_t)mp.cap_cmap - hmc[b],
-                                (float*)(mp.smap + hms[b]), (int64_t)mp.cap_smap - hms[b], &sl.mrep, s);
-          if (rc == LLSR_ERANGE && attempt == 0) {
-            int32_t g = mp_grow(h, mp.cmap, mp.cap_cmap, (size_t)(hmc[b] + sl.mrep.n_corner_ds), hmc[b], s);
-            if (g == LLSR_OK)
-              g = mp_grow(h, mp.smap, mp.cap_smap, (size_t)(hms[b] + sl.mrep.n_surf_ds), hms[b], s);
-            if (g != LLSR_OK) return g;
-            continue;
-          }
-          if (rc != LLSR_OK) return fail(h, rc, std::string("extract: ") + llsr_map_last_error(sl.map));
-          break;
-        }
-        nc = sl.mrep.n_corner_ds;
-        ns = sl.mrep.n_surf_ds;
+  {
+    long long cc = eoc[0], cs = eos[0];
+    int e = 0;
+    for (int b = 0; b < NB; ++b) {
+      hcq[b] = dso[3 * NB + b];
+      hsq[b] = toto[b];
+      hmc[b] = cc;
+      hms[b] = cs;
+      if (e < nE && eslot[e] == b) {
+        mp.slot[b].mrep = ereps[e];
+        cc = eoc[e + 1];
+        cs = eos[e + 1];
+        ++e;
       }
-      sl.n_cq = (int)(dso[3 * NB + b + 1] - dso[3 * NB + b]);
-      sl.n_sq = (int)(toto[b + 1] - toto[b]);
+      mMc = std::max(mMc, (long long)(cc - hmc[b]));
+      mMs = std::max(mMs, (long long)(cs - hms[b]));
+      mQc = std::max(mQc, (long long)(dso[3 * NB + b + 1] - dso[3 * NB + b]));
+      mQs = std::max(mQs, (long long)(toto[b + 1] - toto[b]));
     }
-    hmc[b + 1] = hmc[b] + nc;
-    hms[b + 1] = hms[b] + ns;
-    mMc = nc > mMc ? nc : mMc;
-    mMs = ns > mMs ? ns : mMs;
-    const long long qc = dso[3 * NB + b + 1] - dso[3 * NB + b], qs = toto[b + 1] - toto[b];
-    mQc = qc > mQc ? qc : mQc;
-    mQs = qs > mQs ? qs : mQs;
+    hmc[NB] = cc;
+    hms[NB] = cs;
+    hcq[NB] = dso[4 * NB];
+    hsq[NB] = toto[NB];
   }
-  hcq[NB] = dso[4 * NB];
-  hsq[NB] = toto[NB];
-  if (!mp.cmap) { rc = mp_grow(h, mp.cmap, mp.cap_cmap, 1, 0, s); if (rc != LLSR_OK) return rc; }
-  if (!mp.smap) { rc = mp_grow(h, mp.smap, mp.cap_smap, 1, 0, s); if (rc != LLSR_OK) return rc; }
   // scan2MapOptimization (MO:1572-1610): every slot is a problem; slots without a step, or whose
   // map fails MO:1573, stay inactive and keep their pose and LM members
   rc = llsr_scan2map_reserve(h, NB, (int32_t)mMc, (int32_t)mMs, (int32_t)mQc, (int32_t)mQs);
@@ -1595,8 +1607,8 @@ extern "C" int32_t llsr_mapping_batch(llsr_handle* h, const float* d_xyzi, const
   sb.n_problems = NB;
   sb.corner_q = (const float*)mp.ds; sb.corner_q_off = mp.d_off;
   sb.surf_q = (const float*)mp.tot; sb.surf_q_off = mp.d_off + nb;
-  sb.corner_map = (const float*)mp.cmap; sb.corner_map_off = mp.d_off + 2 * (size_t)nb;
-  sb.surf_map = (const float*)mp.smap; sb.surf_map_off = mp.d_off + 3 * (size_t)nb;
+  sb.corner_map = (const float*)lmap; sb.corner_map_off = mp.d_off + 2 * (size_t)nb;
+  sb.surf_map = (const float*)lmap; sb.surf_map_off = mp.d_off + 3 * (size_t)nb;
   sb.pose = mp.d_pose;
   sb.report = mp.d_rep;
   S2MOpts opt;

@@ -338,18 +338,19 @@ __global__ void k_vg_offsets(const long long* base, const int* flag, const int* 
 
 // transformPointCloud(cloudIn, transformIn) (MO:671-701) of one keyframe chunk per block.
 struct XfChunk {
-  long long src, dst;  // store / map offsets (points)
+  const float4* src;   // keyframe cloud chunk in its map's store
+  long long dst;       // offset in the assembled map (points)
   int n, pad;
   float t[6];          // x, y, z, roll, pitch, yaw
 };
 
-__global__ __launch_bounds__(256) void k_map_transform(const XfChunk* ch, const float4* store, float4* map) {
+__global__ __launch_bounds__(256) void k_map_transform(const XfChunk* ch, float4* map) {
   const XfChunk c = ch[blockIdx.x];
   const float tx = c.t[0], ty = c.t[1], tz = c.t[2], roll = c.t[3], pitch = c.t[4], yaw = c.t[5];
   const float cy = cosf_(yaw), sy = sinf_(yaw), cr = cosf_(roll), sr = sinf_(roll), cp = cosf_(pitch),
               sp = sinf_(pitch);
   for (int k = threadIdx.x; k < c.n; k += blockDim.x) {
-    const float4 q = store[c.src + k];
+    const float4 q = c.src[k];
     const float x1 = cy * q.x - sy * q.y;
     const float y1 = sy * q.x + cy * q.y;
     const float z1 = q.z;
@@ -720,87 +721,111 @@ extern "C" int32_t llsr_map_add_keyframe(llsr_map* m, const float pose[6], const
   return (int32_t)m->kf.size() - 1;
 }
 
-extern "C" int32_t llsr_map_extract(llsr_map* m, const float pos[3], float* d_corner, int64_t cap_c, float* d_surf,
-                                    int64_t cap_s, llsr_map_report* rep, void* hip_stream) {
-  if (!m || !pos || !rep) return mfail(m, LLSR_EINVAL, "extract: bad arguments");
+// extractSurroundingKeyFrames (MO:1096-1232) of n maps at once, with `eng`'s VoxelGrid engine and
+// buffers: one key-pose VoxelGrid over every map's poses in radius, one transform launch over every
+// listed keyframe, one VoxelGrid over the n corner and n surf maps. The local maps land in eng's
+// dsbuf: map i's corner map at [off_c[i], off_c[i+1]), its surf map at [off_s[i], off_s[i+1]).
+int32_t llsr_mapping::extract_multi(llsr_map* eng, llsr_map* const* maps, int n, const float* pos,
+                                    llsr_map_report* reps, const float4** out, long long* off_c, long long* off_s,
+                                    hipStream_t s) {
+  llsr_map* m = eng;
+  if (!m || n < 1) return LLSR_EINVAL;
   const auto t0 = std::chrono::steady_clock::now();
-  std::memset(rep, 0, sizeof *rep);
-  MAP_OK(m, hipSetDevice(m->device));
-  const hipStream_t s = pick(m, hip_stream);
-  const int K = (int)m->kf.size();
-  if (K == 0) return LLSR_OK;  // MO:1097
   // radiusSearch (MO:1157-1159): d^2 = ((0 + dx^2) + dy^2) + dz^2 < float(r^2), over K poses
-  const float r2 = (float)((double)m->cfg.surrounding_radius * (double)m->cfg.surrounding_radius);
   std::vector<float4> sel;
-  for (int k = 0; k < K; ++k) {
-    const float* p = m->kf[k].pose;
-    float d = 0;
-    for (int a = 0; a < 3; ++a) {
-      const float df = pos[a] - p[a];
-      d += df * df;
+  std::vector<long long> sel_off(n + 1, 0);
+  for (int i = 0; i < n; ++i) {
+    llsr_map* mi = maps[i];
+    std::memset(&reps[i], 0, sizeof reps[i]);
+    const float r2 = (float)((double)mi->cfg.surrounding_radius * (double)mi->cfg.surrounding_radius);
+    const int K = (int)mi->kf.size();
+    const size_t s0 = sel.size();
+    for (int k = 0; k < K; ++k) {
+      const float* p = mi->kf[k].pose;
+      float d = 0;
+      for (int a = 0; a < 3; ++a) {
+        const float df = pos[3 * i + a] - p[a];
+        d += df * df;
+      }
+      if (d < r2) sel.push_back(make_float4(p[0], p[1], p[2], (float)k));
     }
-    if (d < r2) sel.push_back(make_float4(p[0], p[1], p[2], (float)k));
+    reps[i].n_in_radius = (int32_t)(sel.size() - s0);
+    sel_off[i + 1] = (long long)sel.size();
   }
-  rep->n_in_radius = (int32_t)sel.size();
   // surroundingKeyPosesDS (MO:1166-1167) on the device; intensity = the mean keyframe index
-  std::vector<int> ds_ids;
+  std::vector<std::vector<int>> ds_ids(n);
   if (!sel.empty()) {
-    MAP_OK(m, grow(m->poses, m->cap_poses, 2 * sel.size()));
-    MAP_OK(m, host_grow(m->hstage, m->cap_hstage, sel.size() * sizeof(float4)));
-    std::memcpy(m->hstage, sel.data(), sel.size() * sizeof(float4));
-    MAP_OK(m, hipMemcpyAsync(m->poses, m->hstage, sel.size() * sizeof(float4), hipMemcpyHostToDevice, s));
-    long long po[2];
-    int32_t rc = vg_run(m, {{m->poses, (long long)sel.size(), m->cfg.keypose_leaf}}, m->poses + sel.size(), po, s);
+    const size_t P = sel.size();
+    MAP_OK(m, grow(m->poses, m->cap_poses, 2 * P));
+    MAP_OK(m, host_grow(m->hstage, m->cap_hstage, 2 * P * sizeof(float4)));
+    std::memcpy(m->hstage, sel.data(), P * sizeof(float4));
+    MAP_OK(m, hipMemcpyAsync(m->poses, m->hstage, P * sizeof(float4), hipMemcpyHostToDevice, s));
+    std::vector<VgCloud> pc(n);
+    for (int i = 0; i < n; ++i) pc[i] = {m->poses + sel_off[i], sel_off[i + 1] - sel_off[i], maps[i]->cfg.keypose_leaf};
+    std::vector<long long> po(n + 1);
+    int32_t rc = vg_run(m, pc, m->poses + P, po.data(), s);
     if (rc != LLSR_OK) return rc;
-    std::vector<float4> ds(po[1]);
-    MAP_OK(m, hipMemcpyAsync(ds.data(), m->poses + sel.size(), po[1] * sizeof(float4), hipMemcpyDeviceToHost, s));
+    float4* hds = reinterpret_cast<float4*>(m->hstage) + P;
+    MAP_OK(m, hipMemcpyAsync(hds, m->poses + P, po[n] * sizeof(float4), hipMemcpyDeviceToHost, s));
     MAP_OK(m, hipStreamSynchronize(s));
-    for (const float4& q : ds) ds_ids.push_back((int)q.w);
+    for (int i = 0; i < n; ++i)
+      for (long long q = po[i]; q < po[i + 1]; ++q) ds_ids[i].push_back((int)hds[q].w);
   }
-  rep->n_poses_ds = (int32_t)ds_ids.size();
-  // MO:1169-1189: drop listed keyframes no downsampled pose names; MO:1190-1222: append new ones
-  std::vector<int> kept;
-  for (int id : m->existing)
-    for (int d : ds_ids)
-      if (d == id) { kept.push_back(id); break; }
-  m->existing.swap(kept);
-  for (int d : ds_ids) {
-    bool found = false;
-    for (int id : m->existing)
-      if (id == d) { found = true; break; }
-    if (!found) {
-      if (d < 0 || d >= K) return mfail(m, LLSR_ERANGE, "extract: key pose index out of range");
-      m->existing.push_back(d);
-      ++rep->n_transformed;
-    }
-  }
-  rep->n_keyframes = (int32_t)m->existing.size();
+  // MO:1169-1189: drop listed keyframes no downsampled pose names; MO:1190-1222: append new ones;
   // MO:1224-1228: corner map = corner clouds; surf map = surf + outlier clouds, in list order
   std::vector<XfChunk> xc;
-  long long nc = 0, ns = 0;
-  for (int id : m->existing) nc += m->kf[id].n[0];
-  for (int id : m->existing) ns += m->kf[id].n[1] + m->kf[id].n[2];
-  long long dc = 0, dsf = nc;
-  auto add = [&](const llsr_map::Kf& k, int a, long long& dst) {
-    for (int b = 0; b < k.n[a]; b += 1024) {
-      XfChunk x{};
-      x.src = k.off[a] + b;
-      x.dst = dst + b;
-      x.n = std::min(1024, k.n[a] - b);
-      std::memcpy(x.t, k.pose, sizeof x.t);
-      xc.push_back(x);
+  std::vector<long long> rc_off(n + 1, 0), rs_off(n + 1, 0);
+  for (int i = 0; i < n; ++i) {
+    llsr_map* mi = maps[i];
+    reps[i].n_poses_ds = (int32_t)ds_ids[i].size();
+    std::vector<int> kept;
+    for (int id : mi->existing)
+      for (int d : ds_ids[i])
+        if (d == id) { kept.push_back(id); break; }
+    mi->existing.swap(kept);
+    const int K = (int)mi->kf.size();
+    for (int d : ds_ids[i]) {
+      bool found = false;
+      for (int id : mi->existing)
+        if (id == d) { found = true; break; }
+      if (!found) {
+        if (d < 0 || d >= K) return mfail(m, LLSR_ERANGE, "extract: key pose index out of range");
+        mi->existing.push_back(d);
+        ++reps[i].n_transformed;
+      }
     }
-    dst += k.n[a];
-  };
-  for (int id : m->existing) {
-    add(m->kf[id], 0, dc);
-    add(m->kf[id], 1, dsf);
-    add(m->kf[id], 2, dsf);
+    reps[i].n_keyframes = (int32_t)mi->existing.size();
+    long long nc = 0, ns = 0;
+    for (int id : mi->existing) nc += mi->kf[id].n[0];
+    for (int id : mi->existing) ns += mi->kf[id].n[1] + mi->kf[id].n[2];
+    reps[i].n_corner_map = nc;
+    reps[i].n_surf_map = ns;
+    rc_off[i + 1] = rc_off[i] + nc;
+    rs_off[i + 1] = rs_off[i] + ns;
   }
-  rep->n_corner_map = nc;
-  rep->n_surf_map = ns;
-  MAP_OK(m, grow(m->mapbuf, m->cap_map, (size_t)(nc + ns)));
-  MAP_OK(m, grow(m->dsbuf, m->cap_ds, (size_t)(nc + ns)));
+  const long long NC = rc_off[n], NS = rs_off[n];
+  for (int i = 0; i < n; ++i) {
+    llsr_map* mi = maps[i];
+    long long dc = rc_off[i], dsf = NC + rs_off[i];
+    auto add = [&](const llsr_map::Kf& k, int a, long long& dst) {
+      for (int b = 0; b < k.n[a]; b += 1024) {
+        XfChunk x{};
+        x.src = mi->store + k.off[a] + b;
+        x.dst = dst + b;
+        x.n = std::min(1024, k.n[a] - b);
+        std::memcpy(x.t, k.pose, sizeof x.t);
+        xc.push_back(x);
+      }
+      dst += k.n[a];
+    };
+    for (int id : mi->existing) {
+      add(mi->kf[id], 0, dc);
+      add(mi->kf[id], 1, dsf);
+      add(mi->kf[id], 2, dsf);
+    }
+  }
+  MAP_OK(m, grow(m->mapbuf, m->cap_map, (size_t)(NC + NS)));
+  MAP_OK(m, grow(m->dsbuf, m->cap_ds, (size_t)(NC + NS)));
   if (!xc.empty()) {
     // hstage is free here: the key-pose VoxelGrid above ended with a stream sync
     const size_t bytes = xc.size() * sizeof(XfChunk);
@@ -808,24 +833,52 @@ extern "C" int32_t llsr_map_extract(llsr_map* m, const float pos[3], float* d_co
     MAP_OK(m, grow(m->dxf, m->cap_dxf, bytes));
     std::memcpy(m->hstage, xc.data(), bytes);
     MAP_OK(m, hipMemcpyAsync(m->dxf, m->hstage, bytes, hipMemcpyHostToDevice, s));
-    k_map_transform<<<(int)xc.size(), 256, 0, s>>>(reinterpret_cast<const XfChunk*>(m->dxf), m->store, m->mapbuf);
+    k_map_transform<<<(int)xc.size(), 256, 0, s>>>(reinterpret_cast<const XfChunk*>(m->dxf), m->mapbuf);
     MAP_OK(m, hipGetLastError());
   }
-  // MO:1225-1231: VoxelGrid corner / surf
-  long long o[3];
-  const int32_t rc = vg_run(m, {{m->mapbuf, nc, m->cfg.corner_leaf}, {m->mapbuf + nc, ns, m->cfg.surf_leaf}},
-                            m->dsbuf, o, s);
+  // MO:1225-1231: VoxelGrid corner / surf of every map
+  std::vector<VgCloud> mc(2 * n);
+  for (int i = 0; i < n; ++i) {
+    mc[i] = {m->mapbuf + rc_off[i], rc_off[i + 1] - rc_off[i], maps[i]->cfg.corner_leaf};
+    mc[n + i] = {m->mapbuf + NC + rs_off[i], rs_off[i + 1] - rs_off[i], maps[i]->cfg.surf_leaf};
+  }
+  std::vector<long long> o(2 * n + 1);
+  const int32_t rc = vg_run(m, mc, m->dsbuf, o.data(), s);
   if (rc != LLSR_OK) return rc;
-  rep->n_corner_ds = o[1] - o[0];
-  rep->n_surf_ds = o[2] - o[1];
+  for (int i = 0; i <= n; ++i) {
+    off_c[i] = o[i];
+    off_s[i] = o[n + i];
+  }
+  const float ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  for (int i = 0; i < n; ++i) {
+    reps[i].n_corner_ds = o[i + 1] - o[i];
+    reps[i].n_surf_ds = o[n + i + 1] - o[n + i];
+    reps[i].ms = ms;
+  }
+  *out = m->dsbuf;
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_map_extract(llsr_map* m, const float pos[3], float* d_corner, int64_t cap_c, float* d_surf,
+                                    int64_t cap_s, llsr_map_report* rep, void* hip_stream) {
+  if (!m || !pos || !rep) return mfail(m, LLSR_EINVAL, "extract: bad arguments");
+  const auto t0 = std::chrono::steady_clock::now();
+  std::memset(rep, 0, sizeof *rep);
+  MAP_OK(m, hipSetDevice(m->device));
+  const hipStream_t s = pick(m, hip_stream);
+  if (m->kf.empty()) return LLSR_OK;  // MO:1097
+  const float4* out = nullptr;
+  long long oc[2], os[2];
+  int32_t rc = llsr_mapping::extract_multi(m, &m, 1, pos, rep, &out, oc, os, s);
+  if (rc != LLSR_OK) return rc;
   if (rep->n_corner_ds > cap_c || rep->n_surf_ds > cap_s)
     return mfail(m, LLSR_ERANGE, "extract: local map exceeds the output capacity");
   if (rep->n_corner_ds && !d_corner) return mfail(m, LLSR_EINVAL, "extract: null corner output");
   if (rep->n_surf_ds && !d_surf) return mfail(m, LLSR_EINVAL, "extract: null surf output");
   if (rep->n_corner_ds)
-    MAP_OK(m, hipMemcpyAsync(d_corner, m->dsbuf, rep->n_corner_ds * sizeof(float4), hipMemcpyDeviceToDevice, s));
+    MAP_OK(m, hipMemcpyAsync(d_corner, out + oc[0], rep->n_corner_ds * sizeof(float4), hipMemcpyDeviceToDevice, s));
   if (rep->n_surf_ds)
-    MAP_OK(m, hipMemcpyAsync(d_surf, m->dsbuf + o[1], rep->n_surf_ds * sizeof(float4), hipMemcpyDeviceToDevice, s));
+    MAP_OK(m, hipMemcpyAsync(d_surf, out + os[0], rep->n_surf_ds * sizeof(float4), hipMemcpyDeviceToDevice, s));
   MAP_OK(m, hipStreamSynchronize(s));
   rep->ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return LLSR_OK;

@@ -22,6 +22,12 @@ namespace llsr_mapping {
 // Synchronises s.
 int32_t voxel_multi(llsr_map* m, const float4* const* src, const long long* n, const float* leaf, int S,
                     float4* out, long long* out_off, hipStream_t s);
+// extractSurroundingKeyFrames of n maps around pos[n][3] in one pass of `eng`'s engine: the local
+// maps in *out (eng-owned, valid until its next use), map i's corner map at [off_c[i], off_c[i+1]),
+// surf map at [off_s[i], off_s[i+1]); reps[i] as llsr_map_extract. A map without keyframes yields
+// empty maps (the caller skips the call for it, MO:1097). Synchronises s.
+int32_t extract_multi(llsr_map* eng, llsr_map* const* maps, int n, const float* pos, llsr_map_report* reps,
+                      const float4** out, long long* off_c, long long* off_s, hipStream_t s);
 
 // tf2::Quaternion::setRPY (tf2/LinearMath/Quaternion.h), double
 inline void tf2_set_rpy(double roll, double pitch, double yaw, double q[4]) {
