@@ -61,7 +61,7 @@ def cpu_baseline(scans: list[np.ndarray], budget_s: float) -> dict:
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle_py
     from llsr import _abi
-    ora = oracle_py.Oracle(_abi.config_for("vlp16"))
+    ora = oracle_py.Oracle(_abi.config_for("vlp16"), pcl_voxel_order=True)  # as PCL (std::sort)
     ora.process(scans[0])  # warm-up (page-in, first-frame state)
     n, t0 = 0, time.perf_counter()
     ip_ms = fa_ms = 0.0

@@ -66,6 +66,16 @@ typedef struct llsr_config {
 /* Fill *cfg with the YAML block for `lidar` (LLSR_LIDAR_VLP16 / LLSR_LIDAR_HDL64E). */
 int32_t llsr_config_default(llsr_config* cfg, int32_t lidar);
 
+/* The less-flat VoxelGrid of the feature stage (surfPointsLessFlatScan, FA:1268-1270) averages
+ * each 0.2 m voxel's points. PCL sums them in the order std::sort leaves its index_vector (equal
+ * voxel ids in libstdc++ introsort's order); LLSR_VOXEL_ORDER_PCL reproduces that exactly (one
+ * wave per ring emulates the introsort: costs ~6 ms per 1024 VLP-16 scans), the default
+ * LLSR_VOXEL_ORDER_INPUT sums each voxel in ring order (a centroid may differ from PCL's in the
+ * last bits when its voxel holds three or more points; voxel set, count and order are the same).
+ * MapOptimization's VoxelGrids (llsr_map_*, llsr_mapping_*) always follow PCL's order. */
+#define LLSR_VOXEL_ORDER_INPUT 0
+#define LLSR_VOXEL_ORDER_PCL 1
+
 /* Per-scan outputs of projection+segmentation (IP) and feature extraction (FA), in the
  * reference's own order. Host buffers, caller-allocated; capacities from llsr_query_sizes().
  * Any pointer may be NULL to skip that output. Counts are always written. */
@@ -141,6 +151,9 @@ int32_t llsr_query_sizes(const llsr_handle* h, llsr_sizes* out);
 /* Reset the per-slot FeatureAssociation carry-over state (FA:167-198: the H*W arrays that the
  * reference sizes once and never clears). */
 int32_t llsr_reset_state(llsr_handle* h);
+/* LLSR_VOXEL_ORDER_INPUT (default) or LLSR_VOXEL_ORDER_PCL for the less-flat VoxelGrid; takes
+ * effect from the next batch. */
+int32_t llsr_set_voxel_order(llsr_handle* h, int32_t order);
 
 /* One scan, host buffers in/out: the ImageProjection::cloudHandler + FeatureAssociation
  * feature-stage replacement. `xyzi` holds n raw points (x,y,z,intensity, NaN allowed). */

@@ -411,6 +411,13 @@ extern "C" int32_t llsr_query_sizes(const llsr_handle* h, llsr_sizes* s) {
   return LLSR_OK;
 }
 
+extern "C" int32_t llsr_set_voxel_order(llsr_handle* h, int32_t order) {
+  if (!h) return LLSR_EINVAL;
+  if (order != LLSR_VOXEL_ORDER_INPUT && order != LLSR_VOXEL_ORDER_PCL) return fail(h, LLSR_EINVAL, "voxel order");
+  h->dc.exact_vg = order == LLSR_VOXEL_ORDER_PCL ? 1 : 0;
+  return LLSR_OK;
+}
+
 extern "C" int32_t llsr_reset_state(llsr_handle* h) {
   if (!h) return LLSR_EINVAL;
   HIP_OK(h, hipSetDevice(h->device));
@@ -549,6 +556,30 @@ extern "C" int32_t llsr_debug_exact_sort(const float* vals, int32_t n, int32_t* 
   (void)hipFree(dv);
   (void)hipFree(di);
   return rc;
+}
+
+// Diagnostics (not part of the ABI header): mean device ms of one exact_introsort of vals[0, n)
+// by one wave (k_debug_exact_sort), over `reps` launches.
+extern "C" float llsr_debug_exact_sort_ms(const float* vals, int32_t n, int32_t reps) {
+  if (!vals || n < 1 || n > 2048 || reps < 1) return -1.f;
+  float* dv = nullptr;
+  int* di = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  float ms = -1.f;
+  if (hipMalloc(&dv, sizeof(float) * n) == hipSuccess && hipMalloc(&di, sizeof(int) * n) == hipSuccess &&
+      hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess &&
+      hipMemcpy(dv, vals, sizeof(float) * n, hipMemcpyHostToDevice) == hipSuccess) {
+    k_debug_exact_sort<<<1, 64>>>(dv, n, di);
+    (void)hipEventRecord(e0, nullptr);
+    for (int r = 0; r < reps; ++r) k_debug_exact_sort<<<1, 64>>>(dv, n, di);
+    (void)hipEventRecord(e1, nullptr);
+    if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess) ms /= reps;
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (dv) (void)hipFree(dv);
+  if (di) (void)hipFree(di);
+  return ms;
 }
 
 // Diagnostics (not part of the ABI header): re-launch kernel k on the last batch's buffers with

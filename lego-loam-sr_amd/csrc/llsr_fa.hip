@@ -247,10 +247,9 @@ __global__ __launch_bounds__(64) void k_debug_exact_sort(const float* vals, int 
   __shared__ uint64_t key[kRingMax];
   __shared__ uint16_t Lp[kRingMax], Rp[kRingMax];
   __shared__ int stk[3 * kSortStack];
-  __shared__ uint64_t leafw[kRingMax / 64 + 1];
   for (int t = threadIdx.x; t < n; t += 64) key[t] = ((uint64_t)__float_as_uint(vals[t]) << 32) | (uint32_t)t;
   wave_sync_lds();
-  exact_introsort(key, n, Lp, Rp, stk, leafw, CurvLess{});
+  exact_introsort(key, n, Lp, Rp, stk, CurvLess{});
   for (int t = threadIdx.x; t < n; t += 64) out[t] = (int)(uint32_t)key[t];
 }
 
@@ -400,7 +399,6 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   const bool ph_in = ph >= ws && ph - ws < wn;
   const float ph_curv = ph < 5 ? 0.0f : curv[ph];  // cloudCurvature[0..4] is never written (FA:819)
   if (sp == 4 && !ph_in && tid == 0) atomicAdd(&d.counts[b * kCnt + C_PHOUT], 1);
-  __shared__ uint64_t leafw[kRingMax / 64 + 1];
   __shared__ int stk[3 * kSortStack];
   __shared__ int s_flag, s_exact;
   // exact-order triggers: ties between eligible keys (found after each fast sort) and, in ring 0, an
@@ -425,7 +423,7 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
       key[t] = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)ind;
     }
     __syncthreads();
-    if (tid < 64) exact_introsort(key, nRng, cpos, rstart, stk, leafw, CurvLess{});
+    if (tid < 64) exact_introsort(key, nRng, cpos, rstart, stk, CurvLess{});
     __syncthreads();
     if (tid == 0) {
       if (sp == 4) d.phantom[b] = (int)(uint32_t)key[0];
@@ -617,52 +615,130 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
     vk[t] = (uint32_t)(i0 + i1 * mul1 + i2 * mul2);
   }
   __syncthreads();
-  // std::sort(index_vector) by voxel id alone (PCL 1.10 voxel_grid.hpp): equal ids keep the order
-  // libstdc++'s introsort leaves them in, and each centroid sums its points in that order.
-  for (int t = tid; t < L; t += nt) key[t] = ((uint64_t)vk[t] << 32) | (uint32_t)t;
-  __syncthreads();
-  if (c.dbg_phase <= 5) return;
-  // Lp = rstart, Rp = the (dead) voxel-id words
-  if (tid < 64) exact_introsort(key, L, rstart, reinterpret_cast<uint16_t*>(win_raw), stk, leafw, VoxLess{});
-  __syncthreads();
-  if (c.dbg_phase <= 6) return;
-  // voxel heads in sorted order; sorted position t = u * 256 + tid sits in slot u of a lane, so a
-  // wave's heads of one slot are consecutive voxels and their centroids are stored contiguously;
-  // output positions come from per-(slot, wave) ballot counts scanned in (slot, wave) = sorted order.
   __shared__ int scnt[kLp * 4 + 1];
   const int wv = tid >> 6, ln = lane_id();
   const unsigned long long ltm = (1ull << ln) - 1ull;
-  unsigned long long mH[kLp];
+  int V;
+  if (c.exact_vg) {
+    // LLSR_VOXEL_ORDER_PCL (llsr_set_voxel_order): std::sort(index_vector) by voxel id alone (PCL
+    // 1.10 voxel_grid.hpp): equal ids keep the order libstdc++'s introsort leaves them in, and each
+    // centroid sums its points in that order.
+    for (int t = tid; t < L; t += nt) key[t] = ((uint64_t)vk[t] << 32) | (uint32_t)t;
+    __syncthreads();
+    if (c.dbg_phase <= 5) return;
+    // Lp = rstart, Rp = the (dead) voxel-id words
+    // (dbg_phase 100: diagnostic re-launch without the depth limit, to time the heap-sort fallback)
+    if (tid < 64)
+      exact_introsort(key, L, rstart, reinterpret_cast<uint16_t*>(win_raw), stk, VoxLess{}, c.dbg_phase == 100 ? 1000 : -1);
+    __syncthreads();
+    if (c.dbg_phase <= 6) return;
+    // voxel heads in sorted order; sorted position t = u * 256 + tid sits in slot u of a lane, so a
+    // wave's heads of one slot are consecutive voxels and their centroids are stored contiguously;
+    // output positions come from per-(slot, wave) ballot counts scanned in (slot, wave) = sorted order.
+    unsigned long long mH[kLp];
 #pragma unroll
-  for (int u = 0; u < kLp; ++u) {
-    const int t = u * 256 + tid;
-    const bool head = t < L && (t == 0 || (key[t] >> 32) != (key[t - 1] >> 32));
-    mH[u] = __ballot(head);
-    if (ln == 0) scnt[u * 4 + wv] = (int)__popcll(mH[u]);
-  }
-  __syncthreads();
-  if (wv == 0) {  // exclusive scan of scnt[0 .. kLp*4) in place, total in scnt[kLp*4]
-    const int v = ln < kLp * 4 ? scnt[ln] : 0;
-    const int incl = wave_incl_scan_add(v);
-    if (ln < kLp * 4) scnt[ln] = incl - v;
-    if (ln == 63) scnt[kLp * 4] = incl;
-  }
-  __syncthreads();
-  const int V = scnt[kLp * 4];
-#pragma unroll
-  for (int u = 0; u < kLp; ++u) {
-    const int t = u * 256 + tid;
-    if (!((mH[u] >> ln) & 1ull)) continue;
-    const uint32_t vid = (uint32_t)(key[t] >> 32);
-    float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
-    int e = t;
-    for (; e < L && (uint32_t)(key[e] >> 32) == vid; ++e) {
-      const float4 p = lp[cpos[(uint32_t)key[e]]];
-      sx += p.x; sy += p.y; sz += p.z; si += p.w;
+    for (int u = 0; u < kLp; ++u) {
+      const int t = u * 256 + tid;
+      const bool head = t < L && (t == 0 || (key[t] >> 32) != (key[t - 1] >> 32));
+      mH[u] = __ballot(head);
+      if (ln == 0) scnt[u * 4 + wv] = (int)__popcll(mH[u]);
     }
-    const float nn = (float)(e - t);
-    const int vo = scnt[u * 4 + wv] + (int)__popcll(mH[u] & ltm);
-    out[vo] = make_float4(sx / nn, sy / nn, sz / nn, si / nn);
+    __syncthreads();
+    if (wv == 0) {  // exclusive scan of scnt[0 .. kLp*4) in place, total in scnt[kLp*4]
+      const int v = ln < kLp * 4 ? scnt[ln] : 0;
+      const int incl = wave_incl_scan_add(v);
+      if (ln < kLp * 4) scnt[ln] = incl - v;
+      if (ln == 63) scnt[kLp * 4] = incl;
+    }
+    __syncthreads();
+    V = scnt[kLp * 4];
+#pragma unroll
+    for (int u = 0; u < kLp; ++u) {
+      const int t = u * 256 + tid;
+      if (!((mH[u] >> ln) & 1ull)) continue;
+      const uint32_t vid = (uint32_t)(key[t] >> 32);
+      float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
+      int e = t;
+      for (; e < L && (uint32_t)(key[e] >> 32) == vid; ++e) {
+        const float4 p = lp[cpos[(uint32_t)key[e]]];
+        sx += p.x; sy += p.y; sz += p.z; si += p.w;
+      }
+      const float nn = (float)(e - t);
+      const int vo = scnt[u * 4 + wv] + (int)__popcll(mH[u] & ltm);
+      out[vo] = make_float4(sx / nn, sy / nn, sz / nn, si / nn);
+    }
+  } else {
+    // LLSR_VOXEL_ORDER_INPUT (default): runs of equal voxel id in ring order -> one sort key per
+    // run: (voxel id, run index), each voxel summed run by run in ring order. Position
+    // t = u * 256 + tid in slot u of a lane; run indices from per-(slot, wave) ballot counts scanned in
+    // (slot, wave) = ring order.
+    auto slot_scan = [&]() {  // exclusive scan of scnt[0 .. kLp*4) in place, total in scnt[kLp*4]
+      __syncthreads();
+      if (wv == 0) {
+        const int v = ln < kLp * 4 ? scnt[ln] : 0;
+        const int incl = wave_incl_scan_add(v);
+        if (ln < kLp * 4) scnt[ln] = incl - v;
+        if (ln == 63) scnt[kLp * 4] = incl;
+      }
+      __syncthreads();
+    };
+    unsigned long long mR[kLp];
+#pragma unroll
+    for (int u = 0; u < kLp; ++u) {
+      const int t = u * 256 + tid;
+      mR[u] = __ballot(t < L && (t == 0 || vk[t] != vk[t - 1]));
+      if (ln == 0) scnt[u * 4 + wv] = (int)__popcll(mR[u]);
+    }
+    slot_scan();
+    const int R = scnt[kLp * 4];
+#pragma unroll
+    for (int u = 0; u < kLp; ++u) {
+      if (!((mR[u] >> ln) & 1ull)) continue;
+      const int t = u * 256 + tid;
+      const int ro = scnt[u * 4 + wv] + (int)__popcll(mR[u] & ltm);
+      rstart[ro] = (uint16_t)t;
+      key[ro] = ((uint64_t)vk[t] << 32) | (uint32_t)ro;
+    }
+    if (tid == 0) rstart[R] = (uint16_t)L;
+    const int R2 = pow2_ceil(R);
+    for (int t = R + tid; t < R2; t += nt) key[t] = ~0ull;
+    __syncthreads();
+    if (c.dbg_phase <= 5) return;
+    bitonic_sort_u64(key, R2);
+    if (c.dbg_phase <= 6) return;
+    // voxels = groups of sorted runs with equal id; sum members in (run start, position) order.
+    // Sorted run t = u * 256 + tid sits in slot u of a lane, so a wave's voxel heads of one slot are
+    // consecutive voxels and their centroids are stored contiguously; output positions come from
+    // per-(slot, wave) ballot counts scanned in (slot, wave) = sorted order.
+    unsigned long long mH[kLp];
+#pragma unroll
+    for (int u = 0; u < kLp; ++u) {
+      const int t = u * 256 + tid;
+      const bool head = t < R && (t == 0 || (key[t] >> 32) != (key[t - 1] >> 32));
+      mH[u] = __ballot(head);
+      if (ln == 0) scnt[u * 4 + wv] = (int)__popcll(mH[u]);
+    }
+    slot_scan();
+    V = scnt[kLp * 4];
+#pragma unroll
+    for (int u = 0; u < kLp; ++u) {
+      const int t = u * 256 + tid;
+      if (!((mH[u] >> ln) & 1ull)) continue;
+      const uint32_t vid = (uint32_t)(key[t] >> 32);
+      float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
+      int cntp = 0;
+      for (int e = t; e < R && (uint32_t)(key[e] >> 32) == vid; ++e) {
+        const int run = (int)(uint32_t)key[e];
+        for (int q = rstart[run]; q < rstart[run + 1]; ++q) {
+          const float4 p = lp[cpos[q]];
+          sx += p.x; sy += p.y; sz += p.z; si += p.w;
+          ++cntp;
+        }
+      }
+      const float nn = (float)cntp;
+      const int vo = scnt[u * 4 + wv] + (int)__popcll(mH[u] & ltm);
+      out[vo] = make_float4(sx / nn, sy / nn, sz / nn, si / nn);
+    }
   }
   if (tid == 0) rc[2 * H + i] = V;
 }

@@ -82,26 +82,172 @@ __device__ void heap_sort_range(uint64_t* key, int f, int l, Lt lt) {
   }
 }
 constexpr int kSortStack = 64;
-// Executed by one full wave (64 lanes). Lp / Rp: n uint16 each; stk: 3 * kSortStack ints;
-// leaf: (n + 64) / 64 uint64 words. Returns nothing; key[0, n) ends up as std::sort leaves it.
-// depth0 < 0: the whole array (depth limit 2 * lg(n)); else a sub-range of a larger sort that
-// inherits the remaining depth limit of its parent range (llsr_map.hip's segmented VoxelGrid).
+
+// ---- ranges of at most 64 elements: the rest of their introsort in registers -----------------
+// Lane i holds element f + i. Partitions, the heap-sort fallback and the final insertion sort of
+// the range's leaves (an insertion sort with a strict comparator is a stable sort, so each leaf's
+// result is its stable sort, computed from ranks) all run on register values with ballots and
+// lane shuffles; only the load and the final store touch LDS.
+__device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
+  return ((uint64_t)hi << 32) | lo;
+}
+// position of the k-th (0-based) set bit of m, from bit 0; k < popcount(m)
+__device__ __forceinline__ int select_bit(uint64_t m, int k) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const uint64_t low = m & ((1ull << w) - 1ull);
+    const int c = __popcll(low);
+    if (k >= c) { k -= c; m >>= w; pos += w; }
+    else m = low;
+  }
+  return pos;
+}
+// libstdc++ heap sort of lanes [f, e) (all lanes execute; every index is wave-uniform)
 template <class Lt>
-__device__ void exact_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp, int* stk, uint64_t* leaf, Lt lt,
+__device__ void reg_heap_adjust(uint64_t& v, int f, int hole, int len, uint64_t val, Lt lt) {
+  const int l = lane_id();
+  const int top = hole;
+  int second = hole;
+  while (second < (len - 1) / 2) {
+    second = 2 * (second + 1);
+    if (lt(rdlane64(v, f + second), rdlane64(v, f + second - 1))) second--;
+    const uint64_t x = rdlane64(v, f + second);
+    if (l == f + hole) v = x;
+    hole = second;
+  }
+  if ((len & 1) == 0 && second == (len - 2) / 2) {
+    second = 2 * (second + 1);
+    const uint64_t x = rdlane64(v, f + second - 1);
+    if (l == f + hole) v = x;
+    hole = second - 1;
+  }
+  int parent = (hole - 1) / 2;
+  while (hole > top && lt(rdlane64(v, f + parent), val)) {
+    const uint64_t x = rdlane64(v, f + parent);
+    if (l == f + hole) v = x;
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  if (l == f + hole) v = val;
+}
+template <class Lt>
+__device__ void reg_heap_sort(uint64_t& v, int f, int e, Lt lt) {
+  const int l = lane_id();
+  const int len = e - f;
+  if (len >= 2)
+    for (int parent = (len - 2) / 2;; --parent) {
+      reg_heap_adjust(v, f, parent, len, rdlane64(v, f + parent), lt);
+      if (parent == 0) break;
+    }
+  for (int last = e; last - f > 1;) {
+    --last;
+    const uint64_t val = rdlane64(v, last);
+    const uint64_t top = rdlane64(v, f);
+    if (l == last) v = top;
+    reg_heap_adjust(v, f, 0, last - f, val, lt);
+  }
+}
+// key[f, f + n), n <= 64, remaining depth limit d: finished exactly as std::sort would.
+template <class Lt>
+__device__ void small_sort(uint64_t* key, int f, int n, int d, Lt lt) {
+  const int l = lane_id();
+  const unsigned long long ltm = (1ull << l) - 1ull;
+  const unsigned long long lem = l == 63 ? ~0ull : (2ull << l) - 1ull;  // bits <= l
+  uint64_t v = l < n ? key[f + l] : 0ull;
+  int dep = d;                  // depth limit of the range starting at this lane
+  unsigned long long bnd = 1ull, leafm = 0ull;
+  int cur = 0;
+  while (cur < n) {
+    const unsigned long long above = cur == 63 ? 0ull : bnd & ~((2ull << cur) - 1ull);
+    const int e = above ? __ffsll((long long)above) - 1 : n;
+    const int dd = __builtin_amdgcn_readlane(dep, cur);
+    if (e - cur <= 16) { leafm |= 1ull << cur; cur = e; continue; }
+    if (dd == 0) { reg_heap_sort(v, cur, e, lt); leafm |= 1ull << cur; cur = e; continue; }
+    // __move_median_to_first(first, first + 1, mid, last - 1)
+    const int a = cur + 1, b = cur + (e - cur) / 2, c = e - 1;
+    const uint64_t va = rdlane64(v, a), vb = rdlane64(v, b), vc = rdlane64(v, c);
+    int mi;
+    uint64_t vm;
+    if (lt(va, vb)) {
+      if (lt(vb, vc)) { mi = b; vm = vb; }
+      else if (lt(va, vc)) { mi = c; vm = vc; }
+      else { mi = a; vm = va; }
+    } else if (lt(va, vc)) { mi = a; vm = va; }
+    else if (lt(vb, vc)) { mi = c; vm = vc; }
+    else { mi = b; vm = vb; }
+    const uint64_t v0 = rdlane64(v, cur);
+    if (l == cur) v = vm;
+    else if (l == mi) v = v0;
+    const uint64_t P = vm;
+    // __unguarded_partition: stop lists L (ascending, (cur, e)) and R (descending, [cur, e))
+    const unsigned long long mL = __ballot(l > cur && l < e && !lt(v, P));
+    const unsigned long long mR = __ballot(l >= cur && l < e && !lt(P, v));
+    const int nL = __popcll(mL), nR = __popcll(mR), nm = nL < nR ? nL : nR;
+    const int Lk = l < nL ? select_bit(mL, l) : 64;
+    const int Rk = l < nR ? select_bit(mR, nR - 1 - l) : -1;
+    const int ks = __popcll(__ballot(l < nm && Lk < Rk));  // monotone: lanes 0 .. ks-1
+    const int Lks = __builtin_amdgcn_readlane(Lk, ks < 63 ? ks : 63);
+    const int Rks = __builtin_amdgcn_readlane(Rk, ks > 0 ? ks - 1 : 0);
+    const int cut = (ks > 0 && (ks >= nL || Lks >= Rks)) ? Rks : Lks;
+    // pairs k < ks swap L[k] <-> R[k]
+    const int kL = __popcll(mL & ltm);
+    const int kR = l == 63 ? 0 : __popcll(mR >> (l + 1));
+    const int toR = __shfl(Rk, kL & 63), toL = __shfl(Lk, kR & 63);
+    int src = l;
+    if (((mL >> l) & 1ull) && kL < ks) src = toR;
+    else if (((mR >> l) & 1ull) && kR < ks) src = toL;
+    v = shfl64(v, src);
+    if (l == cur || l == cut) dep = dd - 1;
+    bnd |= 1ull << cut;
+  }
+  // each leaf's insertion sort = its stable sort
+  const int s0 = 63 - __clzll((long long)(leafm & lem));
+  const unsigned long long up = leafm & ~lem;
+  const int t0 = up ? __ffsll((long long)up) - 1 : n;
+  int len = l < n ? t0 - s0 : 0;
+  int mx = len;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { const int y = __shfl_xor(mx, o); mx = y > mx ? y : mx; }
+  int rank = 0;
+  for (int q = 0; q < mx; ++q) {
+    const int sq = s0 + q;
+    const uint64_t w = shfl64(v, sq < 64 ? sq : 63);
+    if (q < len && (lt(w, v) || (!lt(v, w) && sq < l))) ++rank;
+  }
+  if (l < n) key[f + s0 + rank] = v;
+  wave_sync_lds();
+}
+
+// Executed by one full wave (64 lanes). Lp / Rp: n uint16 each; stk: 3 * kSortStack ints.
+// key[0, n) ends up as std::sort leaves it. depth0 < 0: the whole array (depth limit 2 * lg(n));
+// else a sub-range of a larger sort that inherits the remaining depth limit of its parent range
+// (llsr_map.hip's segmented VoxelGrid). Ranges above 64 elements are partitioned in LDS; each range
+// of at most 64 is finished in registers (small_sort).
+template <class Lt>
+__device__ void exact_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp, int* stk, Lt lt,
                                 int depth0 = -1) {
   const int l = lane_id();
   const unsigned long long ltm = (1ull << l) - 1ull;
-  for (int w = l; w <= (n >> 6); w += 64) leaf[w] = 0ull;
   wave_sync_lds();
   if (n <= 1) return;
   const int lg = 31 - __clz(n);
   int sp = 0;  // stack depth (wave-uniform)
   int rf = 0, rl = n, rd = depth0 < 0 ? 2 * lg : depth0;
   while (true) {
-    while (rl - rf > 16) {
+    bool heaped = false;
+    while (rl - rf > 64) {
       if (rd == 0) {
         if (l == 0) heap_sort_range(key, rf, rl, lt);
         wave_sync_lds();
+        heaped = true;
         break;
       }
       rd--;
@@ -150,36 +296,13 @@ __device__ void exact_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp
       ++sp;
       rl = cut;
     }
-    if (l == 0) leaf[rf >> 6] |= 1ull << (rf & 63);
+    if (!heaped && rl - rf > 1) small_sort(key, rf, rl - rf, rd, lt);
     wave_sync_lds();
     if (sp == 0) break;
     --sp;
     rf = stk[3 * sp]; rl = stk[3 * sp + 1]; rd = stk[3 * sp + 2];
   }
-  // one insertion sort per leaf block: lane w takes the leaves starting in word w, w + 64, ...
-  const int nw = (n + 63) >> 6;
-  for (int w = l; w < nw; w += 64) {
-    uint64_t bits = leaf[w];
-    while (bits) {
-      const int s0 = (w << 6) + __ffsll((long long)bits) - 1;
-      bits &= bits - 1;
-      int e = n;  // next leaf start after s0
-      if (bits) {
-        e = (w << 6) + __ffsll((long long)bits) - 1;
-      } else {
-        for (int w2 = w + 1; w2 < nw; ++w2)
-          if (leaf[w2]) { e = (w2 << 6) + __ffsll((long long)leaf[w2]) - 1; break; }
-      }
-      for (int i = s0 + 1; i < e; ++i) {
-        const uint64_t val = key[i];
-        int j = i;
-        while (j > s0 && lt(val, key[j - 1])) { key[j] = key[j - 1]; --j; }
-        key[j] = val;
-      }
-    }
-  }
   wave_sync_lds();
 }
-
 
 }  // namespace llsr

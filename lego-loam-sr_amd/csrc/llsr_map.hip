@@ -280,12 +280,11 @@ __global__ __launch_bounds__(64) void k_is_leaf(unsigned long long* kk, const Is
   __shared__ uint64_t key[kIsLeaf];
   __shared__ uint16_t Lp[kIsLeaf], Rp[kIsLeaf];
   __shared__ int stk[3 * kSortStack];
-  __shared__ uint64_t leafw[kIsLeaf / 64 + 1];
   const IsRange r = leaves[blockIdx.x];
   const int n = (int)(r.l - r.f);
   for (int k = threadIdx.x; k < n; k += 64) key[k] = kk[r.f + k];
   wave_sync_lds();
-  exact_introsort(key, n, Lp, Rp, stk, leafw, VoxLess{}, r.d);
+  exact_introsort(key, n, Lp, Rp, stk, VoxLess{}, r.d);
   for (int k = threadIdx.x; k < n; k += 64) kk[r.f + k] = key[k];
 }
 

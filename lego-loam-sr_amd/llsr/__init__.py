@@ -42,7 +42,7 @@ EXPORTS = [
     "llsr_map_add_keyframe", "llsr_map_num_keyframes", "llsr_map_extract", "llsr_map_keyframe_ids",
     "llsr_decode_pointcloud2", "llsr_kitti_count", "llsr_kitti_read", "llsr_kitti_load",
     "llsr_mapping_init", "llsr_mapping_batch", "llsr_mapping_fetch", "llsr_mapping_keyposes", "llsr_mapping_reset",
-    "llsr_mapping_associate",
+    "llsr_mapping_associate", "llsr_set_voxel_order",
 ]
 
 
@@ -111,6 +111,7 @@ def lib():
         L.llsr_mapping_keyposes.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]
         L.llsr_mapping_reset.argtypes = [C.c_void_p]
         L.llsr_mapping_associate.argtypes = [C.c_void_p] * 6
+        L.llsr_set_voxel_order.argtypes = [C.c_void_p, C.c_int32]
         L.llsr_decode_pointcloud2.argtypes = [C.POINTER(_abi.Pc2Layout), C.c_void_p, C.c_void_p, C.c_int32,
                                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.llsr_kitti_count.argtypes = [C.c_char_p]
@@ -168,6 +169,10 @@ class Pipeline:
 
     def reset(self):
         self._check(lib().llsr_reset_state(self._h), "llsr_reset_state")
+
+    def set_voxel_order(self, order: int):
+        """_abi.LLSR_VOXEL_ORDER_INPUT (default) or LLSR_VOXEL_ORDER_PCL (the less-flat VoxelGrid)."""
+        self._check(lib().llsr_set_voxel_order(self._h, order), "llsr_set_voxel_order")
 
     def process_scan(self, xyzi: np.ndarray) -> dict:
         xyzi = np.ascontiguousarray(xyzi, dtype=np.float32).reshape(-1, 4)

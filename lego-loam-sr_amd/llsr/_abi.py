@@ -10,6 +10,8 @@ LLSR_LIDAR_VLP16 = 0
 LLSR_LIDAR_HDL64E = 2
 LLSR_MODE_FAITHFUL = 0
 LLSR_MODE_LM_APPLIED = 1
+LLSR_VOXEL_ORDER_INPUT = 0
+LLSR_VOXEL_ORDER_PCL = 1
 NE_WORDS = 32  # LLSR_NE_WORDS: int64 words per problem exchanged by llsr_scan2map_shard_*
 
 

@@ -24,6 +24,10 @@ void oracle_reset(oracle_state* s);
 /* One scan through ImageProjection::cloudHandler (IP:189-222) and the FeatureAssociation
  * feature stage (FA:2766-2775). Same output layout/semantics as llsr_process_scan. */
 int32_t oracle_process_scan(oracle_state* s, const float* xyzi, int32_t n, llsr_scan_out* out);
+/* The less-flat VoxelGrid's summation order (FA:1268-1270): pcl != 0 follows PCL (std::sort's
+ * order of equal voxel ids, LLSR_VOXEL_ORDER_PCL), 0 sums in input order (LLSR_VOXEL_ORDER_INPUT,
+ * the default of both sides). */
+void oracle_set_voxel_order(oracle_state* s, int32_t pcl);
 /* Per-stage wall time of the last oracle_process_scan (ms): IP, FA-features. */
 void oracle_stage_ms(const oracle_state* s, double* ip_ms, double* fa_ms);
 /* RANSAC with a caller seed (seed 12345 = PCL default) over the last scan's near-ground cloud;

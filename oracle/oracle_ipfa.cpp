@@ -132,9 +132,9 @@ struct PlaneRansac {
 };
 
 // PCL 1.10 VoxelGrid<PointXYZI>::applyFilter (FA:1268-1270), restated in oracle_voxel.h.
-void voxel_grid(const std::vector<P4>& in, float leaf, std::vector<P4>& out) {
+void voxel_grid(const std::vector<P4>& in, float leaf, std::vector<P4>& out, bool stable) {
   std::vector<float> o;
-  oracle_voxel::voxel_grid(reinterpret_cast<const float*>(in.data()), in.size(), leaf, o);
+  oracle_voxel::voxel_grid(reinterpret_cast<const float*>(in.data()), in.size(), leaf, o, stable);
   out.resize(o.size() / 4);
   std::memcpy(out.data(), o.data(), o.size() * sizeof(float));
 }
@@ -143,6 +143,9 @@ void voxel_grid(const std::vector<P4>& in, float leaf, std::vector<P4>& out) {
 
 // ------------------------------------------------------------------------------------------
 struct oracle_state {
+  // true: the less-flat VoxelGrid sums each voxel in input order (the device's default,
+  // LLSR_VOXEL_ORDER_INPUT); false: in std::sort's order, as PCL (LLSR_VOXEL_ORDER_PCL)
+  bool vg_stable = true;
   llsr_config cfg;
   int H, W, HW;
   // IP derived constants (IP:117-121, 849)
@@ -231,6 +234,7 @@ extern "C" void oracle_std_sort_by_value(const float* vals, int32_t n, int32_t* 
 
 // cloudSmoothness[4].ind, the entry the next frame's ring-0 sort starts from (test hook)
 extern "C" int32_t oracle_phantom_index(const oracle_state* s) { return (int32_t)s->smooth[4].second; }
+extern "C" void oracle_set_voxel_order(oracle_state* s, int32_t pcl) { s->vg_stable = pcl == 0; }
 
 extern "C" int32_t oracle_ransac_inliers(oracle_state* s, uint32_t seed, int32_t* out, int32_t cap) {
   PlaneRansac rs(s->near, seed);
@@ -578,7 +582,7 @@ extern "C" int32_t oracle_process_scan(oracle_state* s, const float* xyzi, int32
     std::vector<P4> ringLess, ringDS;
     for (int k = sp; k <= ep; ++k)
       if (s->clabel[k] <= 0) ringLess.push_back(pc[k]);
-    voxel_grid(ringLess, 0.2f, ringDS);
+    voxel_grid(ringLess, 0.2f, ringDS, s->vg_stable);
     lessFlat.insert(lessFlat.end(), ringDS.begin(), ringDS.end());
   }
   // ---- DBSCAN_EdgeFeature (FA:1318-1387) ----

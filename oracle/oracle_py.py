@@ -44,6 +44,7 @@ def lib():
         L.oracle_ransac_inliers.restype = C.c_int32
         L.oracle_ransac_inliers.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int32]
         L.oracle_std_sort_by_value.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
+        L.oracle_set_voxel_order.argtypes = [C.c_void_p, C.c_int32]
         L.oracle_phantom_index.restype = C.c_int32
         L.oracle_phantom_index.argtypes = [C.c_void_p]
         for f in ("oracle_eig3", "oracle_eig6"):
@@ -122,11 +123,12 @@ def ref_lib():
 class Oracle:
     """One reference pipeline (IP + FA feature stage) with its own carry-over state."""
 
-    def __init__(self, cfg: _abi.Config):
+    def __init__(self, cfg: _abi.Config, pcl_voxel_order: bool = False):
         self.cfg = cfg
         self._h = lib().oracle_create(C.byref(cfg))
         if not self._h:
             raise ValueError("oracle_create rejected the config")
+        lib().oracle_set_voxel_order(self._h, 1 if pcl_voxel_order else 0)
         self.out = _abi.OutBuffers(cfg.num_vertical_scans, cfg.num_horizontal_scans)
 
     def __del__(self):
@@ -373,9 +375,9 @@ class OracleOdometry:
     feature stage, then updateTransformation against the last clouds, integrateTransformation and
     publishCloudsLast's TransformToEnd (first scan: checkSystemInitialization)."""
 
-    def __init__(self, cfg: _abi.Config):
+    def __init__(self, cfg: _abi.Config, pcl_voxel_order: bool = False):
         self.cfg = cfg
-        self.ora = Oracle(cfg)
+        self.ora = Oracle(cfg, pcl_voxel_order)
         self.shadow = shadow_points()
         self.tcur = np.zeros(6, np.float32)
         self.tsum = np.zeros(6, np.float32)
@@ -519,9 +521,9 @@ class OracleMapping:
     device does; `stable` = True would sum each voxel in input order instead (diagnostics)."""
 
     def __init__(self, cfg: _abi.Config, mo_mode: int, radius=50.0, keypose_leaf=1.0, corner_leaf=0.2,
-                 surf_leaf=0.4, outlier_leaf=0.4, stable: bool = False):
+                 surf_leaf=0.4, outlier_leaf=0.4, stable: bool = False, pcl_voxel_order: bool = False):
         import copy
-        self.odo = OracleOdometry(cfg)
+        self.odo = OracleOdometry(cfg, pcl_voxel_order)
         self.cfg_mo = copy.copy(cfg)
         self.cfg_mo.mode = mo_mode
         self.map = OracleMap(radius, keypose_leaf, corner_leaf, surf_leaf, stable=stable)

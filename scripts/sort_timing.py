@@ -1,0 +1,44 @@
+"""Diagnostics: device time of one wave's exact introsort (llsr_isort.h) on ring-like inputs."""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "lego-loam-sr_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import llsr  # noqa: E402
+import oracle_py  # noqa: E402
+from llsr import _abi, synth  # noqa: E402
+
+f = llsr.lib().llsr_debug_exact_sort_ms
+f.restype, f.argtypes = C.c_float, [C.c_void_p, C.c_int32, C.c_int32]
+
+
+def t(a):
+    a = np.ascontiguousarray(a, np.float32)
+    return round(float(f(a.ctypes.data, len(a), 20)) * 1e3, 1)  # us
+
+
+cfg = _abi.config_for("vlp16")
+o = oracle_py.Oracle(cfg)
+r = o.process(synth.make_scan(5, "vlp16"))
+loam, sr, er, lab = r["loam_xyzi"], r["start_ring_index"], r["end_ring_index"], r["label"]
+res = {}
+for ring in range(0, 16, 3):
+    idx = np.arange(sr[ring], er[ring] + 1)
+    p = loam[idx[lab[idx] <= 0]]
+    inv = np.float32(5.0)
+    mn = p[:, :3].min(0)
+    mx = p[:, :3].max(0)
+    minb = np.floor(mn * inv).astype(np.int64)
+    div = np.floor(mx * inv).astype(np.int64) - minb + 1
+    i = (np.floor(p[:, :3] * inv) - minb.astype(np.float32)).astype(np.int64)
+    v = (i[:, 0] + i[:, 1] * div[0] + i[:, 2] * div[0] * div[1]).astype(np.float32)
+    n = len(v)
+    rng = np.random.default_rng(ring)
+    res[f"ring{ring}"] = {"n": n, "voxel_ids_us": t(v), "random_us": t(rng.random(n)), "sorted_us": t(np.arange(n)),
+                          "few_values_us": t(rng.integers(0, 8, n)), "all_equal_us": t(np.zeros(n))}
+print(json.dumps(res))

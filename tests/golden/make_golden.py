@@ -24,7 +24,7 @@ SEEDS = (1, 2)
 
 def main():
     cfg = _abi.config_for("vlp16")
-    ora = oracle_py.Oracle(cfg)
+    ora = oracle_py.Oracle(cfg, pcl_voxel_order=True)  # PCL's VoxelGrid order: the reference statement
     for k, seed in enumerate(SEEDS):
         pts = synth.make_scan(seed, "vlp16")
         r = ora.process(pts)

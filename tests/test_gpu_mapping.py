@@ -7,8 +7,9 @@ the query and local-map sizes, the LM report, transformSum / TobeMapped / BefMap
 and at the end the key poses (cloudKeyPoses6D).
 
 Bar: bit-exact end to end — counts, LM reports, every pose and the key poses equal the oracle's.
-Every VoxelGrid on both sides sums a voxel in the order libstdc++'s std::sort leaves PCL's
-index_vector, and both LMs sum their normal equations in Eigen's order.
+MapOptimization's VoxelGrids on both sides sum a voxel in the order libstdc++'s std::sort leaves
+PCL's index_vector, the feature stage's less-flat VoxelGrid in the handle's order (input order by
+default, LLSR_VOXEL_ORDER_PCL in one test), and both LMs sum their normal equations in Eigen's order.
 """
 import numpy as np
 import pytest
@@ -20,7 +21,7 @@ pytestmark = pytest.mark.gpu
 POSES = ("transform_sum", "transform_tobe_mapped", "transform_bef_mapped", "transform_aft_mapped")
 
 
-def _drive(mode, seeds, frames, iters=None):
+def _drive(mode, seeds, frames, iters=None, pcl=False):
     import torch
     cfg = default_config("vlp16")
     cfg.mode = _abi.LLSR_MODE_LM_APPLIED
@@ -29,7 +30,9 @@ def _drive(mode, seeds, frames, iters=None):
     H, W = cfg.num_vertical_scans, cfg.num_horizontal_scans
     pipe = Pipeline(cfg, max_batch=len(seeds), max_points=H * W)
     pipe.mapping_init(mode)
-    oras = [oracle_py.OracleMapping(cfg, mode) for _ in seeds]
+    if pcl:
+        pipe.set_voxel_order(_abi.LLSR_VOXEL_ORDER_PCL)
+    oras = [oracle_py.OracleMapping(cfg, mode, pcl_voxel_order=pcl) for _ in seeds]
     errs = []
     for k in range(frames):
         scans = [synth.make_scan(s0 + k, "vlp16") for s0 in seeds]
@@ -78,6 +81,11 @@ def _drive(mode, seeds, frames, iters=None):
 
 def test_mapping_chain_lm_applied(require_gpu):
     errs = _drive(_abi.LLSR_MODE_LM_APPLIED, [1, 65, 130], 6)
+    assert not errs, "\n".join(errs)
+
+
+def test_mapping_chain_pcl_voxel_order(require_gpu):
+    errs = _drive(_abi.LLSR_MODE_LM_APPLIED, [2, 140], 5, pcl=True)
     assert not errs, "\n".join(errs)
 
 

@@ -2,22 +2,26 @@
 
 Bit-exact for labels / indices / clouds (see _compare.py for the bar). Sequences of scans run
 through one handle so the FeatureAssociation carry-over state (picked / cloudLabel arrays,
-phantom smoothness entry) is exercised exactly as in the reference's long-running node.
+phantom smoothness entry) is exercised exactly as in the reference's long-running node. Both
+less-flat VoxelGrid orders: the default (input order) against the oracle's input-order statement,
+LLSR_VOXEL_ORDER_PCL against its PCL (std::sort order) statement.
 """
 import numpy as np
 import pytest
 
 from _compare import compare
-from llsr import Pipeline, default_config, synth
+from llsr import Pipeline, _abi, default_config, synth
 import oracle_py
 
 pytestmark = pytest.mark.gpu
 
 
-def _run_pair(lidar, horizontal, seeds):
+def _run_pair(lidar, horizontal, seeds, pcl=False):
     cfg = default_config(lidar, horizontal)
     pipe = Pipeline(cfg, max_points=2 * cfg.num_vertical_scans * cfg.num_horizontal_scans)
-    ora = oracle_py.Oracle(cfg)
+    if pcl:
+        pipe.set_voxel_order(_abi.LLSR_VOXEL_ORDER_PCL)
+    ora = oracle_py.Oracle(cfg, pcl_voxel_order=pcl)
     failures = []
     for s in seeds:
         pts = synth.make_scan(s, lidar)
@@ -33,6 +37,32 @@ def _run_pair(lidar, horizontal, seeds):
 def test_vlp16_sequence_bit_exact(require_gpu):
     failures = _run_pair("vlp16", None, [1, 2, 3, 70, 71])
     assert not failures, "\n".join(f"seed {s}:\n  " + "\n  ".join(e) for s, e in failures)
+
+
+def test_pcl_voxel_order_bit_exact(require_gpu):
+    for lidar, hz, seeds in (("vlp16", None, [1, 2, 70]), ("hdl64e", 2048, [5])):
+        failures = _run_pair(lidar, hz, seeds, pcl=True)
+        assert not failures, "\n".join(f"{lidar} seed {s}:\n  " + "\n  ".join(e) for s, e in failures)
+
+
+def test_voxel_orders_differ_only_in_centroid_bits(require_gpu):
+    """The two orders give the same voxels in the same order; centroids differ in the last bits at most."""
+    cfg = default_config("vlp16")
+    a = Pipeline(cfg, max_points=40000)
+    b = Pipeline(cfg, max_points=40000)
+    b.set_voxel_order(_abi.LLSR_VOXEL_ORDER_PCL)
+    diff = 0
+    for s in (1, 2, 3):
+        pts = synth.make_scan(s, "vlp16")
+        ga, gb = a.process_scan(pts), b.process_scan(pts)
+        assert ga["less_flat_xyzi"].shape == gb["less_flat_xyzi"].shape
+        np.testing.assert_allclose(ga["less_flat_xyzi"], gb["less_flat_xyzi"], rtol=1e-6, atol=1e-6)
+        diff += int((ga["less_flat_xyzi"] != gb["less_flat_xyzi"]).any(axis=1).sum())
+        for k in ("less_sharp_ind", "sharp_ind", "flat_ind", "seg_xyzi"):
+            assert np.array_equal(ga[k], gb[k]), k
+    assert diff > 0, "the scenes should hold voxels of three or more points whose sums depend on the order"
+    a.close()
+    b.close()
 
 
 def test_hdl64e_bit_exact(require_gpu):
@@ -82,3 +112,24 @@ def test_edge_cases(require_gpu, case):
     errs = compare(g, o)
     pipe.close()
     assert not errs, f"{case}:\n  " + "\n  ".join(errs)
+
+
+def test_golden_fixtures_pcl_order(require_gpu):
+    """The device in LLSR_VOXEL_ORDER_PCL reproduces the committed golden fixtures (the reference
+    statement, tests/golden/make_golden.py) bit for bit, through one handle as the fixtures were made."""
+    import os
+    golden = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    cfg = default_config("vlp16")
+    pipe = Pipeline(cfg, max_points=40000)
+    pipe.set_voxel_order(_abi.LLSR_VOXEL_ORDER_PCL)
+    for k in range(2):
+        z = np.load(os.path.join(golden, f"vlp16_frame{k}.npz"))
+        g = pipe.process_scan(z["input"])
+        assert [g[c] for c in _abi.COUNTS] == z["counts"].tolist()
+        assert np.array_equal(g["orientation"], z["orientation"])
+        for name, *_ in _abi.ARRAYS:
+            a, b = np.asarray(g[name]), z[f"out_{name}"]
+            if a.dtype == np.float32:
+                a, b = a.view(np.uint32), b.view(np.uint32)
+            assert np.array_equal(a, b), (k, name)
+    pipe.close()

@@ -19,7 +19,8 @@ def vlp_cfg():
 
 
 def test_golden_fixtures_reproduce(vlp_cfg):
-    ora = oracle_py.Oracle(vlp_cfg)
+    # the fixtures hold the reference statement: PCL's VoxelGrid order (tests/golden/make_golden.py)
+    ora = oracle_py.Oracle(vlp_cfg, pcl_voxel_order=True)
     for k in range(2):
         z = np.load(os.path.join(GOLDEN, f"vlp16_frame{k}.npz"))
         regen = synth.make_scan(int(z["seed"]), "vlp16")
