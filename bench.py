@@ -6,7 +6,7 @@ feature stage), labels / feature indices bit-exact vs the CPU path. A "step" is 
 hot path over one batch of B scans per GPU that is already resident in HBM.
 
 The same JSON line carries a second measured leg, "scan2map" (BASELINE.json configs[2]): batches
-of P scan-to-map problems (MapOptimization::scan2MapOptimization) against the ~76k-point local
+of P scan-to-map problems (MapOptimization::scan2MapOptimization) against the ~100k-point local
 map of tests/golden/mo_map_vlp16.npz, in lm_applied and faithful (200-iteration) mode, with the
 pose delta against the CPU restatement and its own CPU baseline.
 
@@ -48,7 +48,7 @@ def kernel_bytes(name: str, c: dict, HW: int) -> float:
         "k_ground_elev_ransac": 2 * HW + 16 * N + 16 * K * (c["R"] + 2),
         "k_label": 9 * HW,
         "k_segment": 5 * HW + 53 * S + 9 * (HW - S),
-        "k_fa_points": 62 * S,
+        "k_fa_points": 46 * S,  # adjustDistortion + curvature: seg xyzi/range/col in, loam/curv/picked/label out
         "k_select_ring": 13 * S + 16 * Lc + 16 * L + 8 * (M + F),
         "k_fa_concat": 8 * (M + F) + 32 * L + 40 * M,
         "k_dbscan_adj": 20 * M + c.get("M2", 0) / 8,
@@ -86,13 +86,13 @@ def s2m_bytes_per_iteration(Qc: int, Qs: int, blocks: int) -> float:
 
 
 def scan2map_leg(dev, mode_name: str, P: int, steps: int, warmup: int, dist, run_cpu: bool,
-                 cpu_seconds: float) -> dict:
+                 cpu_seconds: float, fixture: str = "mo_map_vlp16.npz") -> dict:
     """Config 3: P independent scan-to-map problems per step; each problem carries its own copy of
     the local map (its kd-tree/grid is rebuilt every step, as MO rebuilds it every scan,
     MO:1575-1576), one of the fixture's query scans and its own seeded start pose."""
     import torch
     from llsr import Pipeline, _abi, default_config
-    z = np.load(os.path.join(REPO, "tests", "golden", "mo_map_vlp16.npz"))
+    z = np.load(os.path.join(REPO, "tests", "golden", fixture))
     nq = int(z["n_queries"])
     mode = {"lm_applied": _abi.LLSR_MODE_LM_APPLIED, "faithful": _abi.LLSR_MODE_FAITHFUL}[mode_name]
     cfg = default_config("vlp16")
@@ -276,7 +276,7 @@ def scan2map_allreduce_leg(dev, P: int, steps: int, warmup: int, dist, check: bo
     ctx.__exit__(None, None, None)
     out = {"workload": f"configs[4]: {P} scans per step, each scan's scan-to-map correspondences split over "
                        "all ranks, one all-reduce of the [P][32] int64 normal equations per LM iteration "
-                       "(lm_applied, ~76k-point local map)",
+                       "(lm_applied, ~100k-point local map)",
            "value": round(P * steps / el, 1), "unit": "scans/s", "scaling": "strong",
            "scans_per_step": P, "steps": steps, "ms_per_step": round(el / steps * 1e3, 3),
            "lm_iterations_per_step": float(np.mean(iters[warmup:] if len(iters) > warmup else iters)),
@@ -651,6 +651,7 @@ def main():
     ap.add_argument("--s2m-problems", type=int, default=256, help="scan-to-map problems per GPU per step")
     ap.add_argument("--s2m-steps", type=int, default=5)
     ap.add_argument("--s2m-modes", default="lm_applied,faithful", help="comma list; empty = skip the leg")
+    ap.add_argument("--s2m-fixture", default="mo_map_vlp16.npz", help="tests/golden map fixture of the leg")
     ap.add_argument("--odo", default="hdl64e:512,vlp16:1024",
                     help="odometry legs lidar:sequences_per_gpu, comma list (empty = skip)")
     ap.add_argument("--map-keyframes", type=int, default=200,
@@ -737,9 +738,16 @@ def main():
     csum["M2"] = float((cnt[:, 3].astype(np.float64) ** 2).sum())  # DBSCAN pair count
     HWB = float(H * W * B)
     per = {k: kernel_bytes(k, csum, HWB) for k in ktimes}
-    if H <= 16 and H * W <= 32768:  # fused projection kernel (H*W fits LDS): one launch does both
+    fused = H <= 16 and H * W <= 32768
+    if fused:  # fused projection kernel (H*W fits LDS): one launch does both
         per["k_project"] += per["k_gather_column"]
         per["k_gather_column"] = 0.0
+    # SURVEY.md 8(d) B_pc: 20 N + 24 HW for the projection (each input point read once and its index
+    # scattered; range, XYZI and cell->point index written per cell) + 29 S for the curvature; the
+    # fused kernel's other outputs (raw intensity 4 B, ground byte 1 B per cell) are credited too.
+    # Re-reads (the winners' points gathered again) are not algorithmic: they show up in `traffic`.
+    bpc_proj = 20 * csum["N"] + (24 + 4 + 1) * HWB
+    bpc_curv = 29 * csum["S"]
     dom = max((k for k in ktimes if k != "init"), key=lambda k: ktimes[k])
     total_scans = B * args.steps * world
     value = total_scans / el
@@ -765,17 +773,32 @@ def main():
         rec = tjson.get("kernels", {}).get(kname)
         return rec["hbm_bytes"] / tjson["batch"] * B if rec and tjson.get("batch") else None
 
-    def roofline(kname):
-        a = per[kname] / (ktimes[kname] * 1e-3) / 1e9
-        return {"bound": "hbm", "kernel": kname, "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(a / HBM_PEAK_GBS, 4), "traffic": traffic_of(kname),
-                "algorithmic_bytes_per_launch": per[kname], "avg_launch_ms": round(ktimes[kname], 4)}
+    def roofline(kname, nbytes=None, ms=None, traffic=None, note=None):
+        nbytes = per[kname] if nbytes is None else nbytes
+        ms = ktimes[kname] if ms is None else ms
+        a = nbytes / (ms * 1e-3) / 1e9
+        out = {"bound": "hbm", "kernel": kname, "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": round(a / HBM_PEAK_GBS, 4), "traffic": traffic_of(kname) if traffic is None else traffic,
+               "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": round(ms, 4)}
+        if note:
+            out["note"] = note
+        return out
+
+    proj_ms = ktimes["k_project"] + (0.0 if fused else ktimes["k_gather_column"])
+    tp = traffic_of("k_project")
+    roof_proj = roofline("k_project", bpc_proj, proj_ms, note="B_pc projection part: 20 N + 24 HW (+ 5 HW "
+                         "raw intensity and ground outputs); traffic = PMC bytes incl. the winners' re-read")
+    tc = traffic_of("k_fa_points")
+    roof_pc = roofline("k_project+k_fa_points", bpc_proj + bpc_curv, proj_ms + ktimes["k_fa_points"],
+                       traffic=(tp + tc) if (tp is not None and tc is not None) else None,
+                       note="north_star's projection+curvature figure: SURVEY.md 8(d) B_pc = 20 N + 24 HW + 29 S "
+                            "over the two kernels' time")
 
     s2m = {}
     for mode_name in [m for m in args.s2m_modes.split(",") if m]:
         s2m[mode_name] = scan2map_leg(dev, mode_name, args.s2m_problems, args.s2m_steps, 1, dist,
                                       rank == 0 and not args.no_cpu and world == 1,
-                                      min(args.cpu_seconds, 12.0))
+                                      min(args.cpu_seconds, 12.0), args.s2m_fixture)
 
     odo = {}
     for spec in [x for x in args.odo.split(",") if x]:
@@ -822,7 +845,8 @@ def main():
                        "parallelism": f"scan-sharded x{world}"},
             "roofline": roofline(dom),
             # north_star's kernel: the (fused) projection + range image + column ground pass
-            "roofline_projection": roofline("k_project"),
+            "roofline_projection": roof_proj,
+            "roofline_projection_curvature": roof_pc,
             "kernels_ms_per_step": {k: round(v, 4) for k, v in ktimes.items()},
             "pipeline_algorithmic_GBs": round(sum(per.values()) / (sum(ktimes.values()) * 1e-3) / 1e9, 1),
             "per_scan_mean": {k: round(v / B, 1) for k, v in csum.items() if k not in ("R", "M2")},

@@ -6,6 +6,7 @@
 #include <cfloat>
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -79,7 +80,7 @@ struct llsr_handle {
   long long kbatches = 0;
   // scan-to-map (llsr_scan2map_*): buffers sized by llsr_scan2map_reserve
   struct {
-    int P = 0, qc = 0, qs = 0, mc = 0, ms = 0, log2T_c = 0, log2T_s = 0, blocks_c = 0, blocks = 0, red_blocks = 0;
+    int P = 0, qc = 0, qs = 0, mc = 0, ms = 0, log2T_c = 0, log2T_s = 0, blocks_c = 0, blocks = 0;
     void* pool = nullptr;
     S2MArgs a{};
     int* host_flags = nullptr;   // pinned: n_active, error
@@ -716,7 +717,7 @@ extern "C" int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t P, int32_t mc, 
                                          int32_t qs) {
   if (!h) return LLSR_EINVAL;
   if (P < 1 || mc < 0 || ms < 0 || qc < 0 || qs < 0 || mc > (1 << 26) || ms > (1 << 26) ||
-      qc > (1 << 20) || qs > (1 << 20))  // k_s2m_reduce keeps the per-block row prefix in LDS
+      qc > (1 << 20) || qs > (1 << 20))  // the solving block keeps the per-block row prefix in LDS
     return fail(h, LLSR_EINVAL, "scan2map capacities out of range");
   HIP_OK(h, hipSetDevice(h->device));
   auto& m = h->mo;
@@ -732,13 +733,11 @@ extern "C" int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t P, int32_t mc, 
   m.log2T_s = grid_log2_table(ms);
   m.blocks_c = (qc + 255) / 256;
   m.blocks = m.blocks_c + (qs + 255) / 256;
-  // depth blocks of matAt * matA: kc >= 340 rows once N > 680 (llsr_eigen::gemm_kc), + 1 workgroup
-  // for matAt * matB / CF_all
-  m.red_blocks = (qc + qs) / 336 + 3;
+  if (m.blocks == 0) m.blocks = 1;  // one (empty) block still runs each iteration's solve
   const size_t Tc = (size_t)1 << m.log2T_c, Ts = (size_t)1 << m.log2T_s;
   const size_t bytes = sizeof(S2MProb) * P + sizeof(CellSlot) * P * (Tc + Ts) +
                        sizeof(float4) * P * ((size_t)mc + ms) + sizeof(int2) * P * ((size_t)mc + ms) +
-                       sizeof(int) * 2 * P + sizeof(float) * 32 * (size_t)P * m.red_blocks +
+                       sizeof(int) * 2 * P +
                        sizeof(float4) * 2 * 256 * (size_t)P * m.blocks + sizeof(int) * (size_t)P * m.blocks +
                        4096 + 10 * 256;
   if (hipMalloc(&m.pool, bytes) != hipSuccess) {
@@ -762,10 +761,14 @@ extern "C" int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t P, int32_t mc, 
   gs.cursor = carve<int>(q, (size_t)P);
   gc.cap = mc; gs.cap = ms;
   gc.log2T = m.log2T_c; gs.log2T = m.log2T_s;
-  a.partial = carve<float>(q, 32 * (size_t)P * m.red_blocks);
   a.rows = carve<float4>(q, 2 * 256 * (size_t)P * m.blocks);
+  a.solve_rows = (kSolveLds - 4 * ((m.blocks + 4) & ~3)) / 32;
+  if (a.solve_rows < 256)
+    return fail(h, LLSR_EINVAL, "scan2map: too many query blocks for the solve kernel's LDS");
+  if (hipFuncSetAttribute((const void*)k_s2m_solve, hipFuncAttributeMaxDynamicSharedMemorySize, kSolveLds) !=
+      hipSuccess)
+    return fail(h, LLSR_ENODEV, "k_s2m_solve LDS attribute");
   a.bcnt = carve<int>(q, (size_t)P * m.blocks);
-  a.red_blocks = m.red_blocks;
   a.n_active = carve<int>(q, 2);
   a.error = a.n_active + 1;
   a.cap_qc = qc; a.cap_qs = qs; a.cap_mc = mc; a.cap_ms = ms;
@@ -807,6 +810,10 @@ static int32_t s2m_prepare(llsr_handle* h, const llsr_s2m_batch* b, hipStream_t 
   a.deg_in = opt.deg_in; a.matP_in = opt.matP_in;
   a.deg_out = opt.deg_out; a.matP_out = opt.matP_out;
   a.iter_max = h->cfg.iterCountThres;
+  {
+    const char* dbg = std::getenv("LLSR_S2M_DBG");
+    a.dbg = dbg ? std::atoi(dbg) : 0;
+  }
   a.step_size = h->cfg.step_size;
   a.stop_thres = h->cfg.stop_thres;
   a.cq = b->corner_q; a.cq_off = b->corner_q_off;
@@ -846,9 +853,8 @@ static int32_t s2m_batch(llsr_handle* h, const llsr_s2m_batch* b, hipStream_t s,
   for (int it = 0; it < a.iter_max;) {
     const int n = (a.iter_max - it) < poll ? (a.iter_max - it) : poll;
     for (int k = 0; k < n; ++k) {
-      if (m.blocks) k_s2m_iter<<<dim3(m.blocks, P), 256, 0, s>>>(a);
-      k_s2m_reduce<<<dim3(m.red_blocks, P), 256, sizeof(int) * (m.blocks + 1), s>>>(a);
-      k_s2m_solve<<<(P + 63) / 64, 64, 0, s>>>(a);
+      k_s2m_iter<<<dim3(m.blocks, P), 256, 0, s>>>(a);
+      k_s2m_solve<<<P, 256, kSolveLds, s>>>(a);
     }
     it += n;
     launches += n;

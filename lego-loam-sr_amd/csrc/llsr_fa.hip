@@ -235,6 +235,91 @@ __device__ __forceinline__ void bitonic_sort_u64(uint64_t* key, int n2) {
   }
 }
 
+// Block sort of n2 (power of two, 256 <= n2 <= 2048) distinct 64-bit keys in LDS, ascending: each
+// of the 4 waves sorts its quarter in registers (bitonic: stages below 64 with lane shuffles, the
+// rest between a lane's own registers; no barrier), then every key's final position is its rank
+// in its own quarter plus the number of smaller keys in the three others (binary searches in LDS).
+// Same result as bitonic_sort_u64 for distinct keys (padding ~0 keys stay at the end).
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
+  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+  return ((uint64_t)hi << 32) | lo;
+}
+template <int K>
+__device__ __forceinline__ void wave_bitonic(uint64_t (&v)[K]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int size = 2; size <= 64 * K; size <<= 1) {
+#pragma unroll
+    for (int j = size >> 1; j > 0; j >>= 1) {
+      if (j >= 64) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const int kp = k ^ (j >> 6);
+          if (kp > k) {
+            const bool up = ((k * 64 + lane) & size) == 0;
+            const uint64_t a = v[k], b = v[kp];
+            const bool sw = (a > b) == up;
+            v[k] = sw ? b : a;
+            v[kp] = sw ? a : b;
+          }
+        }
+      } else {
+        const bool lower = (lane & j) == 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const uint64_t o = shfl_xor64(v[k], j);
+          const bool up = ((k * 64 + lane) & size) == 0;
+          const uint64_t mn = v[k] < o ? v[k] : o, mx = v[k] < o ? o : v[k];
+          v[k] = (lower == up) ? mn : mx;
+        }
+      }
+    }
+  }
+}
+template <int K>
+__device__ void block4_sort_k(uint64_t* key) {
+  constexpr int Q = 64 * K;  // keys per wave
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint64_t v[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = key[w * Q + k * 64 + lane];
+  wave_bitonic<K>(v);
+#pragma unroll
+  for (int k = 0; k < K; ++k) key[w * Q + k * 64 + lane] = v[k];
+  __syncthreads();
+  int pos[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    int p = k * 64 + lane;
+    for (int o = 0; o < 4; ++o) {
+      if (o == w) continue;
+      const uint64_t* sq = key + o * Q;
+      int lo = 0, hi = Q;  // count of keys < v[k] in quarter o
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (sq[mid] < v[k]) lo = mid + 1;
+        else hi = mid;
+      }
+      p += lo;
+    }
+    pos[k] = p;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) key[pos[k]] = v[k];
+  __syncthreads();
+}
+// n2 = 4 * 64 * K for K in {1, 2, 4, 8}
+__device__ void block4_sort_u64(uint64_t* key, int n2) {
+  switch (n2) {
+    case 256: block4_sort_k<1>(key); break;
+    case 512: block4_sort_k<2>(key); break;
+    case 1024: block4_sort_k<4>(key); break;
+    default: block4_sort_k<8>(key); break;
+  }
+}
+
 __device__ __forceinline__ int pow2_ceil(int n) {
   int n2 = 1;
   while (n2 < n) n2 <<= 1;
@@ -700,11 +785,11 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
       key[ro] = ((uint64_t)vk[t] << 32) | (uint32_t)ro;
     }
     if (tid == 0) rstart[R] = (uint16_t)L;
-    const int R2 = pow2_ceil(R);
+    const int R2 = max(pow2_ceil(R), 256);
     for (int t = R + tid; t < R2; t += nt) key[t] = ~0ull;
     __syncthreads();
     if (c.dbg_phase <= 5) return;
-    bitonic_sort_u64(key, R2);
+    block4_sort_u64(key, R2);
     if (c.dbg_phase <= 6) return;
     // voxels = groups of sorted runs with equal id; sum members in (run start, position) order.
     // Sorted run t = u * 256 + tid sits in slot u of a lane, so a wave's voxel heads of one slot are

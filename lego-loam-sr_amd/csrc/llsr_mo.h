@@ -36,10 +36,8 @@ struct S2MArgs {
   llsr_lm_report* report;      // [P]
   S2MProb* prob;               // [P]
   CellGrids2 grids;            // g[0] corner map, g[1] surf map
-  float* partial;              // [P][red_blocks][32] depth-block sums (k_s2m_reduce)
   float4* rows;                // [P][blocks][256][2] compacted matA rows per query block
   int* bcnt;                   // [P][blocks] rows per query block
-  int red_blocks;              // grid.x of k_s2m_reduce: depth blocks bound + 1 (matAtB / CF_all)
   int* n_active;               // problems still iterating
   int* error;                  // capacity / offset violations
   // split-correspondence mode (llsr_scan2map_shard_*): this rank's share of the query blocks
@@ -48,14 +46,17 @@ struct S2MArgs {
   // MapOptimization members that outlive a frame (mapOptimization.h:279-281, zeroed at
   // construction MO:285-286): isDegenerate / matP in at setup and out at finish (mapping chain;
   // null: a fresh optimiser per problem)
+  int solve_rows;              // matA rows k_s2m_solve stages in LDS at a time
+  int dbg;                     // diagnostics (LLSR_S2M_DBG): k_s2m_solve stops after stage dbg (0: never)
   const int* deg_in; const float* matP_in;
   int* deg_out; float* matP_out;
 };
 
 __global__ void k_s2m_setup(S2MArgs a);
 __global__ void k_s2m_iter(S2MArgs a);
-__global__ void k_s2m_reduce(S2MArgs a);
+
 __global__ void k_s2m_solve(S2MArgs a);
+constexpr int kSolveLds = 144 * 1024;  // k_s2m_solve's dynamic LDS (gfx950: 160 KB per workgroup)
 __global__ void k_s2m_finish(S2MArgs a);
 __global__ void k_s2m_iter_fx(S2MArgs a);
 __global__ void k_s2m_solve_fx(S2MArgs a);

@@ -8,9 +8,8 @@
 //                      setInputCloud, MO:1575-1576), llsr_grid.h
 //   k_s2m_iter  x it   one launch per LM iteration (MO:1578-1608) over (query block, problem):
 //                      pointAssociateToMap, kNN-5, the corner line / surf plane coefficient, the
-//                      Jacobian row, a fixed-order block reduction of the 21 + 6 normal-equation
-//                      terms into per-block partials
-//   k_s2m_solve x it   one thread per problem: the block partials summed in block order, then
+//                      Jacobian row, compacted per block in laserCloudOri order
+//   k_s2m_solve x it   one workgroup per problem: the normal equations in Eigen's order, then
 //                      LMOptimization's solve / degeneracy / update / stop test
 //   k_s2m_finish       pose + llsr_lm_report out
 //
@@ -21,8 +20,8 @@
 // order the cells are visited. The per-correspondence arithmetic repeats the reference's float
 // and double operations one for one (-ffp-contract=off, glibc sinf/cosf ports, Eigen 3.3.7
 // restatements in llsr_eigen.h), so correspondences and coefficients are bit-identical to the
-// oracle; only the normal-equation summation order differs (the reference's is Eigen's GEMM
-// blocking), hence the pose tolerance of north_star (1e-4).
+// oracle, and the normal equations are summed in the reference's Eigen order: the float path is
+// bit-identical to the oracle (tests/test_gpu_mo.py).
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -284,16 +283,264 @@ __device__ __forceinline__ void query_terms(const S2MArgs& a, const S2MProb& st,
 
 // ---- the float path (llsr_scan2map_batch): Eigen's summation order ------------------------
 // LMOptimization's matA rows are the correspondences in laserCloudOri order: the corner queries
-// that found one, in query order, then the surf queries (MO:1582-1583). k_s2m_iter writes each
-// 256-query block's rows compacted in that order (a.rows, 8 floats: J[6], matB, |intensity|) and
-// the block's row count; k_s2m_reduce then sums them exactly as the reference's Eigen 3.3.7 build
-// does (llsr_eigen.h, oracle_eigen.h gemm_ata / gemv_atb): matAt * matA per GEMM depth block of kc
-// rows (one workgroup per block, from zero, rows 4-5 x columns 0-3 through gebp's four-accumulator
-// path), matAt * matB and CF_all left to right over all rows (the last workgroup); k_s2m_solve adds
-// the depth blocks in order. The result is bit-identical to the oracle's statement.
+// that found one, in query order, then the surf queries (MO:1582-1583). Each 256-query block of
+// k_s2m_iter writes its rows compacted in that order (a.rows, 8 floats: J[6], matB, |intensity|)
+// and its row count; k_s2m_solve (one workgroup per problem) then sums them
+// exactly as the reference's Eigen 3.3.7 build does (llsr_eigen.h, oracle_eigen.h gemm_ata /
+// gemv_atb) — matAt * matA per GEMM depth block of kc rows from zero, rows 4-5 x columns 0-3
+// through gebp's four-accumulator path, the depth blocks added in order; matAt * matB and CF_all
+// left to right — one lane per sum (the depth blocks spread over three waves), and runs the LM
+// step. The
+// result is bit-identical to the oracle's statement; one launch per LM iteration.
+namespace {
+constexpr int kRedWords = 29;   // AtA: 21 upper-triangle entries + the 8 of rows 4-5 x columns 0-3
+
+// Exclusive prefix of the problem's block row counts into pre[0..blocks] (LDS).
+__device__ void block_prefix(const S2MArgs& a, int p, int* pre, int* tmp) {
+  const int nb = a.blocks, t = threadIdx.x;
+  const int per = (nb + 255) / 256, b0 = t * per, b1 = min(nb, b0 + per);
+  const int* cnt = a.bcnt + (size_t)p * nb;
+  int s = 0;
+  for (int b = b0; b < b1; ++b) s += cnt[b];
+  tmp[t] = s;
+  __syncthreads();
+  if (t == 0) {
+    int acc = 0;
+    for (int k = 0; k < 256; ++k) { const int v = tmp[k]; tmp[k] = acc; acc += v; }
+  }
+  __syncthreads();
+  s = tmp[t];
+  for (int b = b0; b < b1; ++b) { pre[b] = s; s += cnt[b]; }
+  if (b1 == nb && b0 < b1) pre[nb] = s;
+  if (nb == 0 && t == 0) pre[0] = 0;
+  __syncthreads();
+}
+
+// Rows [r0, r0 + d) of the problem's matA into lrow (LDS, 8 floats per row), all threads: each
+// lane locates four rows at a time, then issues their eight loads at once.
+__device__ void stage_rows(const S2MArgs& a, int p, const int* pre, int r0, int d, float4* lrow) {
+  const int nb = a.blocks;
+  constexpr int kU = 4;
+  for (int i0 = 0; i0 < d; i0 += kU * 256) {
+  const float4* src[kU];
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const int i = i0 + threadIdx.x + u * 256;
+    src[u] = nullptr;
+    if (i < d) {
+      const int g = r0 + i;
+      int lo = 0, hi = nb - 1;  // the block b with pre[b] <= g < pre[b + 1]
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= g) lo = mid;
+        else hi = mid - 1;
+      }
+      src[u] = a.rows + (((size_t)p * nb + lo) * 256 + (g - pre[lo])) * 2;
+    }
+  }
+  float4 v0[kU], v1[kU];
+#pragma unroll
+  for (int u = 0; u < kU; ++u)
+    if (src[u]) { v0[u] = src[u][0]; v1[u] = src[u][1]; }
+#pragma unroll
+  for (int u = 0; u < kU; ++u)
+    if (src[u]) {
+      const int i = i0 + threadIdx.x + u * 256;
+      lrow[2 * i] = v0[u];
+      lrow[2 * i + 1] = v1[u];
+    }
+  }
+}
+
+// The problem's normal equations in Eigen's order and the LM step (MO:1444-1570), by one
+// workgroup. The rows stream through LDS a.solve_rows at a time (all of them at once for the usual
+// few thousand correspondences, so the waves never wait on each other); wave 0 lanes 0..6 sum matAt * matB (6,
+// from the first product) and CF_all (from zero) over every row; waves 1..3 own the depth blocks of
+// matAt * matA round robin (block x: wave 1 + x % 3), 29 lanes each (the 21 upper-triangle
+// entries, then rows 4-5 x columns 0-3 through gebp's four-accumulator path), each block summed
+// from zero; thread 0 adds the blocks in order and runs the LM step.
+__device__ void s2m_assemble_solve(const S2MArgs& a, int p, int* pre, int* tmp, float4* lrow) {
+  S2MProb& st = a.prob[p];
+  block_prefix(a, p, pre, tmp);
+  if (a.dbg == 1) return;
+  const int N = pre[a.blocks];
+  const int nc = pre[a.blocks_c];
+  const int t = threadIdx.x, wv = t >> 6, ln = t & 63;
+  constexpr int kMaxDepthBlocks = 64;
+  __shared__ float s_blk[kMaxDepthBlocks][kRedWords];
+  __shared__ float s_b[7];
+  const int kc = N >= 50 ? llsr_eigen::gemm_kc(N, 6, 6) : 1;
+  const int nkb = N >= 50 ? (N + kc - 1) / kc : 0;
+  // lane roles: wave 0 lanes < 7 -> matB / CF; waves 1..3 lanes < 29 -> AtA
+  int ia = 0, ib = 0;
+  bool sw = false;
+  if (wv == 0) {
+    ia = ln < 6 ? ln : 7;
+    ib = 6;
+  } else if (ln < 21) {
+    int i = 0, k = ln;
+    while (k >= 6 - i) { k -= 6 - i; ++i; }
+    ia = i; ib = i + k;
+  } else if (ln < kRedWords) {
+    sw = true; ia = 4 + (ln - 21) / 4; ib = (ln - 21) % 4;
+  }
+  const bool busy = (wv == 0 && ln < 7) || (wv > 0 && ln < kRedWords);
+  float c = 0.0f, C0 = 0.0f, C1 = 0.0f, C2 = 0.0f, C3 = 0.0f;
+  if (N >= 50) {
+    for (int r0 = 0; r0 < N; r0 += a.solve_rows) {
+      const int d = min(a.solve_rows, N - r0);
+      stage_rows(a, p, pre, r0, d, lrow);
+      __syncthreads();
+      if (a.dbg == 2) continue;
+      const float* lr = reinterpret_cast<const float*>(lrow);
+      if (busy && wv == 0 && a.dbg != 5) {
+        // the products do not depend on the running sum: load 8 rows ahead, then add in order;
+        // loads unconditional and the CF lane's factor a select, so the loop has no branch
+        const int ib2 = ln < 6 ? 6 : 7, ia2 = ln < 6 ? ia : 7;
+        const bool mul = ln < 6;
+        int q = 0;
+        if (r0 == 0) {
+          const float x = lr[ia2], y = lr[ib2];
+          c = mul ? x * y : c + x;
+          q = 1;
+        }
+        for (; q + 32 <= d; q += 32) {
+          float v[32];
+#pragma unroll
+          for (int u = 0; u < 32; ++u) {
+            const float x = lr[8 * (q + u) + ia2], y = lr[8 * (q + u) + ib2];
+            v[u] = x * (mul ? y : 1.0f);
+          }
+#pragma unroll
+          for (int u = 0; u < 32; ++u) c = c + v[u];
+        }
+        for (; q < d; ++q) {
+          const float x = lr[8 * q + ia2], y = lr[8 * q + ib2];
+          c = c + x * (mul ? y : 1.0f);
+        }
+      } else if (wv > 0 && a.dbg != 4 && d == N) {
+        // every row is in LDS: each depth block runs on 53 lanes of one wave without selects —
+        // lanes 0..20 the upper-triangle entries (c = c + a_i a_j over the block), lanes 21..52 the
+        // 8 swapped entries x 4 accumulators (lane u sums rows q = u mod 4 below endk4), merged as
+        // (C0 + C1) + (C2 + C3) and followed by the remainder rows on the entry's first lane
+        const bool nrm = ln < 21;
+        const int e8 = (ln - 21) >> 2, u4 = (ln - 21) & 3;
+        int fa = ia, fb = ib;
+        if (!nrm && ln < 53) { fa = 4 + e8 / 4; fb = e8 % 4; }
+        for (int x = wv - 1; x < nkb; x += 3) {
+          const int k2 = x * kc, db = min(kc, N - k2), endk4 = (db / 4) * 4;
+          const int q0 = nrm ? 0 : u4, qs = nrm ? 1 : 4, qe = nrm ? db : endk4;
+          float acc = 0.0f;
+          int q = q0;
+          for (; q + 7 * qs < qe; q += 8 * qs) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const float* row = lr + 8 * (k2 + q + u * qs);
+              v[u] = nrm ? row[fa] * row[fb] : row[fb] * row[fa];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc = nrm ? acc + v[u] : v[u] + acc;
+          }
+          for (; q < qe; q += qs) {
+            const float* row = lr + 8 * (k2 + q);
+            acc = nrm ? acc + row[fa] * row[fb] : row[fb] * row[fa] + acc;
+          }
+          // swapped entries: merge the four accumulators on the entry's first lane
+          const int base = 21 + 4 * e8;
+          const float a0 = __shfl(acc, base & 63), a1 = __shfl(acc, (base + 1) & 63);
+          const float a2 = __shfl(acc, (base + 2) & 63), a3 = __shfl(acc, (base + 3) & 63);
+          if (ln < 21) {
+            if (x < kMaxDepthBlocks) s_blk[x][ln] = acc;
+          } else if (ln < 53 && u4 == 0) {
+            float cc = (a0 + a1) + (a2 + a3);
+            for (int qq = endk4; qq < db; ++qq) {
+              const float* row = lr + 8 * (k2 + qq);
+              cc = row[fb] * row[fa] + cc;
+            }
+            if (x < kMaxDepthBlocks) s_blk[x][21 + e8] = cc;
+          }
+        }
+      } else if (busy && wv > 0 && a.dbg != 4) {
+        // the rows stream in chunks: the depth-block segments of this chunk that belong to this wave
+        for (int g = r0; g < r0 + d;) {
+          const int x = g / kc, k2 = x * kc, db = min(kc, N - k2);
+          const int ge = min(k2 + db, r0 + d);
+          if (x % 3 == wv - 1) {
+            const int endk4 = (db / 4) * 4;
+            // branch-free per row: gebp's four accumulators by qq mod 4 below endk4 (swapped
+            // lanes), the merge at endk4, then c = c + product
+            auto step = [&](int qq, float pr) {
+              const bool mn = sw && qq < endk4;
+              const int uu = qq & 3;
+              C0 = (mn && uu == 0) ? pr + C0 : C0;
+              C1 = (mn && uu == 1) ? pr + C1 : C1;
+              C2 = (mn && uu == 2) ? pr + C2 : C2;
+              C3 = (mn && uu == 3) ? pr + C3 : C3;
+              const float cb = (sw && qq == endk4) ? (C0 + C1) + (C2 + C3) : c;
+              c = mn ? c : cb + pr;
+            };
+            int gg = g;
+            for (; gg + 8 <= ge; gg += 8) {
+              float v[8];  // the products, 8 rows ahead of the in-order additions
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                const float* row = lr + 8 * (gg + u - r0);
+                v[u] = row[ia] * row[ib];
+              }
+#pragma unroll
+              for (int u = 0; u < 8; ++u) step(gg + u - k2, v[u]);
+            }
+            for (; gg < ge; ++gg) {
+              const float* row = lr + 8 * (gg - r0);
+              step(gg - k2, row[ia] * row[ib]);
+            }
+            if (ge == k2 + db) {  // the depth block is complete
+              const float v = (sw && endk4 == db) ? (C0 + C1) + (C2 + C3) : c;
+              if (x < kMaxDepthBlocks) s_blk[x][ln] = v;
+              c = 0.0f; C0 = 0.0f; C1 = 0.0f; C2 = 0.0f; C3 = 0.0f;
+            }
+          }
+          g = ge;
+        }
+      }
+      __syncthreads();
+    }
+    if (wv == 0 && ln < 7) s_b[ln] = c;
+  }
+  __syncthreads();
+  if (t != 0 || (a.dbg >= 2 && a.dbg <= 5)) return;
+  st.iter += 1;
+  const int iterCount = st.iter - 1;
+  st.nc = nc;
+  st.ns = N - nc;
+  bool conv = false;
+  if (N >= 50 && nkb <= kMaxDepthBlocks) {  // MO:1453
+    float wsum[kRedWords];
+    for (int e = 0; e < kRedWords; ++e) wsum[e] = 0.0f;
+    for (int x = 0; x < nkb; ++x)
+      for (int e = 0; e < kRedWords; ++e) wsum[e] = wsum[e] + 1.0f * s_blk[x][e];
+    float AtA[36];
+    int e = 0;
+    for (int r = 0; r < 6; ++r)
+      for (int q = r; q < 6; ++q, ++e) { AtA[r + 6 * q] = wsum[e]; AtA[q + 6 * r] = wsum[e]; }
+    for (int r = 4; r < 6; ++r)
+      for (int q = 0; q < 4; ++q, ++e) AtA[r + 6 * q] = wsum[e];
+    conv = llsr_lm::lm_update_full(st, AtA, s_b, s_b[6], N, iterCount, a.applied != 0, a.stop_thres);
+  } else if (N >= 50) {
+    atomicOr(a.error, 1);  // more depth blocks than kMaxDepthBlocks (> ~21k correspondences)
+  }
+  if (conv) st.converged = 1;
+  if (conv || st.iter >= a.iter_max) {
+    st.active = 0;
+    atomicSub(a.n_active, 1);
+  }
+}
+}  // namespace
+
 template <bool kCorner>
 __device__ __forceinline__ void s2m_block(const S2MArgs& a, int p, int qb) {
-  const S2MProb& st = a.prob[p];
+  S2MProb& st = a.prob[p];
   if (!st.active) return;
   __shared__ int wcnt[4];
   float J[6], bb = 0.0f, ald = 0.0f;
@@ -321,156 +568,16 @@ __global__ __launch_bounds__(256) void k_s2m_iter(S2MArgs a) {
     s2m_block<false>(a, blockIdx.y, blockIdx.x - a.blocks_c);
 }
 
-namespace {
-constexpr int kMaxKc = 680;     // llsr_eigen::gemm_kc's ceiling with a 32 KiB L1 (rows per depth block)
-constexpr int kRedWords = 29;   // AtA: 21 upper-triangle entries + the 8 of rows 4-5 x columns 0-3
-
-// Exclusive prefix of the problem's block row counts into pre[0..blocks] (LDS).
-__device__ void block_prefix(const S2MArgs& a, int p, int* pre, int* tmp) {
-  const int nb = a.blocks, t = threadIdx.x;
-  const int per = (nb + 255) / 256, b0 = t * per, b1 = min(nb, b0 + per);
-  const int* cnt = a.bcnt + (size_t)p * nb;
-  int s = 0;
-  for (int b = b0; b < b1; ++b) s += cnt[b];
-  tmp[t] = s;
-  __syncthreads();
-  if (t == 0) {
-    int acc = 0;
-    for (int k = 0; k < 256; ++k) { const int v = tmp[k]; tmp[k] = acc; acc += v; }
-  }
-  __syncthreads();
-  s = tmp[t];
-  for (int b = b0; b < b1; ++b) { pre[b] = s; s += cnt[b]; }
-  if (b1 == nb && b0 < b1) pre[nb] = s;
-  if (nb == 0 && t == 0) pre[0] = 0;
-  __syncthreads();
-}
-
-// Rows [r0, r0 + d) of the problem's matA into lrow (LDS, 2 float4 per row).
-__device__ void gather_rows(const S2MArgs& a, int p, const int* pre, int r0, int d, float4* lrow) {
-  const int nb = a.blocks;
-  for (int i = threadIdx.x; i < d; i += blockDim.x) {
-    const int g = r0 + i;
-    int lo = 0, hi = nb - 1;  // the block b with pre[b] <= g < pre[b + 1]
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (pre[mid] <= g) lo = mid;
-      else hi = mid - 1;
-    }
-    const float4* src = a.rows + (((size_t)p * nb + lo) * 256 + (g - pre[lo])) * 2;
-    lrow[2 * i] = src[0];
-    lrow[2 * i + 1] = src[1];
-  }
-}
-}  // namespace
-
-// grid (red_blocks, P), 256 threads: workgroup x < nkb sums depth block x of matAt * matA; the last
-// workgroup sums matAt * matB and CF_all over every row.
-__global__ __launch_bounds__(256) void k_s2m_reduce(S2MArgs a) {
-  const int p = blockIdx.y;
-  const S2MProb& st = a.prob[p];
-  if (!st.active) return;
-  extern __shared__ int sm_pre[];                  // [blocks + 1]
+// grid P, 256 threads, dynamic LDS a.solve_lds bytes: one workgroup per problem assembles the
+// normal equations from the rows k_s2m_iter wrote (the kernel boundary makes them visible: no
+// device-scope fences, which would write back every L2 on MI355X's eight XCDs) and solves.
+__global__ __launch_bounds__(256) void k_s2m_solve(S2MArgs a) {
+  const int p = blockIdx.x;
+  if (!a.prob[p].active) return;
+  extern __shared__ int s_dyn[];  // [blocks + 1] block prefix, then a.solve_rows matA rows
   __shared__ int tmp[256];
-  __shared__ float4 lrow[2 * kMaxKc];
-  block_prefix(a, p, sm_pre, tmp);
-  const int N = sm_pre[a.blocks];
-  float* part = a.partial + ((size_t)p * a.red_blocks + blockIdx.x) * 32;
-  const int t = threadIdx.x;
-  if ((int)blockIdx.x == a.red_blocks - 1) {
-    // matAtB = matAt * matB (lazy product: from the first product, left to right) and CF_all
-    float acc = 0.0f;
-    for (int r0 = 0; r0 < N; r0 += kMaxKc) {
-      const int d = min(kMaxKc, N - r0);
-      gather_rows(a, p, sm_pre, r0, d, lrow);
-      __syncthreads();
-      if (t < 7) {
-        const float* lr = reinterpret_cast<const float*>(lrow);
-        for (int q = 0; q < d; ++q) {
-          const float* row = lr + 8 * q;
-          if (t < 6) acc = (r0 + q == 0) ? row[t] * row[6] : acc + row[t] * row[6];
-          else acc = acc + row[7];
-        }
-      }
-      __syncthreads();
-    }
-    if (t < 7) part[t] = acc;
-    if (t == 7) part[7] = __int_as_float(sm_pre[a.blocks_c]);  // corner correspondences
-    if (t == 8) part[8] = __int_as_float(N);
-    return;
-  }
-  if (N < 50) return;  // MO:1453: no solve this iteration
-  const int kc = llsr_eigen::gemm_kc(N, 6, 6);
-  const int x = blockIdx.x;
-  const int r0 = x * kc;
-  if (r0 >= N) return;
-  const int d = min(kc, N - r0);
-  gather_rows(a, p, sm_pre, r0, d, lrow);
-  __syncthreads();
-  if (t < kRedWords) {
-    const float* lr = reinterpret_cast<const float*>(lrow);
-    float c;
-    if (t < 21) {  // upper triangle (i <= j), row-major order: c = c + a_i * a_j from zero
-      int i = 0, k = t;
-      while (k >= 6 - i) { k -= 6 - i; ++i; }
-      const int j = i + k;
-      c = 0.0f;
-      for (int q = 0; q < d; ++q) c = c + lr[8 * q + i] * lr[8 * q + j];
-    } else {       // (i, j), i in {4, 5}, j in {0..3}: gebp's swapped 1 x 4 path
-      const int i = 4 + (t - 21) / 4, j = (t - 21) % 4;
-      float C0 = 0.0f, C1 = 0.0f, C2 = 0.0f, C3 = 0.0f;
-      const int endk4 = (d / 4) * 4;
-      int q = 0;
-      for (; q < endk4; q += 4) {
-        C0 = lr[8 * q + j] * lr[8 * q + i] + C0;
-        C1 = lr[8 * (q + 1) + j] * lr[8 * (q + 1) + i] + C1;
-        C2 = lr[8 * (q + 2) + j] * lr[8 * (q + 2) + i] + C2;
-        C3 = lr[8 * (q + 3) + j] * lr[8 * (q + 3) + i] + C3;
-      }
-      c = (C0 + C1) + (C2 + C3);
-      for (; q < d; ++q) c = lr[8 * q + j] * lr[8 * q + i] + c;
-    }
-    part[t] = c;
-  }
-}
-
-// One thread per problem: the depth blocks added in order (res = res + 1.0f * block), then the LM
-// step on the full matAtA (not symmetric in the last bits: rows 4-5 x columns 0-3).
-__global__ __launch_bounds__(64) void k_s2m_solve(S2MArgs a) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= a.P) return;
-  S2MProb& st = a.prob[p];
-  if (!st.active) return;
-  const float* last = a.partial + ((size_t)p * a.red_blocks + a.red_blocks - 1) * 32;
-  const int N = __float_as_int(last[8]);
-  const int nc = __float_as_int(last[7]);
-  st.iter += 1;
-  const int iterCount = st.iter - 1;
-  st.nc = nc;
-  st.ns = N - nc;
-  bool conv = false;
-  if (N >= 50) {  // MO:1453
-    const int kc = llsr_eigen::gemm_kc(N, 6, 6);
-    const int nkb = (N + kc - 1) / kc;
-    float w[kRedWords];
-    for (int e = 0; e < kRedWords; ++e) w[e] = 0.0f;
-    for (int x = 0; x < nkb; ++x) {
-      const float* pp = a.partial + ((size_t)p * a.red_blocks + x) * 32;
-      for (int e = 0; e < kRedWords; ++e) w[e] = w[e] + 1.0f * pp[e];
-    }
-    float AtA[36];
-    int e = 0;
-    for (int i = 0; i < 6; ++i)
-      for (int j = i; j < 6; ++j, ++e) { AtA[i + 6 * j] = w[e]; AtA[j + 6 * i] = w[e]; }
-    for (int i = 4; i < 6; ++i)
-      for (int j = 0; j < 4; ++j, ++e) AtA[i + 6 * j] = w[e];
-    conv = llsr_lm::lm_update_full(st, AtA, last, last[6], N, iterCount, a.applied != 0, a.stop_thres);
-  }
-  if (conv) st.converged = 1;
-  if (conv || st.iter >= a.iter_max) {
-    st.active = 0;
-    atomicSub(a.n_active, 1);
-  }
+  float4* lrow = reinterpret_cast<float4*>(s_dyn + ((a.blocks + 4) & ~3));
+  s2m_assemble_solve(a, p, s_dyn, tmp, lrow);
 }
 
 // ---- split-correspondence mode (llsr_scan2map_shard_*) ----------------------

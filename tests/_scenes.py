@@ -13,7 +13,8 @@ import numpy as np
 import oracle_py
 from llsr import default_config, synth
 
-FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mo_map_vlp16.npz")
+# the one-lane 76k map (tests/golden/make_mo_fixture.py, mo_map_vlp16_small.npz)
+FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mo_map_vlp16_small.npz")
 
 
 def _scaled(a, f):

@@ -1,12 +1,15 @@
 """Build the scan-to-map fixture (BASELINE.json configs[2]); run from the repo root.
 
 A local map made the way MapOptimization makes one (extractSurroundingKeyFrames, MO:1096-1232):
-keyframes every 1 m (the 1 m keypose leaf, MO:99) along the whole 150 m synthetic street — wider
-than the 50 m surrounding-keyframe radius (loam_config.yaml:26) so the map reaches the config's
-~100k-point size (15.2k corner + 61.3k surf = 76k) — each keyframe's corner (less-sharp), surf
-(less-flat) and outlier clouds from the oracle's IP + FA feature stage, moved into the map
-frame by the known sensor pose, concatenated (MO:1219-1221) and voxel-downsampled (corner 0.2 m,
-surf 0.4 m; MO:92-94, 1225-1231). Queries follow downsampleCurrentScan (MO:1234-1267): corner
+keyframes every 1 m (the 1 m keypose leaf, MO:99) along the whole 150 m synthetic street on five
+lanes (y = 0, 3.5, -3.0, 6.5, -6.5 m) — wider than the 50 m surrounding-keyframe radius
+(loam_config.yaml:26) so the map reaches the config's size (BASELINE.json configs[2]: ~100k
+points, corner ~10k, surf ~90k; the corner map takes the centre lane's keyframes only, which
+gives that split) — each keyframe's corner (cornerPointsSharp: the SR fork stores
+laserCloudCornerScan as the corner keyframe, MO:1746), surf (less-flat) and outlier clouds from
+the oracle's IP + FA feature stage, moved into the map frame by the known sensor pose,
+concatenated (MO:1219-1221) and voxel-downsampled (corner 0.2 m, surf 0.4 m; MO:92-94,
+1225-1231). Queries follow downsampleCurrentScan (MO:1234-1267): corner
 = sharp DS 0.2, surf total = DS 0.4 of (less-flat DS 0.4 + outliers DS 0.4). True pose = the
 frame's sensor position in the LOAM frame; the optimiser starts from a seeded (0.05 rad, 0.2 m)
 perturbation. The scene, noise and oracle are seeded, so the script is deterministic.
@@ -42,7 +45,7 @@ def voxel_ds(p, leaf):
 
 def frame_clouds(cfg, seed, x, y):
     """(less_sharp, sharp, less_flat, outliers) of one frame in its LOAM frame, + map offset."""
-    ora = oracle_py.Oracle(cfg)
+    ora = oracle_py.Oracle(cfg, pcl_voxel_order=True)  # PCL VoxelGrid order: the reference statement
     r = ora.process(synth.make_scan(seed, "vlp16", origin_xy=(x, y), scene_id=0))
     loam = r["loam_xyzi"]
     out = r["outlier_xyzi"].copy()
@@ -51,16 +54,23 @@ def frame_clouds(cfg, seed, x, y):
     return loam[r["less_sharp_ind"]], loam[r["sharp_ind"]], r["less_flat_xyzi"], out, off
 
 
-def main(query_x=(5.3, 10.7, 15.2, 20.6), out="mo_map_vlp16.npz"):
+def main(query_x=(5.3, 10.7, 15.2, 20.6), out="mo_map_vlp16.npz", lanes=(0.0, 3.5, -3.0, 6.5, -6.5),
+         corner_kind="sharp"):
+    """corner_kind "sharp" (the SR fork's corner keyframe) or "less_sharp" (round 1's fixture)."""
     cfg = _abi.config_for("vlp16")
     rng = np.random.default_rng(77)
     corner, surf = [], []
-    for k, x in enumerate(np.arange(-62.0, 89.0, 1.0)):
-        ls, _, lf, ol, off = frame_clouds(cfg, 2000 + k, x, rng.uniform(-0.5, 0.5))
-        for dst, pts in ((corner, ls), (surf, lf), (surf, ol)):
+    xs = np.arange(-62.0, 89.0, 1.0)
+    for lane, y0 in enumerate(lanes):
+      for k, x in enumerate(xs):
+        ls, sh, lf, ol, off = frame_clouds(cfg, 2000 + 1000 * lane + k, x, y0 + rng.uniform(-0.5, 0.5))
+        if corner_kind == "less_sharp":
+            sh = ls
+        for dst, pts in (((corner, sh),) if lane == 0 else ()) + ((surf, lf), (surf, ol)):
             q = pts.copy()
             q[:, :3] += off
             dst.append(q)
+      print(f"lane {lane}: corner raw {sum(len(c) for c in corner)}, surf raw {sum(len(c) for c in surf)}", flush=True)
     corner_map = voxel_ds(np.concatenate(corner), 0.2)
     surf_map = voxel_ds(np.concatenate(surf), 0.4)
     frames = {}
@@ -80,3 +90,6 @@ def main(query_x=(5.3, 10.7, 15.2, 20.6), out="mo_map_vlp16.npz"):
 
 if __name__ == "__main__":
     main()
+    # the smaller map of round 1 (one lane, less-sharp corners): tests/_scenes.py shrinks it into
+    # the degenerate-branch scenes
+    main(out="mo_map_vlp16_small.npz", lanes=(0.0,), corner_kind="less_sharp")

@@ -1,7 +1,7 @@
 """GPU parity of the scan-to-map LM (MapOptimization::scan2MapOptimization, MO:1572-1610).
 
 HIP path through the C-ABI (llsr_scan2map / llsr_scan2map_batch) against the oracle
-(oracle/oracle_mo.cpp) on the committed ~76k-point map fixture (tests/golden/make_mo_fixture.py).
+(oracle/oracle_mo.cpp) on the committed ~100k-point map fixture (13.0k corner + 87.3k surf) (tests/golden/make_mo_fixture.py).
 
 The bar is bit-exactness: the correspondences and Jacobian rows repeat the reference's float /
 double operations one for one, and the normal equations are summed in the order of the
