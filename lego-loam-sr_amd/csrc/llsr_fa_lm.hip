@@ -26,6 +26,7 @@
 #include "llsr_device.h"
 #include "llsr_eigen.h"
 #include "llsr_grid.h"
+#include "llsr_isort.h"
 #include "llsr_s2s.h"
 
 namespace llsr {
@@ -173,7 +174,7 @@ __device__ void nn1_block_multi(const float4* pts, int n, const float4* qs, int 
 // The two linear scans of the tripod searches walk the last cloud away from the nearest neighbour
 // until the ring leaves [cs - 2.5, cs + 2.5]; they read 8 points per step (all loads in flight at
 // once) and replay the serial test on them in order, so the result is the serial loop's.
-constexpr int kScan = 4;
+constexpr int kScan = 8;
 
 template <class Visit>
 __device__ __forceinline__ void scan_up(const float4* pts, int from, int end, int cs, Visit visit) {
@@ -267,6 +268,32 @@ __device__ void surf_finish(const float4* sl, int Ns, int fwd, float4 sel, float
   i3 = b3;
 }
 
+// brute-force kNN-1 of J queries per thread over the LDS corner cloud (index order, strict '<')
+template <int J>
+__device__ __forceinline__ void corner_brute(const float4* cl, int Nc, const float4* qs, float* bd, int* bi) {
+  int k = 0;
+  for (; k + 8 <= Nc; k += 8) {  // 8 LDS reads in flight, then the in-order tests
+    float4 c[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) c[u] = cl[k + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const float d = l2(qs[j], c[u]);
+        if (d < bd[j]) { bd[j] = d; bi[j] = k + u; }
+      }
+  }
+  for (; k < Nc; ++k) {
+    const float4 c = cl[k];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const float d = l2(qs[j], c);
+      if (d < bd[j]) { bd[j] = d; bi[j] = k; }
+    }
+  }
+}
+
 // Jacobian constants of calculateTransformationSurf (FA:1858-1891) / ...Corner (FA:2025-2043)
 struct JacSurf {
   float a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11, crx, b2, b6, c1, c2, c3, c4, c5, c6, c7, c8, c9;
@@ -345,7 +372,7 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
   const int p = blockIdx.x;
   const int tid = threadIdx.x;
 #ifdef LLSR_S2S_PROF
-  unsigned long long tprev = wall_clock64(), tAks = 0, tAkc = 0, tA = 0, tB = 0, tC = 0;
+  unsigned long long tprev = wall_clock64(), tAks = 0, tAkc = 0, tA = 0, tB = 0, tC = 0, tF = 0;
 #endif
   __shared__ float t[6];
   __shared__ float matP[9];
@@ -353,6 +380,7 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
   __shared__ int isDeg, stop, n_corr[2], iters[2];
   __shared__ float4 lrows[kLdsRows];
   __shared__ uint8_t lvalid[kLdsRows];
+  __shared__ uint16_t lvix[kLdsRows];  // phase B: the rows holding a correspondence, in order
   __shared__ float4 lcl[kLdsCorner];
   __shared__ int fbq[kFbMax], nfb, nvalid;
   __shared__ float red_d[kMulti][kThreads / 64];
@@ -379,11 +407,8 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
   if (!skipped) {
     const bool corner_lds = Nc <= kLdsCorner;
     const float4* clg = gc.src + gc.off[p];
-    const float4* cl = clg;
-    if (corner_lds) {
-      for (int k = tid; k < Nc; k += kThreads) lcl[k] = cl[k];
-      cl = lcl;  // visible to every thread after the barrier at the top of the first phase
-    }
+    if (corner_lds)  // visible to every thread after the barrier at the top of the first phase
+      for (int k = tid; k < Nc; k += kThreads) lcl[k] = clg[k];
     const float4* sl = gs.src + gs.off[p];
     const int capq = a.cap_sharp > a.cap_flat ? a.cap_sharp : a.cap_flat;
     int* idx = a.idx + (size_t)p * capq * 3;
@@ -414,8 +439,13 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
         // FA:1737-1803) and the correspondence indices it leaves in idx
         auto finish = [&](int q, float4 sel, int nn, float nd) {
           int i1, i2, i3 = -1;
-          if (surf) surf_finish(sl, Ns, F, sel, a.dist_sqr, nn, nd, i1, i2, i3);
-          else corner_finish(cl, Nc, Ms, sel, a.dist_sqr, nn, nd, i1, i2);
+          if (surf) {
+            surf_finish(sl, Ns, F, sel, a.dist_sqr, nn, nd, i1, i2, i3);
+          } else if (corner_lds) {  // LDS-typed accesses (a generic pointer would issue flat loads)
+            corner_finish(lcl, Nc, Ms, sel, a.dist_sqr, nn, nd, i1, i2);
+          } else {
+            corner_finish(clg, Nc, Ms, sel, a.dist_sqr, nn, nd, i1, i2);
+          }
           int* ix = idx + 3 * q;
           ix[0] = i1; ix[1] = i2; ix[2] = i3;
         };
@@ -434,14 +464,13 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
                 bd[j] = INFINITY;
                 bi[j] = INT_MAX;
               }
-              for (int k = 0; k < Nc; ++k) {
-                const float4 c = cl[k];
-#pragma unroll
-                for (int j = 0; j < kMulti; ++j) {
-                  const float d = l2(qs[j], c);
-                  if (d < bd[j]) { bd[j] = d; bi[j] = k; }
-                }
-              }
+              // queries this wave holds (wave-uniform): no distance work for empty slots
+              const int wq = Q - (q0 - lane_id());
+              const int nj = wq > 3 * kThreads ? 4 : wq > 2 * kThreads ? 3 : wq > kThreads ? 2 : 1;
+              if (nj == 1) corner_brute<1>(lcl, Nc, qs, bd, bi);
+              else if (nj == 2) corner_brute<2>(lcl, Nc, qs, bd, bi);
+              else if (nj == 3) corner_brute<3>(lcl, Nc, qs, bd, bi);
+              else corner_brute<4>(lcl, Nc, qs, bd, bi);
 #pragma unroll
               for (int j = 0; j < kMulti; ++j)
                 if (q0 + j * kThreads < Q) finish(q0 + j * kThreads, qs[j], bi[j], bd[j]);
@@ -465,6 +494,8 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
             }
           }
           __syncthreads();
+          if (surf) LLSR_STAMP(tAks);
+          else LLSR_STAMP(tAkc);
           // queries the shells left open: the whole block scans the cloud, kMulti queries per pass
           const int nq = nfb < kFbMax ? nfb : kFbMax;
           for (int k0 = 0; k0 < nq; k0 += kMulti) {
@@ -481,6 +512,7 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
           }
           if (tid == 0) nfb = 0;
           __syncthreads();
+          LLSR_STAMP(tF);
         }
         int nval = 0;
         for (int q = tid; q < Q; q += kThreads) {
@@ -511,7 +543,9 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
               }
             }
           } else if (ix[1] >= 0) {
-            const float4 t1 = cl[ix[0]], t2 = cl[ix[1]];
+            float4 t1, t2;
+            if (corner_lds) { t1 = lcl[ix[0]]; t2 = lcl[ix[1]]; }
+            else { t1 = clg[ix[0]]; t2 = clg[ix[1]]; }
             const float x0 = sel.x, y0 = sel.y, z0 = sel.z;
             const float x1 = t1.x, y1 = t1.y, z1 = t1.z, x2 = t2.x, y2 = t2.y, z2 = t2.z;
             const float m11 = ((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1));
@@ -532,22 +566,66 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
               valid = true;
             }
           }
-          rows[q] = row;
-          vf[q] = valid ? 1 : 0;
+          if (Q <= kLdsRows) { lrows[q] = row; lvalid[q] = valid ? 1 : 0; }
+          else { grows[q] = row; gvalid[q] = valid ? 1 : 0; }
           nval += valid ? 1 : 0;
         }
         if (nval) atomicAdd(&nvalid, nval);
         __syncthreads();
-        if (it % 5 == 0 && surf) LLSR_STAMP(tAks);
-        else if (it % 5 == 0) LLSR_STAMP(tAkc);
-        else LLSR_STAMP(tA);
+        LLSR_STAMP(tA);
         // ---- B: AtA / AtB as Eigen evaluates matAt * matA and matAt * matB (FA:1953-1955) ----
         // Lane r + 3c sums AtA(r, c), lanes 9..11 AtB: the products of two components of each
         // correspondence's row in correspondence order. matAt * matA is Eigen's GEMM: each depth
         // block of kc rows (llsr_eigen::gemm_kc) is summed from zero and added to the result; below
         // N + 6 < 20 it is the lazy coefficient product, and matAt * matB always is (a sum that
         // starts from the first product). Rows without a correspondence are skipped.
-        if (tid < 12) {
+        if (Q <= kLdsRows && tid < 64) {
+          // rows in LDS: wave 0 lists the rows holding a correspondence (ballot compaction, order
+          // kept), then lanes 0..11 run their sums over that list with no per-row test
+          int N = 0;
+          for (int q0 = 0; q0 < Q; q0 += 64) {
+            const int q = q0 + tid;
+            const bool v = q < Q && lvalid[q] != 0;
+            const unsigned long long m = __ballot(v);
+            if (v) lvix[N + __popcll(m & ((1ull << tid) - 1ull))] = (uint16_t)q;
+            N += __popcll(m);
+          }
+          wave_sync_lds();
+          if (tid < 12) {
+            const int ra = tid < 9 ? tid % 3 : tid - 9, rb = tid < 9 ? tid / 3 : 3;
+            const float* rf = reinterpret_cast<const float*>(lrows);
+            const bool lazy = tid >= 9 || N + 6 < 20;
+            const int kc = lazy ? N : llsr_eigen::gemm_kc(N, 3, 3);
+            float tot = 0.0f, c = 0.0f;
+            for (int b0 = 0; b0 < N; b0 += kc) {
+              const int b1 = N - b0 < kc ? N : b0 + kc;
+              int i = b0;
+              if (lazy) {  // the coefficient product: starts from the first product
+                const int q = lvix[0];
+                c = rf[4 * q + ra] * rf[4 * q + rb];
+                i = 1;
+              } else {     // a GEMM depth block: summed from zero
+                c = 0.0f;
+              }
+              for (; i + 16 <= b1; i += 16) {
+                int qv[16];
+                float pv[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) qv[u] = 4 * lvix[i + u];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) pv[u] = rf[qv[u] + ra] * rf[qv[u] + rb];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) c = c + pv[u];
+              }
+              for (; i < b1; ++i) {
+                const int q = 4 * lvix[i];
+                c = c + rf[q + ra] * rf[q + rb];
+              }
+              if (!lazy) tot = tot + 1.0f * c;
+            }
+            sums[tid] = lazy ? c : tot;
+          }
+        } else if (Q > kLdsRows && tid < 12) {
           const int ra = tid < 9 ? tid % 3 : tid - 9, rb = tid < 9 ? tid / 3 : 3;
           const float* rf = reinterpret_cast<const float*>(rows);
           const int N = nvalid;
@@ -556,21 +634,34 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
           float tot = 0.0f, c = 0.0f;
           int cnt = 0;
           bool first = true;
-          for (int q = 0; q < Q; ++q) {
-            if (!vf[q]) continue;
-            const float pr = rf[4 * q + ra] * rf[4 * q + rb];
+          // branch-free: rows without a correspondence are selected out (never added), the
+          // products of 8 rows are formed before their in-order additions
+          auto add = [&](bool ok, float pr) {
             if (lazy) {
-              c = first ? pr : c + pr;
-              first = false;
+              c = ok ? (first ? pr : c + pr) : c;
+              first = first && !ok;
             } else {
-              c = c + pr;
-              if (++cnt == kc) {
-                tot = tot + 1.0f * c;
-                c = 0.0f;
-                cnt = 0;
-              }
+              const float cn = ok ? c + pr : c;
+              const int kn = cnt + (ok ? 1 : 0);
+              const bool fl = kn == kc;
+              tot = fl ? tot + 1.0f * cn : tot;
+              c = fl ? 0.0f : cn;
+              cnt = fl ? 0 : kn;
             }
+          };
+          int q = 0;
+          for (; q + 8 <= Q; q += 8) {
+            float pv[8];
+            bool ok[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              ok[u] = vf[q + u] != 0;
+              pv[u] = rf[4 * (q + u) + ra] * rf[4 * (q + u) + rb];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) add(ok[u], pv[u]);
           }
+          for (; q < Q; ++q) add(vf[q] != 0, rf[4 * q + ra] * rf[4 * q + rb]);
           sums[tid] = lazy ? c : (cnt ? tot + 1.0f * c : tot);
         }
         __syncthreads();
@@ -649,7 +740,7 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
     r.ms = 0.0f;
 #ifdef LLSR_S2S_PROF
     r.transform_cur[0] = (float)tAks; r.transform_cur[1] = (float)tAkc; r.transform_cur[2] = (float)tA;
-    r.transform_cur[3] = (float)tB; r.transform_cur[4] = (float)tC;
+    r.transform_cur[3] = (float)tB; r.transform_cur[4] = (float)tC; r.transform_cur[5] = (float)tF;
 #endif
     a.degen[p] = isDeg;
   }

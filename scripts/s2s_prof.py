@@ -1,7 +1,7 @@
 """Phase attribution of k_s2s_lm from the diagnostic build (make -C lego-loam-sr_amd prof): runs
 the odometry batch with LLSR_LIB=libllsr_prof.so and reports, over the slots, the mean per-problem
-wall time of phase A on the surf / corner kNN iterations, phase A otherwise, B (ordered sums)
-and C (solve), in us.
+wall time of the kNN search (shells / LDS scan + ring search) for surf / corner, the block
+scans for queries the shells left open, the Jacobian rows, B (ordered sums) and C (solve), in us.
 
     python scripts/s2s_prof.py [vlp16|hdl64e] [B]
 """
@@ -10,7 +10,7 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["LLSR_LIB"] = os.path.join(REPO, "lego-loam-sr_amd", "libllsr_prof.so")
+os.environ["LLSR_LIB"] = os.path.join(REPO, "lego-loam-sr_amd", os.environ.get("S2S_PROF_LIB", "libllsr_prof.so"))
 sys.path.insert(0, os.path.join(REPO, "lego-loam-sr_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -34,9 +34,9 @@ rows = []
 for b in range(0, B, max(1, B // 64)):
     f = pipe.odometry_fetch(b)
     t = f["lm"]["transform_cur"] / 100.0  # 100 MHz ticks -> us
-    rows.append(list(t[:5]) + [f["lm"]["surf_iterations"], f["lm"]["corner_iterations"]])
+    rows.append(list(t[:6]) + [f["lm"]["surf_iterations"], f["lm"]["corner_iterations"]])
 r = np.array(rows)
 print(json.dumps({"lidar": lidar, "B": B,
-                  "us_per_problem": dict(zip(["A_knn_surf", "A_knn_corner", "A", "B_sums", "C_solve"],
-                                             r[:, :5].mean(0).round(1).tolist())),
-                  "iterations": dict(zip(["surf", "corner"], r[:, 5:].mean(0).round(1).tolist()))}))
+                  "us_per_problem": dict(zip(["knn_surf", "knn_corner", "A_rows", "B_sums", "C_solve",
+                                              "knn_fallback"], r[:, :6].mean(0).round(1).tolist())),
+                  "iterations": dict(zip(["surf", "corner"], r[:, 6:].mean(0).round(1).tolist()))}))
