@@ -336,13 +336,50 @@ def odometry_leg(dev, lidar: str, B: int, seqs: int, frames: int, steps: int, wa
         dist.barrier()
     el = max_over_ranks(time.perf_counter() - t0, dev)
     world = dist.get_world_size() if dist else 1
+    # per-kernel device times (HIP events on the launch stream), after the timed region: the IP +
+    # feature kernels of llsr_process_batch and the scan-to-scan grid build + LM of the same step
+    pipe.set_profiling(True)
+    nprof = 2
+    for _ in range(nprof):
+        step()
+    torch.cuda.synchronize(dev)
+    kt = pipe.kernel_times()
+    st = pipe.scan2scan_stats()
+    pipe.set_profiling(False)
+    cnt = pipe.batch_counts(B)  # N, S, O, M, sharp, F, L, K of the last batch
+    # LM bytes per problem: every iteration reads each query (16 B) and writes its
+    # Jacobian row + residual (16 B); every 5th iteration also gathers the tripod (3 x 16 B) from
+    # the last clouds; the grids are rebuilt once per scan (32 B per last-cloud point)
+    reps = [pipe.odometry_fetch(b)["lm"] for b in range(0, B, max(1, B // 64))]
+    q_mean = float(np.mean(cnt[:, 4] + cnt[:, 5] + 160))
+    it_mean = float(np.mean([r["surf_iterations"] + r["corner_iterations"] for r in reps]))
+    lm_bytes = B * q_mean * (32.0 * it_mean + 48.0 * np.ceil(it_mean / 5.0))
+    lm_ms = st["lm_ms"] / max(1, st["batches"])
+    N = float(cnt[:, 0].sum())
+    proj_ms = kt["k_project"] + kt["k_gather_column"]
+    bpc_proj = 20 * N + (24 + 4 + 1) * float(H * W * B)
+    def roof(kname, nbytes, ms, note):
+        a = nbytes / (ms * 1e-3) / 1e9
+        return {"bound": "hbm", "kernel": kname, "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(a / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes_per_launch": nbytes,
+                "avg_launch_ms": round(ms, 4), "note": note}
     s0 = pipe.odometry_fetch(0)
     out = {"workload": f"{'configs[3]: HDL-64E 64x2048' if hdl else 'VLP-16 1800x16'} end-to-end odometry: "
                        "projection + segmentation + features + scan-to-scan LM + transformSum + last clouds, "
                        f"{B} sequences per GPU, one scan each per step",
            "value": round(B * steps * world / el, 1), "unit": "scans/s", "scaling": "weak",
            "sequences_per_gpu": B, "steps": steps, "ms_per_step": round(el / steps * 1e3, 3),
-           "slot0_frames": s0["frames"], "slot0_lm_iterations": [s0["lm"]["surf_iterations"], s0["lm"]["corner_iterations"]]}
+           "slot0_frames": s0["frames"], "slot0_lm_iterations": [s0["lm"]["surf_iterations"], s0["lm"]["corner_iterations"]],
+           "roofline": roof("k_s2s_lm", lm_bytes, lm_ms,
+                            "dominant kernel of the leg; bytes = queries x (32 B per iteration + 48 B tripod "
+                            "gather every 5th), latency-bound (one workgroup per scan, ordered sums)"),
+           "roofline_projection": roof("k_project" if not hdl else "k_project+k_gather_column", bpc_proj, proj_ms,
+                                       "SURVEY 8(d) B_pc projection part 20 N + 24 HW (+ 5 HW raw intensity "
+                                       "and ground) over the projection kernels"),
+           "kernels_ms_per_step": {**{k: round(v, 4) for k, v in kt.items()},
+                                   "s2s_grid_build": round(st["grid_ms"] / max(1, st["batches"]), 4),
+                                   "k_s2s_lm": round(lm_ms, 4)},
+           "lm_iterations_mean": it_mean, "lm_queries_mean": q_mean}
     if check:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle_py

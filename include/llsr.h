@@ -269,6 +269,16 @@ typedef struct llsr_s2m_stats {
   float iterate_ms;            /* first to last LM launch incl. the host's convergence polls, summed */
 } llsr_s2m_stats;
 int32_t llsr_scan2map_stats(llsr_handle* h, llsr_s2m_stats* out);
+/* Device time of the scan-to-scan batches (llsr_scan2scan_batch, and the LM inside
+ * llsr_odometry_batch) run since profiling was (re)enabled, from HIP events on the launch stream.
+ * Profiling syncs the stream after each batch. */
+typedef struct llsr_s2s_stats {
+  int32_t batches;
+  int32_t reserved;
+  float grid_ms; /* cell grids of the last clouds (kd-tree build, FA:2313-2314), summed */
+  float lm_ms;   /* k_s2s_lm: both LM phases of every problem (FA:2505-2535), summed */
+} llsr_s2s_stats;
+int32_t llsr_scan2scan_stats(llsr_handle* h, llsr_s2s_stats* out);
 /* ---- Split-correspondence scan-to-map for multi-GPU (BASELINE.json configs[4]) ----
  * The optimisation of llsr_scan2map_batch driven one LM iteration at a time, so that the
  * per-problem normal equations can be summed across GPUs between the Jacobian build and the

@@ -103,6 +103,8 @@ struct llsr_handle {
     size_t stage_bytes = 0;
     hipStream_t last = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipEvent_t p0 = nullptr, p1 = nullptr, p2 = nullptr;  // profiling: start, grids built, LM done
+    llsr_s2s_stats stats{};
   } s2s;
   // end-to-end odometry (llsr_odometry_*): per-slot FA state + packed clouds, allocated lazily
   struct {
@@ -371,6 +373,8 @@ extern "C" void llsr_destroy(llsr_handle* h) {
   if (h->s2s.host_flag) (void)hipHostFree(h->s2s.host_flag);
   if (h->s2s.e0) (void)hipEventDestroy(h->s2s.e0);
   if (h->s2s.e1) (void)hipEventDestroy(h->s2s.e1);
+  for (hipEvent_t e : {h->s2s.p0, h->s2s.p1, h->s2s.p2})
+    if (e) (void)hipEventDestroy(e);
   if (h->odo.pool) (void)hipFree(h->odo.pool);
   if (h->odo.h_off) (void)hipHostFree(h->odo.h_off);
   if (h->odo.h_counts) (void)hipHostFree(h->odo.h_counts);
@@ -448,6 +452,7 @@ extern "C" int32_t llsr_set_profiling(llsr_handle* h, int32_t enable) {
   for (double& v : h->ksum) v = 0.0;
   h->kbatches = 0;
   h->mo.stats = llsr_s2m_stats{};
+  h->s2s.stats = llsr_s2s_stats{};
   h->profiling = enable != 0;
   return LLSR_OK;
 }
@@ -472,7 +477,7 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   };
   mark();
   const bool fused = use_fused(h);
-  if (!fused) HIP_OK(h, hipMemsetAsync(h->d.cell_pt, 0xFF, sizeof(int) * (size_t)B * c.HW, s));
+  if (!fused) HIP_OK(h, hipMemsetAsync(h->d.ccl_a, 0xFF, sizeof(int) * (size_t)B * c.HW, s));
   k_init_counts<<<(B + 255) / 256, 256, 0, s>>>(h->d.counts, B);
   mark();
   if (fused) {  // fused projection + column ground pass with the cell table in LDS
@@ -482,7 +487,7 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   } else {
     k_project<<<dim3((h->max_points + 255) / 256, B), 256, 0, s>>>(c, pts, d_offsets, h->d);
     mark();
-    k_gather_column<<<dim3((c.W + 255) / 256, B), 256, 0, s>>>(c, pts, d_offsets, h->d);
+    k_gather_column<<<dim3((c.W + 63) / 64, B), 64, 0, s>>>(c, pts, d_offsets, h->d);
     mark();
   }
   k_ground_add<<<dim3((c.H + 3) / 4, B), 256, 0, s>>>(c, h->d);
@@ -1125,10 +1130,31 @@ extern "C" int32_t llsr_scan2scan_batch(llsr_handle* h, const llsr_s2s_batch* b,
   a.tcur = b->transform_cur;
   a.degen = b->is_degenerate;
   a.report = b->report;
+  if (h->profiling && !m.p0 &&
+      (hipEventCreate(&m.p0) != hipSuccess || hipEventCreate(&m.p1) != hipSuccess || hipEventCreate(&m.p2) != hipSuccess))
+    return fail(h, LLSR_ENODEV, "events");
+  if (h->profiling) HIP_OK(h, hipEventRecord(m.p0, s));
   grid_build(a.grids, s);
+  if (h->profiling) HIP_OK(h, hipEventRecord(m.p1, s));
   k_s2s_lm<<<P, 256, 0, s>>>(a);
   HIP_OK(h, hipGetLastError());
   m.last = s;
+  if (h->profiling) {
+    float g = 0.f, lm = 0.f;
+    HIP_OK(h, hipEventRecord(m.p2, s));
+    HIP_OK(h, hipEventSynchronize(m.p2));
+    HIP_OK(h, hipEventElapsedTime(&g, m.p0, m.p1));
+    HIP_OK(h, hipEventElapsedTime(&lm, m.p1, m.p2));
+    m.stats.batches += 1;
+    m.stats.grid_ms += g;
+    m.stats.lm_ms += lm;
+  }
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_scan2scan_stats(llsr_handle* h, llsr_s2s_stats* out) {
+  if (!h || !out) return LLSR_EINVAL;
+  *out = h->s2s.stats;
   return LLSR_OK;
 }
 

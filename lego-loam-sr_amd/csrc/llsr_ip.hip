@@ -108,6 +108,9 @@ __device__ __forceinline__ int project_cell_any(const DevCfg& c, float4 p, float
 // One thread per raw point; the serial "last writer wins" of IP:337-347 becomes atomicMax of
 // the raw index per cell (the compacted order preserves raw order). Also counts finite points
 // and the first/last finite index for findStartEndAngle (IP:430-436).
+// The winners go to a COLUMN-major scratch table (ccl_a, dead until k_label): Velodyne order
+// fires all rings of one azimuth back to back, so a wave's 64 atomics land in one or two 128-byte
+// lines instead of 64 (row-major: one line per ring). k_gather_column turns it row-major.
 // grid (ceil(maxN/256), B), block 256.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_project(DevCfg c, const float4* __restrict__ pts,
@@ -123,7 +126,10 @@ __global__ __launch_bounds__(256) void k_project(DevCfg c, const float4* __restr
       fin = finite3(p);
       if (fin) {
         const int cell = project_cell_any(c, p, 1.0f / c.ip_resY, 1.0f / c.ip_resX);
-        if (cell >= 0) atomicMax(&d.cell_pt[(size_t)b * c.HW + cell], (int)i);
+        if (cell >= 0) {
+          const int row = cell / c.W, col = cell - row * c.W;
+          atomicMax(&d.ccl_a[(size_t)b * c.HW + (size_t)col * c.H + row], (int)i);
+        }
       }
     }
     const unsigned long long m = __ballot(fin);
@@ -140,23 +146,35 @@ __global__ __launch_bounds__(256) void k_project(DevCfg c, const float4* __restr
 // ---------------------------------------------------------------------------------------------
 // K2 gather + ground column pass: builds range_mat/full_cloud for each cell (IP:337-347,
 // resetParameters IP:170-179) and runs groundRemovalOurs' per-column vector test and Filter
-// (IP:524-629) in the same sweep. One thread per (scan, column), rows bottom-up.
-// grid (ceil(W/256), B), block 256.
+// (IP:524-629) in the same sweep. One thread per (scan, column), rows bottom-up; the column's
+// winners are read from k_project's column-major table four rows per 16-byte load, and the
+// row-major cell->point map is written here.
+// grid (ceil(W/64), B), block 64.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_gather_column(DevCfg c, const float4* __restrict__ pts,
-                                                       const int64_t* __restrict__ off, DevBufs d) {
+__global__ __launch_bounds__(64) void k_gather_column(DevCfg c, const float4* __restrict__ pts,
+                                                      const int64_t* __restrict__ off, DevBufs d) {
   const int b = blockIdx.y;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= c.W) return;
   const int64_t o0 = off[b];
   const size_t base = (size_t)b * c.HW;
+  const int* colw = d.ccl_a + base + (size_t)j * c.H;  // this column's winners, row 0 first
+  const bool vec4 = (c.H & 3) == 0;                      // 16-byte aligned column runs
   const float qnan = __builtin_nanf("");
   bool haveRV = false, obs = false;
   float RVx = 0.f, RVy = 0.f, RVz = 0.f;
   float lx = 0.f, ly = 0.f, lz = 0.f;
+  int4 w4 = make_int4(-1, -1, -1, -1);
   for (int i = 0; i < c.H; ++i) {
     const int cell = j + i * c.W;
-    const int pi = d.cell_pt[base + cell];
+    int pi;
+    if (vec4) {
+      if ((i & 3) == 0) w4 = *reinterpret_cast<const int4*>(colw + i);
+      pi = (i & 3) == 0 ? w4.x : (i & 3) == 1 ? w4.y : (i & 3) == 2 ? w4.z : w4.w;
+    } else {
+      pi = colw[i];
+    }
+    d.cell_pt[base + cell] = pi;
     float4 f;
     float rng, vis;
     if (pi >= 0) {

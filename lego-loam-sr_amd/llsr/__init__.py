@@ -33,7 +33,7 @@ EXPORTS = [
     "llsr_config_default", "llsr_create", "llsr_destroy", "llsr_last_error", "llsr_query_sizes",
     "llsr_reset_state", "llsr_process_scan", "llsr_process_batch", "llsr_fetch_scan",
     "llsr_batch_counts", "llsr_kernel_times_ms", "llsr_kernel_name", "llsr_set_profiling",
-    "llsr_scan2map_reserve", "llsr_scan2map_batch", "llsr_scan2map", "llsr_scan2map_stats",
+    "llsr_scan2map_reserve", "llsr_scan2map_batch", "llsr_scan2map", "llsr_scan2map_stats", "llsr_scan2scan_stats",
     "llsr_shadow_points", "llsr_scan2scan_reserve", "llsr_scan2scan_batch", "llsr_scan2scan_check",
     "llsr_scan2scan", "llsr_scan2map_shard_begin", "llsr_scan2map_shard_partial",
     "llsr_scan2map_shard_step", "llsr_scan2map_shard_end", "llsr_odometry_batch", "llsr_odometry_fetch",
@@ -76,6 +76,7 @@ def lib():
         L.llsr_scan2map_reserve.argtypes = [C.c_void_p] + [C.c_int32] * 5
         L.llsr_scan2map_batch.argtypes = [C.c_void_p, C.POINTER(_abi.S2MBatch), C.c_void_p]
         L.llsr_scan2map_stats.argtypes = [C.c_void_p, C.POINTER(_abi.S2MStats)]
+        L.llsr_scan2scan_stats.argtypes = [C.c_void_p, C.POINTER(_abi.S2SStats)]
         L.llsr_shadow_points.argtypes = [C.c_void_p]
         L.llsr_scan2scan_reserve.argtypes = [C.c_void_p] + [C.c_int32] * 5
         L.llsr_scan2scan_batch.argtypes = [C.c_void_p, C.POINTER(_abi.S2SBatch), C.c_void_p]
@@ -269,6 +270,11 @@ class Pipeline:
         self._check(lib().llsr_scan2map_stats(self._h, C.byref(st)), "llsr_scan2map_stats")
         return {k: getattr(st, k) for k, _ in st._fields_}
 
+
+    def scan2scan_stats(self) -> dict:
+        st = _abi.S2SStats()
+        self._check(lib().llsr_scan2scan_stats(self._h, C.byref(st)), "llsr_scan2scan_stats")
+        return {k: getattr(st, k) for k, _ in st._fields_}
 
     # ---- scan-to-scan (FeatureAssociation::updateTransformation) ------------------------------
     def scan2scan_reserve(self, problems: int, sharp: int, flat: int, corner_last: int, surf_last: int):

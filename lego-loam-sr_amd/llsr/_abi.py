@@ -204,6 +204,10 @@ class S2MStats(C.Structure):
                 ("iterate_ms", C.c_float)]
 
 
+class S2SStats(C.Structure):
+    _fields_ = [("batches", C.c_int32), ("reserved", C.c_int32), ("grid_ms", C.c_float), ("lm_ms", C.c_float)]
+
+
 class MapConfig(C.Structure):
     """llsr_map_config (include/llsr.h): MapOptimization's local-map parameters."""
     _fields_ = [("surrounding_radius", C.c_float), ("keypose_leaf", C.c_float), ("corner_leaf", C.c_float),
