@@ -1136,7 +1136,7 @@ extern "C" int32_t llsr_scan2scan_batch(llsr_handle* h, const llsr_s2s_batch* b,
   if (h->profiling) HIP_OK(h, hipEventRecord(m.p0, s));
   grid_build(a.grids, s);
   if (h->profiling) HIP_OK(h, hipEventRecord(m.p1, s));
-  k_s2s_lm<<<P, 256, 0, s>>>(a);
+  k_s2s_lm<<<P, kS2SThreads, 0, s>>>(a);
   HIP_OK(h, hipGetLastError());
   m.last = s;
   if (h->profiling) {

@@ -1,10 +1,10 @@
 // llsr_fa_lm.hip — FeatureAssociation scan-to-scan LM on gfx950 (updateTransformation,
 // featureAssociation.cpp:2505-2535) for a batch of independent scans.
 //
-// k_s2s_lm: one 256-thread workgroup per scan runs the whole two-phase optimisation in-kernel
+// k_s2s_lm: one kS2SThreads-thread workgroup per scan runs the whole two-phase optimisation in-kernel
 // (no host round trips): surf phase (FA:2508-2516) then corner phase (FA:2519-2527), each up to
 // 100 iterations. Per iteration:
-//   A  on iterations % 5 == 0 the kNN-1 of every query (q = tid, tid + 256, ...) after
+//   A  on iterations % 5 == 0 the kNN-1 of every query (q = tid, tid + kThreads, ...) after
 //      TransformToStart (FA:1389-1412) in the last cloud: the sparse corner cloud is scanned from
 //      LDS, the surf cloud searched over shells of its 1 m cell grid (llsr_grid.h), and queries
 //      the shells leave open are resolved by a block-wide scan; then the ring-constrained scans
@@ -39,7 +39,7 @@ using llsr_libm::sqrt_;
 
 namespace {
 
-constexpr int kThreads = 256;
+constexpr int kThreads = kS2SThreads;
 constexpr int kMaxShell = 2;  // grid shells searched before the exact block-wide scan (queries in sparse regions)
 constexpr int kLdsRows = 2048;    // Jacobian rows kept in LDS (32 KB); larger phases use the HBM buffer
 constexpr int kLdsCorner = 2048;  // laserCloudCornerLast kept in LDS (32 KB) for a brute-force kNN-1
