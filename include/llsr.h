@@ -455,6 +455,46 @@ int32_t llsr_mapping_associate(const float transform_sum_fa[6], const float tran
                                float transform_tobe_mapped[6], float transform_incre[6]);
 
 
+/* ---- TransformFusion (transformFusion.cpp) ----
+ * The fourth node of the reference fuses the 10 Hz scan-to-scan odometry with the slower mapped
+ * pose. It is scalar host work per message, so these entry points run on the host side of the
+ * library (no device, no handle), with the reference's float / double typing: tf2's
+ * Quaternion::setRPY / Matrix3x3::getRPY in double, transformAssociateToMap on floats (the same
+ * routine as MO:458-581, TF:65-186). The odometry messages carry the nav_msgs/Odometry fields the
+ * nodes read and write. */
+typedef struct llsr_odometry_msg {
+  double orientation[4];    /* pose.pose.orientation x, y, z, w */
+  double position[3];       /* pose.pose.position */
+  double twist_angular[3];  /* twist.twist.angular (MO's transformBefMapped[0..2]) */
+  double twist_linear[3];   /* twist.twist.linear (MO's transformBefMapped[3..5]) */
+} llsr_odometry_msg;
+typedef struct llsr_fusion_state {  /* TransformFusion's members (transformFusion.h) */
+  float transform_sum[6];
+  float transform_incre[6];
+  float transform_mapped[6];
+  float transform_bef_mapped[6];
+  float transform_aft_mapped[6];
+} llsr_fusion_state;
+/* The constructor's zeros (TF:51-57). */
+int32_t llsr_fusion_init(llsr_fusion_state* st);
+/* How the publishers encode a pose: orientation = (-q.y, -q.z, q.x, q.w) of
+ * setRPY(pose[2], -pose[0], -pose[1]), position = pose[3..5]; twist = twist6 (NULL: zeros).
+ * FeatureAssociation::publishOdometry (FA:2612-2625: transformSum, no twist),
+ * MapOptimization::publishTF (MO:704-723: transformAftMapped, twist = transformBefMapped),
+ * TransformFusion's /integrated_to_init (TF:193-206: transformMapped, no twist). */
+int32_t llsr_pose_to_odometry(const float pose[6], const float twist6[6], llsr_odometry_msg* out);
+/* OdometryToTransform (UT:99-113): getRPY of Quaternion(o.z, -o.x, -o.y, o.w) -> (-pitch, -yaw,
+ * roll), position. */
+int32_t llsr_odometry_to_transform(const llsr_odometry_msg* in, float transform[6]);
+/* TransformFusion::laserOdometryHandler (TF:188-280): transform_sum from /laser_odom_to_init,
+ * transformAssociateToMap, and the /integrated_to_init message (also the camera_init -> camera tf,
+ * same rotation and translation). */
+int32_t llsr_fusion_laser_odometry(llsr_fusion_state* st, const llsr_odometry_msg* laser_odometry,
+                                   llsr_odometry_msg* integrated);
+/* TransformFusion::odomAftMappedHandler (TF:282-304): transform_aft_mapped from the pose (getRPY
+ * of Quaternion(o.z, -o.x, -o.y, o.w) -> -pitch, -yaw, roll), transform_bef_mapped from the twist. */
+int32_t llsr_fusion_aft_mapped(llsr_fusion_state* st, const llsr_odometry_msg* odom_aft_mapped);
+
 /* ---- Input wire formats (llsr_input.hip) ----
  * sensor_msgs/PointCloud2 (PointField datatype codes, sensor_msgs/msg/PointField.msg) decoded as
  * pcl::fromROSMsg<PointXYZI> (IP:196): x, y, z, intensity are taken from the fields of that name

@@ -1767,3 +1767,55 @@ extern "C" int32_t llsr_mapping_associate(const float* ts_fa, const float* bef, 
   }
   return LLSR_OK;
 }
+
+// ---- TransformFusion (transformFusion.cpp, TF:65-304): host-side scalar glue ----------------
+extern "C" int32_t llsr_fusion_init(llsr_fusion_state* st) {
+  if (!st) return LLSR_EINVAL;
+  std::memset(st, 0, sizeof *st);
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_pose_to_odometry(const float* pose, const float* twist6, llsr_odometry_msg* out) {
+  if (!pose || !out) return LLSR_EINVAL;
+  llsr_mapping::pose_to_odometry(pose, twist6, *out);
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_odometry_to_transform(const llsr_odometry_msg* in, float* transform) {
+  if (!in || !transform) return LLSR_EINVAL;
+  llsr_mapping::odometry_to_transform(*in, transform);
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_fusion_laser_odometry(llsr_fusion_state* st, const llsr_odometry_msg* laser_odometry,
+                                              llsr_odometry_msg* integrated) {
+  if (!st || !laser_odometry || !integrated) return LLSR_EINVAL;
+  // TF:190-192: OdometryToTransform, then transformAssociateToMap (TF:65-186 = MO:458-581 with
+  // transformMapped in place of transformTobeMapped)
+  llsr_mapping::MoPoses P;
+  llsr_mapping::odometry_to_transform(*laser_odometry, P.transformSum);
+  for (int k = 0; k < 6; ++k) {
+    P.transformBefMapped[k] = st->transform_bef_mapped[k];
+    P.transformAftMapped[k] = st->transform_aft_mapped[k];
+    P.transformIncre[k] = st->transform_incre[k];
+  }
+  llsr_mapping::transform_associate_to_map(P);
+  for (int k = 0; k < 6; ++k) {
+    st->transform_sum[k] = P.transformSum[k];
+    st->transform_incre[k] = P.transformIncre[k];
+    st->transform_mapped[k] = P.transformTobeMapped[k];
+  }
+  // TF:194-206: q.setRPY(mapped[2], -mapped[0], -mapped[1]); /integrated_to_init
+  llsr_mapping::pose_to_odometry(st->transform_mapped, nullptr, *integrated);
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_fusion_aft_mapped(llsr_fusion_state* st, const llsr_odometry_msg* m) {
+  if (!st || !m) return LLSR_EINVAL;
+  llsr_mapping::odometry_to_transform(*m, st->transform_aft_mapped);  // TF:284-297: -pitch, -yaw, roll, position
+  for (int k = 0; k < 3; ++k) {                                       // TF:299-304
+    st->transform_bef_mapped[k] = (float)m->twist_angular[k];
+    st->transform_bef_mapped[3 + k] = (float)m->twist_linear[k];
+  }
+  return LLSR_OK;
+}

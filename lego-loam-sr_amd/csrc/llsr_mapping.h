@@ -29,12 +29,16 @@ int32_t voxel_multi(llsr_map* m, const float4* const* src, const long long* n, c
 int32_t extract_multi(llsr_map* eng, llsr_map* const* maps, int n, const float* pos, llsr_map_report* reps,
                       const float4** out, long long* off_c, long long* off_s, hipStream_t s);
 
-// tf2::Quaternion::setRPY (tf2/LinearMath/Quaternion.h), double
+// tf2::Quaternion::setRPY (tf2/LinearMath/Quaternion.h), double. The reference's GCC -O3 build
+// merges each tf2Cos(a) / tf2Sin(a) pair into one glibc sincos(a) call (GCC's sincos pass), and
+// glibc's sincos can differ from separate sin / cos in the last bit (e.g. q.w of setRPY(0.963,
+// -2.970, 1.414) by 2 ulps); clang does not merge, so the call is written out.
 inline void tf2_set_rpy(double roll, double pitch, double yaw, double q[4]) {
   const double halfYaw = yaw * 0.5, halfPitch = pitch * 0.5, halfRoll = roll * 0.5;
-  const double cosYaw = std::cos(halfYaw), sinYaw = std::sin(halfYaw);
-  const double cosPitch = std::cos(halfPitch), sinPitch = std::sin(halfPitch);
-  const double cosRoll = std::cos(halfRoll), sinRoll = std::sin(halfRoll);
+  double cosYaw, sinYaw, cosPitch, sinPitch, cosRoll, sinRoll;
+  ::sincos(halfYaw, &sinYaw, &cosYaw);
+  ::sincos(halfPitch, &sinPitch, &cosPitch);
+  ::sincos(halfRoll, &sinRoll, &cosRoll);
   q[0] = sinRoll * cosPitch * cosYaw - cosRoll * sinPitch * sinYaw;
   q[1] = cosRoll * sinPitch * cosYaw + sinRoll * cosPitch * sinYaw;
   q[2] = cosRoll * cosPitch * sinYaw - sinRoll * sinPitch * cosYaw;
@@ -79,6 +83,32 @@ inline void odometry_roundtrip(const float ts[6], float out[6]) {
   out[3] = (float)(double)ts[3];  // position.x/y/z: float -> double -> float
   out[4] = (float)(double)ts[4];
   out[5] = (float)(double)ts[5];
+}
+
+// the publishers' pose -> nav_msgs/Odometry encoding (FA:2612-2625, MO:704-723, TF:193-206)
+inline void pose_to_odometry(const float pose[6], const float* twist6, llsr_odometry_msg& m) {
+  double q[4];
+  tf2_set_rpy((double)pose[2], -(double)pose[0], -(double)pose[1], q);  // float args -> double
+  m.orientation[0] = -q[1];
+  m.orientation[1] = -q[2];
+  m.orientation[2] = q[0];
+  m.orientation[3] = q[3];
+  for (int k = 0; k < 3; ++k) {
+    m.position[k] = (double)pose[3 + k];
+    m.twist_angular[k] = twist6 ? (double)twist6[k] : 0.0;
+    m.twist_linear[k] = twist6 ? (double)twist6[3 + k] : 0.0;
+  }
+}
+
+// OdometryToTransform (UT:99-113)
+inline void odometry_to_transform(const llsr_odometry_msg& m, float t[6]) {
+  const double q2[4] = {m.orientation[2], -m.orientation[0], -m.orientation[1], m.orientation[3]};
+  double roll, pitch, yaw;
+  tf2_get_rpy(q2, roll, pitch, yaw);
+  t[0] = (float)(-pitch);
+  t[1] = (float)(-yaw);
+  t[2] = (float)roll;
+  for (int k = 0; k < 3; ++k) t[3 + k] = (float)m.position[k];
 }
 
 // MapOptimization's pose members (mapOptimization.h), one sequence

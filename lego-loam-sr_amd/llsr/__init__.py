@@ -33,7 +33,7 @@ EXPORTS = [
     "llsr_config_default", "llsr_create", "llsr_destroy", "llsr_last_error", "llsr_query_sizes",
     "llsr_reset_state", "llsr_process_scan", "llsr_process_batch", "llsr_fetch_scan",
     "llsr_batch_counts", "llsr_kernel_times_ms", "llsr_kernel_name", "llsr_set_profiling",
-    "llsr_scan2map_reserve", "llsr_scan2map_batch", "llsr_scan2map", "llsr_scan2map_stats", "llsr_scan2scan_stats",
+    "llsr_scan2map_reserve", "llsr_scan2map_batch", "llsr_scan2map", "llsr_scan2map_stats",
     "llsr_shadow_points", "llsr_scan2scan_reserve", "llsr_scan2scan_batch", "llsr_scan2scan_check",
     "llsr_scan2scan", "llsr_scan2map_shard_begin", "llsr_scan2map_shard_partial",
     "llsr_scan2map_shard_step", "llsr_scan2map_shard_end", "llsr_odometry_batch", "llsr_odometry_fetch",
@@ -42,7 +42,8 @@ EXPORTS = [
     "llsr_map_add_keyframe", "llsr_map_num_keyframes", "llsr_map_extract", "llsr_map_keyframe_ids",
     "llsr_decode_pointcloud2", "llsr_kitti_count", "llsr_kitti_read", "llsr_kitti_load",
     "llsr_mapping_init", "llsr_mapping_batch", "llsr_mapping_fetch", "llsr_mapping_keyposes", "llsr_mapping_reset",
-    "llsr_mapping_associate", "llsr_set_voxel_order",
+    "llsr_mapping_associate", "llsr_set_voxel_order", "llsr_scan2scan_stats", "llsr_fusion_init",
+    "llsr_pose_to_odometry", "llsr_odometry_to_transform", "llsr_fusion_laser_odometry", "llsr_fusion_aft_mapped",
 ]
 
 
@@ -77,6 +78,12 @@ def lib():
         L.llsr_scan2map_batch.argtypes = [C.c_void_p, C.POINTER(_abi.S2MBatch), C.c_void_p]
         L.llsr_scan2map_stats.argtypes = [C.c_void_p, C.POINTER(_abi.S2MStats)]
         L.llsr_scan2scan_stats.argtypes = [C.c_void_p, C.POINTER(_abi.S2SStats)]
+        L.llsr_fusion_init.argtypes = [C.POINTER(_abi.FusionState)]
+        L.llsr_pose_to_odometry.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(_abi.OdometryMsg)]
+        L.llsr_odometry_to_transform.argtypes = [C.POINTER(_abi.OdometryMsg), C.c_void_p]
+        L.llsr_fusion_laser_odometry.argtypes = [C.POINTER(_abi.FusionState), C.POINTER(_abi.OdometryMsg),
+                                                 C.POINTER(_abi.OdometryMsg)]
+        L.llsr_fusion_aft_mapped.argtypes = [C.POINTER(_abi.FusionState), C.POINTER(_abi.OdometryMsg)]
         L.llsr_shadow_points.argtypes = [C.c_void_p]
         L.llsr_scan2scan_reserve.argtypes = [C.c_void_p] + [C.c_int32] * 5
         L.llsr_scan2scan_batch.argtypes = [C.c_void_p, C.POINTER(_abi.S2SBatch), C.c_void_p]
@@ -374,6 +381,73 @@ def mapping_associate(transform_sum_fa, bef, aft):
     if rc != 0:
         raise LlsrError(f"llsr_mapping_associate: {rc}")
     return tuple(out)
+
+
+def _msg_to_array(m: "_abi.OdometryMsg") -> np.ndarray:
+    return np.array(list(m.orientation) + list(m.position) + list(m.twist_angular) + list(m.twist_linear),
+                    np.float64)
+
+
+def _array_to_msg(a) -> "_abi.OdometryMsg":
+    a = np.asarray(a, np.float64)
+    m = _abi.OdometryMsg()
+    m.orientation[:] = a[0:4].tolist()
+    m.position[:] = a[4:7].tolist()
+    m.twist_angular[:] = a[7:10].tolist()
+    m.twist_linear[:] = a[10:13].tolist()
+    return m
+
+
+def pose_to_odometry(pose, twist=None) -> np.ndarray:
+    """The publishers' pose -> nav_msgs/Odometry encoding (llsr_pose_to_odometry: FA:2612-2625,
+    MO:704-723, TF:193-206), as 13 doubles: orientation xyzw, position, twist angular, twist linear."""
+    p = np.ascontiguousarray(pose, np.float32)
+    t = None if twist is None else np.ascontiguousarray(twist, np.float32)
+    m = _abi.OdometryMsg()
+    rc = lib().llsr_pose_to_odometry(p.ctypes.data, None if t is None else t.ctypes.data, C.byref(m))
+    if rc != 0:
+        raise LlsrError(f"llsr_pose_to_odometry: {rc}")
+    return _msg_to_array(m)
+
+
+def odometry_to_transform(msg) -> np.ndarray:
+    """OdometryToTransform (UT:99-113) of a 13-double odometry message."""
+    out = np.zeros(6, np.float32)
+    m = _array_to_msg(msg)
+    rc = lib().llsr_odometry_to_transform(C.byref(m), out.ctypes.data)
+    if rc != 0:
+        raise LlsrError(f"llsr_odometry_to_transform: {rc}")
+    return out
+
+
+class TransformFusion:
+    """The TransformFusion node's arithmetic (transformFusion.cpp) over the C-ABI's host entry points:
+    `laser_odometry_handler(msg)` takes /laser_odom_to_init and returns /integrated_to_init (TF:188-280),
+    `odom_aft_mapped_handler(msg)` takes /aft_mapped_to_init (TF:282-304). Messages are 13 doubles."""
+
+    def __init__(self):
+        self.state = _abi.FusionState()
+        rc = lib().llsr_fusion_init(C.byref(self.state))
+        if rc != 0:
+            raise LlsrError(f"llsr_fusion_init: {rc}")
+
+    def laser_odometry_handler(self, msg) -> np.ndarray:
+        m, out = _array_to_msg(msg), _abi.OdometryMsg()
+        rc = lib().llsr_fusion_laser_odometry(C.byref(self.state), C.byref(m), C.byref(out))
+        if rc != 0:
+            raise LlsrError(f"llsr_fusion_laser_odometry: {rc}")
+        return _msg_to_array(out)
+
+    def odom_aft_mapped_handler(self, msg):
+        m = _array_to_msg(msg)
+        rc = lib().llsr_fusion_aft_mapped(C.byref(self.state), C.byref(m))
+        if rc != 0:
+            raise LlsrError(f"llsr_fusion_aft_mapped: {rc}")
+
+    def state_array(self) -> np.ndarray:
+        """transformSum, transformIncre, transformMapped, transformBefMapped, transformAftMapped."""
+        st = self.state
+        return np.concatenate([np.array(getattr(st, f), np.float32) for f, _ in st._fields_])
 
 
 def shadow_points() -> np.ndarray:

@@ -208,6 +208,19 @@ class S2SStats(C.Structure):
     _fields_ = [("batches", C.c_int32), ("reserved", C.c_int32), ("grid_ms", C.c_float), ("lm_ms", C.c_float)]
 
 
+class OdometryMsg(C.Structure):
+    """llsr_odometry_msg: the nav_msgs/Odometry fields the nodes use."""
+    _fields_ = [("orientation", C.c_double * 4), ("position", C.c_double * 3),
+                ("twist_angular", C.c_double * 3), ("twist_linear", C.c_double * 3)]
+
+
+class FusionState(C.Structure):
+    """llsr_fusion_state: TransformFusion's members (transformFusion.h)."""
+    _fields_ = [("transform_sum", C.c_float * 6), ("transform_incre", C.c_float * 6),
+                ("transform_mapped", C.c_float * 6), ("transform_bef_mapped", C.c_float * 6),
+                ("transform_aft_mapped", C.c_float * 6)]
+
+
 class MapConfig(C.Structure):
     """llsr_map_config (include/llsr.h): MapOptimization's local-map parameters."""
     _fields_ = [("surrounding_radius", C.c_float), ("keypose_leaf", C.c_float), ("corner_leaf", C.c_float),

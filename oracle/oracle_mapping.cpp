@@ -24,12 +24,12 @@ Quat set_rpy(double roll, double pitch, double yaw) {
   const double halfYaw = yaw * 0.5;
   const double halfPitch = pitch * 0.5;
   const double halfRoll = roll * 0.5;
-  const double cosYaw = ::cos(halfYaw);
-  const double sinYaw = ::sin(halfYaw);
-  const double cosPitch = ::cos(halfPitch);
-  const double sinPitch = ::sin(halfPitch);
-  const double cosRoll = ::cos(halfRoll);
-  const double sinRoll = ::sin(halfRoll);
+  // tf2Cos / tf2Sin of one angle: GCC -O3 (the reference's build) emits one glibc sincos call for
+  // each pair; written out so the statement does not depend on this build's optimiser
+  double cosYaw, sinYaw, cosPitch, sinPitch, cosRoll, sinRoll;
+  ::sincos(halfYaw, &sinYaw, &cosYaw);
+  ::sincos(halfPitch, &sinPitch, &cosPitch);
+  ::sincos(halfRoll, &sinRoll, &cosRoll);
   Quat q;
   q.x = sinRoll * cosPitch * cosYaw - cosRoll * sinPitch * sinYaw;
   q.y = cosRoll * sinPitch * cosYaw + sinRoll * cosPitch * sinYaw;
@@ -170,4 +170,67 @@ extern "C" void oracle_associate_to_map(const float* transformSum, const float* 
   tobe[3] = aft[3] - (cos(tobe[1]) * x2 + sin(tobe[1]) * z2);
   tobe[4] = aft[4] - y2;
   tobe[5] = aft[5] - (-sin(tobe[1]) * x2 + cos(tobe[1]) * z2);
+}
+
+// ---- TransformFusion (transformFusion.cpp) — the node's two handlers, one statement per line ----
+// Messages are 13 doubles: orientation x, y, z, w; position x, y, z; twist angular x, y, z; twist
+// linear x, y, z. The state is TransformFusion's members, 5 x 6 floats: transformSum,
+// transformIncre, transformMapped, transformBefMapped, transformAftMapped.
+
+// the publishers' encoding: FA:2612-2625 (transformSum), MO:704-723 (transformAftMapped, twist =
+// transformBefMapped), TF:193-206 (transformMapped)
+extern "C" void oracle_pose_to_odometry(const float* pose, const float* twist, double* msg) {
+  const Quat q = set_rpy(pose[2], -pose[0], -pose[1]);
+  msg[0] = -q.y;  // orientation.x = -geoQuat.y
+  msg[1] = -q.z;
+  msg[2] = q.x;
+  msg[3] = q.w;
+  msg[4] = pose[3];
+  msg[5] = pose[4];
+  msg[6] = pose[5];
+  for (int k = 0; k < 6; ++k) msg[7 + k] = twist ? twist[k] : 0.0;
+}
+
+// OdometryToTransform (utility.h:99-113)
+static void odometry_to_transform_msg(const double* msg, float* transform) {
+  double roll, pitch, yaw;
+  get_rpy(Quat{msg[2], -msg[0], -msg[1], msg[3]}, roll, pitch, yaw);
+  transform[0] = -pitch;
+  transform[1] = -yaw;
+  transform[2] = roll;
+  transform[3] = msg[4];
+  transform[4] = msg[5];
+  transform[5] = msg[6];
+}
+
+// TransformFusion::laserOdometryHandler (TF:188-208)
+extern "C" void oracle_fusion_laser_odometry(float* st, const double* laserOdometry, double* laserOdometry2) {
+  float* transformSum = st;
+  float* transformIncre = st + 6;
+  float* transformMapped = st + 12;
+  float* transformBefMapped = st + 18;
+  float* transformAftMapped = st + 24;
+  odometry_to_transform_msg(laserOdometry, transformSum);
+  oracle_associate_to_map(transformSum, transformBefMapped, transformAftMapped, transformMapped, transformIncre);
+  oracle_pose_to_odometry(transformMapped, nullptr, laserOdometry2);
+}
+
+// TransformFusion::odomAftMappedHandler (TF:282-304)
+extern "C" void oracle_fusion_aft_mapped(float* st, const double* odomAftMapped) {
+  float* transformBefMapped = st + 18;
+  float* transformAftMapped = st + 24;
+  double roll, pitch, yaw;
+  get_rpy(Quat{odomAftMapped[2], -odomAftMapped[0], -odomAftMapped[1], odomAftMapped[3]}, roll, pitch, yaw);
+  transformAftMapped[0] = -pitch;
+  transformAftMapped[1] = -yaw;
+  transformAftMapped[2] = roll;
+  transformAftMapped[3] = odomAftMapped[4];
+  transformAftMapped[4] = odomAftMapped[5];
+  transformAftMapped[5] = odomAftMapped[6];
+  transformBefMapped[0] = odomAftMapped[7];
+  transformBefMapped[1] = odomAftMapped[8];
+  transformBefMapped[2] = odomAftMapped[9];
+  transformBefMapped[3] = odomAftMapped[10];
+  transformBefMapped[4] = odomAftMapped[11];
+  transformBefMapped[5] = odomAftMapped[12];
 }

@@ -81,6 +81,9 @@ def lib():
             [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(_abi.LmReport)]
         L.oracle_odometry_to_transform.argtypes = [C.c_void_p, C.c_void_p]
         L.oracle_associate_to_map.argtypes = [C.c_void_p] * 5
+        L.oracle_pose_to_odometry.argtypes = [C.c_void_p] * 3
+        L.oracle_fusion_laser_odometry.argtypes = [C.c_void_p] * 3
+        L.oracle_fusion_aft_mapped.argtypes = [C.c_void_p] * 2
         _LIB = L
     return _LIB
 
@@ -513,6 +516,33 @@ def odometry_to_transform(transform_sum_fa) -> np.ndarray:
     out = np.zeros(6, np.float32)
     lib().oracle_odometry_to_transform(t.ctypes.data, out.ctypes.data)
     return out
+
+
+def pose_to_odometry(pose, twist=None) -> np.ndarray:
+    """The publishers' pose -> nav_msgs/Odometry encoding (FA:2612-2625, MO:704-723, TF:193-206):
+    13 doubles (orientation xyzw, position, twist angular, twist linear)."""
+    p = np.ascontiguousarray(pose, np.float32)
+    t = None if twist is None else np.ascontiguousarray(twist, np.float32)
+    out = np.zeros(13, np.float64)
+    lib().oracle_pose_to_odometry(p.ctypes.data, None if t is None else t.ctypes.data, out.ctypes.data)
+    return out
+
+
+class OracleTransformFusion:
+    """TransformFusion (transformFusion.cpp): state = 5 x 6 floats (sum, incre, mapped, bef, aft)."""
+
+    def __init__(self):
+        self.state = np.zeros(30, np.float32)
+
+    def laser_odometry(self, msg: np.ndarray) -> np.ndarray:
+        m = np.ascontiguousarray(msg, np.float64)
+        out = np.zeros(13, np.float64)
+        lib().oracle_fusion_laser_odometry(self.state.ctypes.data, m.ctypes.data, out.ctypes.data)
+        return out
+
+    def aft_mapped(self, msg: np.ndarray):
+        m = np.ascontiguousarray(msg, np.float64)
+        lib().oracle_fusion_aft_mapped(self.state.ctypes.data, m.ctypes.data)
 
 
 class OracleMapping:
