@@ -80,6 +80,16 @@ def cpu_baseline(scans: list[np.ndarray], budget_s: float) -> dict:
             "ip_ms": ip_ms / n, "fa_features_ms": fa_ms / n}
 
 
+def lm_traffic(kernel: str, problems: int):
+    """PMC-measured HBM bytes per launch of an LM kernel (scripts/pmc_lm.sh, committed as
+    profiles/traffic_lm_latest.json), or None when it was measured at another batch size."""
+    f = os.environ.get("LLSR_TRAFFIC_LM_JSON", os.path.join(REPO, "profiles", "traffic_lm_latest.json"))
+    if not os.path.exists(f):
+        return None
+    rec = json.load(open(f)).get("kernels", {}).get(kernel)
+    return rec["hbm_bytes_per_launch"] if rec and rec.get("problems") == problems else None
+
+
 def s2m_bytes_per_iteration(Qc: int, Qs: int, blocks: int) -> float:
     """query 16 B + 5 neighbours x 16 B per query, 29 partial words per block."""
     return 96.0 * (Qc + Qs) + 116.0 * blocks
@@ -178,9 +188,12 @@ def scan2map_leg(dev, mode_name: str, P: int, steps: int, warmup: int, dist, run
         "k_s2m_iter_launches_per_step": launches_per_batch,
         "roofline": {"bound": "hbm", "kernel": "k_s2m_iter", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None, "algorithmic_bytes_per_step": lm_bytes,
+                     "traffic": lm_traffic("k_s2m_iter", P), "algorithmic_bytes_per_step": lm_bytes,
+                     "algorithmic_bytes_per_launch": lm_bytes / max(1, launches_per_batch),
                      "avg_launch_ms": round(per_launch_ms, 4),
-                     "note": "iterate window includes the host's convergence polls (every 4 launches)"},
+                     "note": "iterate window includes the host's convergence polls (every 4 launches); "
+                             "traffic = PMC HBM bytes per launch: the kNN-5 walks of 27 cells per query "
+                             "read far more than the 96 B per query of SURVEY 8(d)"},
     }
     if run_cpu:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -370,9 +383,11 @@ def odometry_leg(dev, lidar: str, B: int, seqs: int, frames: int, steps: int, wa
            "value": round(B * steps * world / el, 1), "unit": "scans/s", "scaling": "weak",
            "sequences_per_gpu": B, "steps": steps, "ms_per_step": round(el / steps * 1e3, 3),
            "slot0_frames": s0["frames"], "slot0_lm_iterations": [s0["lm"]["surf_iterations"], s0["lm"]["corner_iterations"]],
-           "roofline": roof("k_s2s_lm", lm_bytes, lm_ms,
-                            "dominant kernel of the leg; bytes = queries x (32 B per iteration + 48 B tripod "
-                            "gather every 5th), latency-bound (one workgroup per scan, ordered sums)"),
+           "roofline": {**roof("k_s2s_lm", lm_bytes, lm_ms,
+                                "dominant kernel of the leg; bytes = queries x (32 B per iteration + 48 B "
+                                "tripod gather every 5th), latency-bound (one workgroup per scan, ordered "
+                                "sums); traffic = PMC HBM bytes per launch (the ring-window walks)"),
+                         "traffic": lm_traffic("k_s2s_lm", B)},
            "roofline_projection": roof("k_project" if not hdl else "k_project+k_gather_column", bpc_proj, proj_ms,
                                        "SURVEY 8(d) B_pc projection part 20 N + 24 HW (+ 5 HW raw intensity "
                                        "and ground) over the projection kernels"),
