@@ -858,7 +858,7 @@ static int32_t s2m_batch(llsr_handle* h, const llsr_s2m_batch* b, hipStream_t s,
   for (int it = 0; it < a.iter_max;) {
     const int n = (a.iter_max - it) < poll ? (a.iter_max - it) : poll;
     for (int k = 0; k < n; ++k) {
-      k_s2m_iter<<<dim3(m.blocks, P), 256, 0, s>>>(a);
+      k_s2m_iter<<<8 * ((P + 7) / 8) * m.blocks, 256, 0, s>>>(a);  // XCD-aware (llsr_mo.hip)
       k_s2m_solve<<<P, 256, kSolveLds, s>>>(a);
     }
     it += n;
@@ -924,7 +924,7 @@ extern "C" int32_t llsr_scan2map_shard_partial(llsr_handle* h, int32_t rank, int
   HIP_OK(h, hipMemsetAsync(d_ne, 0, sizeof(int64_t) * LLSR_NE_WORDS * (size_t)a.P, s));
   const int bs = m.blocks - m.blocks_c;
   const int nb = (m.blocks_c + world - 1) / world + (bs + world - 1) / world;
-  if (nb > 0) k_s2m_iter_fx<<<dim3(nb, a.P), 256, 0, s>>>(a);
+  if (nb > 0) k_s2m_iter_fx<<<8 * ((a.P + 7) / 8) * nb, 256, 0, s>>>(a, nb);  // XCD-aware (llsr_mo.hip)
   HIP_OK(h, hipGetLastError());
   return LLSR_OK;
 }

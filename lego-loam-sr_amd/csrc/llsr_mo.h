@@ -58,7 +58,7 @@ __global__ void k_s2m_iter(S2MArgs a);
 __global__ void k_s2m_solve(S2MArgs a);
 constexpr int kSolveLds = 144 * 1024;  // k_s2m_solve's dynamic LDS (gfx950: 160 KB per workgroup)
 __global__ void k_s2m_finish(S2MArgs a);
-__global__ void k_s2m_iter_fx(S2MArgs a);
+__global__ void k_s2m_iter_fx(S2MArgs a, int nb);
 __global__ void k_s2m_solve_fx(S2MArgs a);
 
 }  // namespace llsr

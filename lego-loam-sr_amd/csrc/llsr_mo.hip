@@ -560,12 +560,31 @@ __device__ __forceinline__ void s2m_block(const S2MArgs& a, int p, int qb) {
   if (threadIdx.x == 0) a.bcnt[(size_t)p * a.blocks + gb] = (wcnt[0] + wcnt[1]) + (wcnt[2] + wcnt[3]);
 }
 
-// grid (blocks, P): corner blocks first, then surf blocks; the branch is block-uniform.
+// XCD-aware placement of the (problem, query block) workgroups: the dispatcher deals workgroups
+// round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch), so with a plain
+// (blocks, P) grid every problem's blocks land on all 8 XCDs and each XCD's L2 fetches the same
+// local map. Linear workgroup L -> XCD class x = L % 8 and slot j = L / 8; class x runs the blocks
+// of problems x, x + 8, x + 16, ... in order, so a problem's map is read through one L2 (and
+// k_s2m_solve's workgroup p, class p % 8, finds its rows there). Placement only: results do not
+// depend on it. Grid: 8 * ceil(P / 8) * nb workgroups; false = padding.
+__device__ __forceinline__ bool xcd_problem_block(int nb, int P, int& p, int& b) {
+  const int L = (int)blockIdx.x;
+  const int j = L >> 3;
+  const int pp = j / nb;
+  b = j - pp * nb;
+  p = pp * 8 + (L & 7);
+  return p < P;
+}
+
+// grid 8 * ceil(P / 8) * blocks (xcd_problem_block): corner blocks first, then surf blocks; the
+// branch is block-uniform.
 __global__ __launch_bounds__(256) void k_s2m_iter(S2MArgs a) {
-  if ((int)blockIdx.x < a.blocks_c)
-    s2m_block<true>(a, blockIdx.y, blockIdx.x);
+  int p, b;
+  if (!xcd_problem_block(a.blocks, a.P, p, b)) return;
+  if (b < a.blocks_c)
+    s2m_block<true>(a, p, b);
   else
-    s2m_block<false>(a, blockIdx.y, blockIdx.x - a.blocks_c);
+    s2m_block<false>(a, p, b - a.blocks_c);
 }
 
 // grid P, 256 threads, dynamic LDS a.solve_lds bytes: one workgroup per problem assembles the
@@ -614,15 +633,16 @@ __device__ __forceinline__ void s2m_block_fx(const S2MArgs& a, int p, int qb) {
   }
 }
 
-// grid (ceil(blocks_c / world) + ceil(blocks_s / world), P): rank r takes the corner blocks
-// r, r + world, ... and likewise the surf blocks.
-__global__ __launch_bounds__(256) void k_s2m_iter_fx(S2MArgs a) {
+// grid 8 * ceil(P / 8) * nb with nb = ceil(blocks_c / world) + ceil(blocks_s / world)
+// (xcd_problem_block): rank r takes the corner blocks r, r + world, ... and likewise the surf blocks.
+__global__ __launch_bounds__(256) void k_s2m_iter_fx(S2MArgs a, int nb) {
+  int p, bx;
+  if (!xcd_problem_block(nb, a.P, p, bx)) return;
   const int bcw = (a.blocks_c + a.world - 1) / a.world;
-  const int bx = blockIdx.x;
   if (bx < bcw)
-    s2m_block_fx<true>(a, blockIdx.y, bx * a.world + a.rank);
+    s2m_block_fx<true>(a, p, bx * a.world + a.rank);
   else
-    s2m_block_fx<false>(a, blockIdx.y, (bx - bcw) * a.world + a.rank);
+    s2m_block_fx<false>(a, p, (bx - bcw) * a.world + a.rank);
 }
 
 // One thread per problem: the summed words (all ranks) -> the LM step.
