@@ -109,71 +109,107 @@ __device__ __forceinline__ int project_cell_any(const DevCfg& c, float4 p, float
 // the raw index per cell (the compacted order preserves raw order). Also counts finite points
 // and the first/last finite index for findStartEndAngle (IP:430-436).
 // The winners go to a COLUMN-major scratch table (ccl_a, dead until k_label): Velodyne order
-// fires all rings of one azimuth back to back, so a wave's 64 atomics land in one or two 128-byte
+// fires all rings of one azimuth back to back, so a wave's stores land in one or two 128-byte
 // lines instead of 64 (row-major: one line per ring). k_gather_column turns it row-major.
+// No atomics on the first pass: every point stores its index with a plain store (some colliding
+// point wins), then k_project_fix re-projects each point and raises the cell with atomicMax only
+// when it holds a smaller index, so only colliding cells pay an atomic and the table ends at the
+// maximum raw index per cell, exactly as atomicMax would leave it.
 // grid (ceil(maxN/256), B), block 256.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_project(DevCfg c, const float4* __restrict__ pts,
                                                  const int64_t* __restrict__ off, DevBufs d) {
   const int b = blockIdx.y;
   const int64_t o0 = off[b], n = off[b + 1] - o0;
-  // grid-stride over the scan: every raw point is projected whatever the grid's width
-  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t i = base + threadIdx.x;
-    bool fin = false;
-    if (i < n) {
-      const float4 p = pts[o0 + i];
-      fin = finite3(p);
-      if (fin) {
-        const int cell = project_cell_any(c, p, 1.0f / c.ip_resY, 1.0f / c.ip_resX);
-        if (cell >= 0) {
-          const int row = cell / c.W, col = cell - row * c.W;
-          atomicMax(&d.ccl_a[(size_t)b * c.HW + (size_t)col * c.H + row], (int)i);
-        }
-      }
+  // grid-stride over the scan: every raw point is projected whatever the grid's width; the
+  // finite-point count and first / last finite index are reduced per workgroup (3 atomics each)
+  int npts = 0, first = INT_MAX, last = -1;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 p = pts[o0 + i];
+    if (!finite3(p)) continue;
+    ++npts;
+    first = min(first, (int)i);
+    last = max(last, (int)i);
+    const int cell = project_cell_any(c, p, 1.0f / c.ip_resY, 1.0f / c.ip_resX);
+    if (cell >= 0) {
+      const int row = cell / c.W, col = cell - row * c.W;
+      d.ccl_a[(size_t)b * c.HW + (size_t)col * c.H + row] = (int)i;
     }
-    const unsigned long long m = __ballot(fin);
-    if (lane_id() == 0 && m) {
+  }
+  __shared__ int red[3][4];
+  npts = wave_reduce_add(npts);
+  first = wave_reduce_min(first);
+  last = wave_reduce_max(last);
+  if (lane_id() == 0) { red[0][threadIdx.x >> 6] = npts; red[1][threadIdx.x >> 6] = first; red[2][threadIdx.x >> 6] = last; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = blockDim.x >> 6;
+    for (int w = 1; w < nw; ++w) {
+      npts += red[0][w];
+      first = min(first, red[1][w]);
+      last = max(last, red[2][w]);
+    }
+    if (npts) {
       int* cnt = d.counts + b * kCnt;
-      atomicAdd(&cnt[C_NPTS], (int)__popcll(m));
-      const int wb = (int)(base + (threadIdx.x & ~63));
-      atomicMin(&cnt[C_FIRST], wb + (int)__ffsll((long long)m) - 1);
-      atomicMax(&cnt[C_LAST], wb + 63 - (int)__clzll((long long)m));
+      atomicAdd(&cnt[C_NPTS], npts);
+      atomicMin(&cnt[C_FIRST], first);
+      atomicMax(&cnt[C_LAST], last);
     }
+  }
+}
+
+// K1b: after k_project's plain stores (kernel boundary), each point whose cell holds a smaller
+// raw index raises it; the result is the maximum index per cell (IP:337-347 "last writer wins").
+__global__ __launch_bounds__(256) void k_project_fix(DevCfg c, const float4* __restrict__ pts,
+                                                     const int64_t* __restrict__ off, DevBufs d) {
+  const int b = blockIdx.y;
+  const int64_t o0 = off[b], n = off[b + 1] - o0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 p = pts[o0 + i];
+    if (!finite3(p)) continue;
+    const int cell = project_cell_any(c, p, 1.0f / c.ip_resY, 1.0f / c.ip_resX);
+    if (cell < 0) continue;
+    const int row = cell / c.W, col = cell - row * c.W;
+    int* w = &d.ccl_a[(size_t)b * c.HW + (size_t)col * c.H + row];
+    if (*w < (int)i) atomicMax(w, (int)i);
   }
 }
 
 // ---------------------------------------------------------------------------------------------
 // K2 gather + ground column pass: builds range_mat/full_cloud for each cell (IP:337-347,
 // resetParameters IP:170-179) and runs groundRemovalOurs' per-column vector test and Filter
-// (IP:524-629) in the same sweep. One thread per (scan, column), rows bottom-up; the column's
-// winners are read from k_project's column-major table four rows per 16-byte load, and the
+// (IP:524-629) in the same sweep. One thread per (scan, column), rows bottom-up. The wave's 64
+// columns of k_project's column-major winner table are one contiguous run of 64 * H ints: loaded
+// coalesced into LDS (column stride H + 1 against bank conflicts), then read per column; the
 // row-major cell->point map is written here.
-// grid (ceil(W/64), B), block 64.
+// grid (ceil(W/64), B), block 64, dynamic LDS 64 * (H + 1) ints.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_gather_column(DevCfg c, const float4* __restrict__ pts,
                                                       const int64_t* __restrict__ off, DevBufs d) {
+  extern __shared__ int lwin[];
   const int b = blockIdx.y;
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= c.W) return;
+  const int j0 = blockIdx.x * blockDim.x;
+  const int j = j0 + threadIdx.x;
   const int64_t o0 = off[b];
   const size_t base = (size_t)b * c.HW;
-  const int* colw = d.ccl_a + base + (size_t)j * c.H;  // this column's winners, row 0 first
-  const bool vec4 = (c.H & 3) == 0;                      // 16-byte aligned column runs
+  {
+    const int ncol = min(64, c.W - j0);
+    const int* src = d.ccl_a + base + (size_t)j0 * c.H;  // columns j0 .. j0 + ncol - 1, row 0 first
+    for (int t = threadIdx.x; t < ncol * c.H; t += 64) {
+      const int cj = t / c.H, ci = t - cj * c.H;
+      lwin[cj * (c.H + 1) + ci] = src[t];
+    }
+  }
+  __syncthreads();
+  if (j >= c.W) return;
+  const int* colw = lwin + threadIdx.x * (c.H + 1);  // this column's winners, row 0 first
   const float qnan = __builtin_nanf("");
   bool haveRV = false, obs = false;
   float RVx = 0.f, RVy = 0.f, RVz = 0.f;
   float lx = 0.f, ly = 0.f, lz = 0.f;
-  int4 w4 = make_int4(-1, -1, -1, -1);
   for (int i = 0; i < c.H; ++i) {
     const int cell = j + i * c.W;
-    int pi;
-    if (vec4) {
-      if ((i & 3) == 0) w4 = *reinterpret_cast<const int4*>(colw + i);
-      pi = (i & 3) == 0 ? w4.x : (i & 3) == 1 ? w4.y : (i & 3) == 2 ? w4.z : w4.w;
-    } else {
-      pi = colw[i];
-    }
+    const int pi = colw[i];
     d.cell_pt[base + cell] = pi;
     float4 f;
     float rng, vis;
