@@ -23,7 +23,6 @@
 
 namespace llsr {
 __global__ void k_project(DevCfg, const float4*, const int64_t*, DevBufs);
-__global__ void k_project_fix(DevCfg, const float4*, const int64_t*, DevBufs);
 __global__ void k_gather_column(DevCfg, const float4*, const int64_t*, DevBufs);
 __global__ void k_project_fused(DevCfg, const float4*, const int64_t*, DevBufs);
 __global__ void k_ground_add(DevCfg, DevBufs);
@@ -489,7 +488,6 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
     // grid-stride kernels: ~16k workgroups in all, at least 4 per scan
     const int gx = std::max(1, std::min((h->max_points + 255) / 256, std::max(4, 16384 / B)));
     k_project<<<dim3(gx, B), 256, 0, s>>>(c, pts, d_offsets, h->d);
-    k_project_fix<<<dim3(gx, B), 256, 0, s>>>(c, pts, d_offsets, h->d);
     mark();
     k_gather_column<<<dim3((c.W + 63) / 64, B), 64, sizeof(int) * 64 * (c.H + 1), s>>>(c, pts, d_offsets, h->d);
     mark();

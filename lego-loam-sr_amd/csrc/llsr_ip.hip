@@ -111,10 +111,8 @@ __device__ __forceinline__ int project_cell_any(const DevCfg& c, float4 p, float
 // The winners go to a COLUMN-major scratch table (ccl_a, dead until k_label): Velodyne order
 // fires all rings of one azimuth back to back, so a wave's stores land in one or two 128-byte
 // lines instead of 64 (row-major: one line per ring). k_gather_column turns it row-major.
-// No atomics on the first pass: every point stores its index with a plain store (some colliding
-// point wins), then k_project_fix re-projects each point and raises the cell with atomicMax only
-// when it holds a smaller index, so only colliding cells pay an atomic and the table ends at the
-// maximum raw index per cell, exactly as atomicMax would leave it.
+// (Measured per 512 HDL-64E scans: per-wave counter atomics 4.17 ms -> per-workgroup 0.36 ms; a
+// plain-store pass plus an atomicMax fix-up pass for colliding cells was slower, 0.61 ms.)
 // grid (ceil(maxN/256), B), block 256.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_project(DevCfg c, const float4* __restrict__ pts,
@@ -133,7 +131,7 @@ __global__ __launch_bounds__(256) void k_project(DevCfg c, const float4* __restr
     const int cell = project_cell_any(c, p, 1.0f / c.ip_resY, 1.0f / c.ip_resX);
     if (cell >= 0) {
       const int row = cell / c.W, col = cell - row * c.W;
-      d.ccl_a[(size_t)b * c.HW + (size_t)col * c.H + row] = (int)i;
+      atomicMax(&d.ccl_a[(size_t)b * c.HW + (size_t)col * c.H + row], (int)i);
     }
   }
   __shared__ int red[3][4];
@@ -155,23 +153,6 @@ __global__ __launch_bounds__(256) void k_project(DevCfg c, const float4* __restr
       atomicMin(&cnt[C_FIRST], first);
       atomicMax(&cnt[C_LAST], last);
     }
-  }
-}
-
-// K1b: after k_project's plain stores (kernel boundary), each point whose cell holds a smaller
-// raw index raises it; the result is the maximum index per cell (IP:337-347 "last writer wins").
-__global__ __launch_bounds__(256) void k_project_fix(DevCfg c, const float4* __restrict__ pts,
-                                                     const int64_t* __restrict__ off, DevBufs d) {
-  const int b = blockIdx.y;
-  const int64_t o0 = off[b], n = off[b + 1] - o0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const float4 p = pts[o0 + i];
-    if (!finite3(p)) continue;
-    const int cell = project_cell_any(c, p, 1.0f / c.ip_resY, 1.0f / c.ip_resX);
-    if (cell < 0) continue;
-    const int row = cell / c.W, col = cell - row * c.W;
-    int* w = &d.ccl_a[(size_t)b * c.HW + (size_t)col * c.H + row];
-    if (*w < (int)i) atomicMax(w, (int)i);
   }
 }
 
