@@ -1138,7 +1138,12 @@ extern "C" int32_t llsr_scan2scan_batch(llsr_handle* h, const llsr_s2s_batch* b,
   if (h->profiling) HIP_OK(h, hipEventRecord(m.p0, s));
   grid_build(a.grids, s);
   if (h->profiling) HIP_OK(h, hipEventRecord(m.p1, s));
-  k_s2s_lm<<<P, kS2SThreads, 0, s>>>(a);
+  // the small-LDS instantiation (4 workgroups per CU instead of 2) when every problem's queries
+  // and corner-last cloud fit it (reserved capacities are the batch maxima)
+  if (m.ms <= 1024 && m.f <= 1024 && m.nc <= 1024)
+    k_s2s_lm<1024, 1024><<<P, kS2SThreads, 0, s>>>(a);
+  else
+    k_s2s_lm<2048, 2048><<<P, kS2SThreads, 0, s>>>(a);
   HIP_OK(h, hipGetLastError());
   m.last = s;
   if (h->profiling) {

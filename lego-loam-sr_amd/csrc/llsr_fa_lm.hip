@@ -41,8 +41,6 @@ namespace {
 
 constexpr int kThreads = kS2SThreads;
 constexpr int kMaxShell = 2;  // grid shells searched before the exact block-wide scan (queries in sparse regions)
-constexpr int kLdsRows = 2048;    // Jacobian rows kept in LDS (32 KB); larger phases use the HBM buffer
-constexpr int kLdsCorner = 2048;  // laserCloudCornerLast kept in LDS (32 KB) for a brute-force kNN-1
 constexpr int kFbMax = 256;       // queries per kNN iteration whose shells did not settle (block scan)
 
 // TransformToStart (FA:1389-1412)
@@ -368,7 +366,12 @@ struct JacCorner {
 #define LLSR_STAMP(acc) do {} while (0)
 #endif
 
-__global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
+// kLdsRows: Jacobian rows kept in LDS (16 B each; larger phases use the HBM buffer); kLdsCorner:
+// laserCloudCornerLast kept in LDS for a brute-force kNN-1 (larger clouds use the cell grid).
+// Two instantiations (llsr_s2s.h): 2048 / 2048 (70 KB, 2 workgroups per CU) and 1024 / 1024
+// (35 KB, 4 per CU) for batches whose queries and corner clouds fit it.
+template <int kLdsRows, int kLdsCorner>
+__global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
   const int p = blockIdx.x;
   const int tid = threadIdx.x;
 #ifdef LLSR_S2S_PROF
@@ -745,5 +748,8 @@ __global__ __launch_bounds__(kThreads) void k_s2s_lm(S2SArgs a) {
     a.degen[p] = isDeg;
   }
 }
+
+template __global__ void k_s2s_lm<2048, 2048>(S2SArgs);
+template __global__ void k_s2s_lm<1024, 1024>(S2SArgs);
 
 }  // namespace llsr

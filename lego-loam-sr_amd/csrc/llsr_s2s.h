@@ -26,6 +26,7 @@ struct S2SArgs {
 // threads per scan-to-scan workgroup (one workgroup per problem)
 constexpr int kS2SThreads = 512;  // measured: 256 -> 512 HDL-64E LM 39.3 -> 32.6 ms, VLP-16 9.1 -> 8.4 ms; 1024 slower on VLP-16
 
+template <int kLdsRows, int kLdsCorner>
 __global__ void k_s2s_lm(S2SArgs a);
 
 }  // namespace llsr
