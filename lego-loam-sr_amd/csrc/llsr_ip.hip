@@ -454,7 +454,9 @@ __device__ __forceinline__ bool add_test(const float4* __restrict__ full, int ce
   return (double)dr <= 0.061 * (double)r && (double)dz <= 0.1;
 }
 
-__global__ __launch_bounds__(256) void k_ground_add(DevCfg c, DevBufs d) {
+// 8 waves per SIMD (45 VGPRs, no spills): 0.190 -> 0.154 ms per 1024 VLP-16 scans; the same bound
+// on k_segment / k_ground_elev_ransac spills and was slower
+__global__ __launch_bounds__(256, 8) void k_ground_add(DevCfg c, DevBufs d) {
   __shared__ int8_t grow[4][2048];
   const int b = blockIdx.y;
   const int wv = threadIdx.x >> 6, l = lane_id();
