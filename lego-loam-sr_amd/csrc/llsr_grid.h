@@ -25,7 +25,7 @@ struct CellGrid {
   const float4* src;    // the clouds, concatenated over the batch
   const int64_t* off;   // [P+1]
   int cap;              // points per problem reserved
-  int log2T;            // table slots per problem = 1 << log2T (>= 2 * cap)
+  int log2T;            // table slots per problem = 1 << log2T (> cap, grid_log2_table)
   CellSlot* tab;        // [P][1 << log2T]
   float4* sorted;       // [P][cap]
   int2* where;          // [P][cap] (slot, rank) of each point
@@ -59,7 +59,7 @@ __device__ __forceinline__ uint32_t cell_hash(uint64_t k, int log2T) {
   return (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> (64 - log2T));
 }
 
-// Probe for `key`; returns the slot or -1 (the table is never full: load factor <= 0.5).
+// Probe for `key`; returns the slot or -1 (the table is never full: more slots than points).
 __device__ __forceinline__ int grid_find(const CellSlot* __restrict__ tab, int log2T, uint64_t key) {
   const uint32_t mask = (1u << log2T) - 1u;
   uint32_t s = cell_hash(key, log2T);
