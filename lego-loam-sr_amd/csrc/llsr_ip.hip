@@ -317,25 +317,108 @@ __global__ __launch_bounds__(1024) void k_project_fused(DevCfg c, const float4* 
   __syncthreads();
   int nfin = 0, first = INT_MAX, last = -1;
   const float invResY = 1.0f / c.ip_resY, invResX = 1.0f / c.ip_resX;
-  // four coalesced point loads in flight per lane before any of the projection math
-  constexpr int kP = 4;
-  for (int i0 = tid; i0 < n; i0 += kP * nt) {
-    float4 pp[kP];
+  const float qnan = __builtin_nanf("");
+  const int W = c.W;
+  // (float)(row + (double)col / 1e4) == (float)(row + col * 1e-4) for every row < 256, col < 8192
+  // (tests/test_oracle.py checks all of them), so the double division becomes a multiply there.
+  const bool mulInt = c.H <= 256 && W <= 8192;
+  // Chunks of nt raw points in DESCENDING index order. "Last writer wins" (IP:337-347) makes a
+  // cell's point the largest raw index mapped to it, so once a chunk has raised the LDS winner table
+  // (atomicMax) a cell holding an index of THIS chunk is final: no later-processed (lower-index)
+  // point can take it. Its winner emits the cell's range / full cloud / intensity / point index from
+  // registers, so the raw points are read from HBM exactly once. A firing-ordered stream (Velodyne:
+  // the rings of one azimuth are consecutive) puts a chunk's cells in a band of ~nt / H columns:
+  // winners inside the 64-column band starting at the chunk's smallest column go through an LDS
+  // tile written out row by row (full lines); any other winner (wrap-around, unordered input)
+  // writes its cell directly.
+  // Chunks of kU * nt points (kU per lane, loads of the next chunk issued before this chunk's
+  // barriers); the tile holds the band's full cloud and intensity, and "won in this chunk" is read
+  // back from the winner table (index within the chunk's range).
+  constexpr int kU = 2, kTC = 128, kTP = kTC + 1;  // padded rows
+  __shared__ float4 tfull[16 * kTP];
+  __shared__ float tvis[16 * kTP];
+  __shared__ int s_cmin[2];
+  if (tid < 2) s_cmin[tid] = INT_MAX;
+  const int C = kU * nt;
+  const int nch = (n + C - 1) / C;
+  float4 pn[kU];
+  auto load = [&](int ch) {
 #pragma unroll
-    for (int u = 0; u < kP; ++u) {
-      const int i = i0 + u * nt;
-      pp[u] = i < n ? pts[o0 + i] : make_float4(__builtin_nanf(""), 0.f, 0.f, 0.f);
+    for (int u = 0; u < kU; ++u) {
+      const int i = ch * C + u * nt + tid;
+      pn[u] = (ch >= 0 && i < n) ? pts[o0 + i] : make_float4(qnan, 0.f, 0.f, 0.f);
     }
+  };
+  load(nch - 1);
+  __syncthreads();
+  for (int ch = nch - 1; ch >= 0; --ch) {
+    const int par = ch & 1;
+    const int lo = ch * C, hi = lo + C;  // this chunk's raw index range
+    float4 pp[kU];
 #pragma unroll
-    for (int u = 0; u < kP; ++u) {
-      const int i = i0 + u * nt;
+    for (int u = 0; u < kU; ++u) pp[u] = pn[u];
+    load(ch - 1);  // in flight during this chunk
+    if (tid == 0) s_cmin[par ^ 1] = INT_MAX;  // the next chunk's
+    int cell[kU], row[kU], col[kU];
+    int cm = INT_MAX;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = lo + u * nt + tid;
+      cell[u] = -1;
+      row[u] = 0;
+      col[u] = INT_MAX;
       if (!finite3(pp[u])) continue;
       ++nfin;
       first = i < first ? i : first;
-      last = i;
-      const int cell = project_cell_any(c, pp[u], invResY, invResX);
-      if (cell >= 0) atomicMax(&cidx[cell], i);
+      last = i > last ? i : last;
+      cell[u] = project_cell_any(c, pp[u], invResY, invResX);
+      if (cell[u] >= 0) {
+        atomicMax(&cidx[cell[u]], i);
+        row[u] = cell[u] / W;
+        col[u] = cell[u] - row[u] * W;
+        cm = col[u] < cm ? col[u] : cm;
+      }
     }
+    cm = wave_reduce_min(cm);
+    if (lane_id() == 0 && cm != INT_MAX) atomicMin(&s_cmin[par], cm);
+    __syncthreads();
+    const int c0 = s_cmin[par];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = lo + u * nt + tid;
+      if (cell[u] < 0 || cidx[cell[u]] != i) continue;
+      const float4 p = pp[u];
+      const double dc = mulInt ? (double)(float)col[u] * 1e-4 : (double)(float)col[u] / 10000.0;
+      const float4 f = make_float4(p.x, p.y, p.z, (float)((double)(float)row[u] + dc));
+      if (col[u] - c0 < kTC) {
+        const int t = row[u] * kTP + (col[u] - c0);
+        tfull[t] = f;
+        tvis[t] = p.w;
+      } else {
+        const size_t q = base + cell[u];
+        d.cell_pt[q] = i;
+        d.range[q] = sqrt_(p.x * p.x + p.y * p.y + p.z * p.z);
+        d.full[q] = f;
+        d.vis[q] = p.w;
+      }
+    }
+    __syncthreads();
+    if (c0 != INT_MAX) {  // row-major over the tile: the cells this chunk won
+      for (int t = tid; t < c.H * kTC; t += nt) {
+        const int trow = t / kTC, ck = t % kTC, tcol = c0 + ck;
+        if (tcol >= W) continue;
+        const int wpi = cidx[trow * W + tcol];
+        if (wpi < lo || wpi >= hi) continue;
+        const int tt = trow * kTP + ck;
+        const size_t q = base + (size_t)trow * W + tcol;
+        const float4 f = tfull[tt];
+        d.cell_pt[q] = wpi;
+        d.range[q] = sqrt_(f.x * f.x + f.y * f.y + f.z * f.z);
+        d.full[q] = f;
+        d.vis[q] = tvis[tt];
+      }
+    }
+    __syncthreads();
   }
   nfin = block_reduce_add(nfin, tmp);
   first = block_reduce_min(first, tmp);
@@ -347,67 +430,15 @@ __global__ __launch_bounds__(1024) void k_project_fused(DevCfg c, const float4* 
     cnt[C_LAST] = last;
   }
   if (c.dbg_phase <= 0) return;
-  // Pass 2 over tiles of H rows x 64 columns. A firing-ordered sensor stream (Velodyne: the rings of
-  // one azimuth are consecutive raw points) stores a tile's winners as one contiguous run of the
-  // input, so the tile is gathered column by column (coalesced) into LDS and written out row by
-  // row (coalesced full lines): neither side strides. Empty cells get the resetParameters values
-  // (IP:170-179); only the winner's range is recomputed, row / column come from the cell.
-  constexpr int kTC = 64, kTP = kTC + 1;  // padded rows: column-major LDS writes spread over banks
-  __shared__ float4 tfull[16 * kTP];
-  __shared__ float tvis[16 * kTP];
-  __shared__ int tpi[16 * kTP];
-  const float qnan = __builtin_nanf("");
-  const int H = c.H, W = c.W;
-  // (float)(row + (double)col / 1e4) == (float)(row + col * 1e-4) for every row < 256, col < 8192
-  // (tests/test_oracle.py checks all of them), so the double division becomes a multiply there.
-  const bool mulInt = H <= 256 && W <= 8192;
-  // The gather of the next tile is issued before this tile's barrier and write-out, so the point
-  // loads of consecutive tiles overlap instead of paying one memory round trip per tile.
-  const bool act = tid < H * kTC;
-  const int grow = tid % H, gck = tid / H;
-  auto gather = [&](int c0, int& pi, float4& p) {
-    const int col = c0 + gck;
-    pi = -1;
-    if (act && col < W) {
-      pi = cidx[grow * W + col];
-      if (pi >= 0) p = pts[o0 + pi];
-    }
-  };
-  int pi_n = -1;
-  float4 p_n = make_float4(0.f, 0.f, 0.f, 0.f);
-  gather(0, pi_n, p_n);
-  for (int c0 = 0; c0 < W; c0 += kTC) {
-    const int pi = pi_n;
-    const float4 p = p_n;
-    if (act) {  // column-major over the tile
-      const int col = c0 + gck;
-      float4 f = make_float4(qnan, qnan, qnan, 0.0f);
-      float vis = 0.0f;
-      if (pi >= 0) {
-        const double dc = mulInt ? (double)(float)col * 1e-4 : (double)(float)col / 10000.0;
-        f = make_float4(p.x, p.y, p.z, (float)((double)(float)grow + dc));
-        vis = p.w;
-      }
-      tfull[grow * kTP + gck] = f;
-      tvis[grow * kTP + gck] = vis;
-      tpi[grow * kTP + gck] = pi;
-    }
-    if (c0 + kTC < W) gather(c0 + kTC, pi_n, p_n);
-    __syncthreads();
-    if (act) {  // row-major over the tile
-      const int row = tid / kTC, ck = tid % kTC, col = c0 + ck;
-      if (col < W) {
-        const size_t q = base + (size_t)row * W + col;
-        const float4 f = tfull[row * kTP + ck];
-        const int wpi = tpi[row * kTP + ck];
-        d.cell_pt[q] = wpi;
-        d.range[q] = wpi >= 0 ? sqrt_(f.x * f.x + f.y * f.y + f.z * f.z) : FLT_MAX;
-        d.full[q] = f;
-        d.vis[q] = tvis[row * kTP + ck];
-      }
-    }
-    __syncthreads();
+  // cells no point reached keep the resetParameters values (IP:170-179)
+  for (int q = tid; q < HW; q += nt) {
+    if (cidx[q] >= 0) continue;
+    d.cell_pt[base + q] = -1;
+    d.range[base + q] = FLT_MAX;
+    d.full[base + q] = make_float4(qnan, qnan, qnan, 0.0f);
+    d.vis[base + q] = 0.0f;
   }
+  __syncthreads();
   if (c.dbg_phase <= 1) return;
   for (int j = tid; j < c.W; j += 2 * nt) ground_columns2(c, d.full + base, d.ground + base, j, j + nt);
 }
