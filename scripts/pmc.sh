@@ -8,7 +8,7 @@ OUT=gpurun_out/${TAG:-pmc}
 B=${B:-1024}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS="--steps 3 --warmup 1 --no-cpu --streams 1 --batch $B --s2m-modes= --allreduce-scans 0 --odo= --map-keyframes 0 --pc2 0"
+ARGS="--steps 3 --warmup 1 --no-cpu --streams 1 --batch $B --s2m-modes= --allreduce-scans 0 --odo= --map-keyframes 0 --pc2 0 --mapping="
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$PWD/$OUT/fetch" -o run -- python3 bench.py $ARGS > "$OUT/fetch.log" 2>&1 || exit $?
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$PWD/$OUT/write" -o run -- python3 bench.py $ARGS > "$OUT/write.log" 2>&1 || exit $?
 python3 scripts/pmc_parse.py "$OUT" "$B" > "$OUT/traffic.json"
