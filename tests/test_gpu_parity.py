@@ -98,11 +98,18 @@ def _edge_inputs():
     allnan = np.full((100, 4), np.nan, dtype=np.float32)
     origin = np.zeros((10, 4), dtype=np.float32)  # range 0 -> dropped (IP:333)
     shuffled = finite[rng.permutation(finite.shape[0])]
+    # firing order started mid-revolution / run backwards: the projection's descending-index chunks
+    # then straddle the column wrap or sweep the columns the other way (k_project_fused's direct
+    # writes outside the tile band)
+    rolled = np.roll(base, 7777, axis=0)
+    reversed_ = np.ascontiguousarray(base[::-1])
     return {"empty": np.zeros((0, 4), np.float32), "allnan": allnan, "tiny": tiny,
-            "collisions": dup, "origin": origin, "shuffled": shuffled}
+            "collisions": dup, "origin": origin, "shuffled": shuffled, "rolled": rolled,
+            "reversed": reversed_}
 
 
-@pytest.mark.parametrize("case", ["empty", "allnan", "tiny", "collisions", "origin", "shuffled"])
+@pytest.mark.parametrize("case", ["empty", "allnan", "tiny", "collisions", "origin", "shuffled", "rolled",
+                                  "reversed"])
 def test_edge_cases(require_gpu, case):
     cfg = default_config("vlp16")
     pts = _edge_inputs()[case]
@@ -132,4 +139,49 @@ def test_golden_fixtures_pcl_order(require_gpu):
             if a.dtype == np.float32:
                 a, b = a.view(np.uint32), b.view(np.uint32)
             assert np.array_equal(a, b), (k, name)
+    pipe.close()
+
+
+def test_batches_alternating_streams_one_handle(require_gpu):
+    """Batches of one handle on two different streams: each batch starts after the
+    previous one (the slot buffers and the FA carry-over state are shared), so a sequence of batches
+    alternating between the streams equals the oracle's per-slot sequences."""
+    import torch
+    cfg = default_config("vlp16")
+    B = 4
+    pipe = Pipeline(cfg, max_batch=B, max_points=40000)
+    oracles = [oracle_py.Oracle(cfg) for _ in range(B)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for rep in range(4):
+        pts, off = synth.make_batch(B, "vlp16", distinct=B, seed0=31 + 10 * rep)
+        s = streams[rep % 2]
+        with torch.cuda.stream(s):
+            d_pts = torch.from_numpy(pts).cuda()
+            d_off = torch.from_numpy(off).cuda()
+        s.synchronize()
+        pipe.process_batch(d_pts.data_ptr(), d_off.data_ptr(), B, s.cuda_stream)
+        for b in range(B):
+            o = oracles[b].process(pts[off[b]:off[b + 1]])
+            errs = compare(pipe.fetch(b), o)
+            assert not errs, f"rep {rep} slot {b}:\n  " + "\n  ".join(errs)
+    pipe.close()
+
+
+@pytest.mark.parametrize("lidar", ["vlp16", "hdl64e"])
+def test_batch_scan_longer_than_max_points(require_gpu, lidar):
+    """A device-resident batch whose scans exceed the handle's max_points: every raw
+    point is still projected (both projection paths loop over the whole scan), so the slot equals
+    the oracle on the full scan."""
+    import torch
+    cfg = default_config(lidar, 2048 if lidar == "hdl64e" else None)
+    B = 2
+    pts, off = synth.make_batch(B, lidar, distinct=2, seed0=41)
+    pipe = Pipeline(cfg, max_batch=B, max_points=1000)
+    d_pts, d_off = torch.from_numpy(pts).cuda(), torch.from_numpy(off).cuda()
+    torch.cuda.synchronize()
+    pipe.process_batch(d_pts.data_ptr(), d_off.data_ptr(), B)
+    for b in range(B):
+        o = oracle_py.Oracle(cfg).process(pts[off[b]:off[b + 1]])
+        errs = compare(pipe.fetch(b), o)
+        assert not errs, f"slot {b}:\n  " + "\n  ".join(errs)
     pipe.close()
