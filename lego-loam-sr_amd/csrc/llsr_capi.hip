@@ -155,6 +155,7 @@ struct llsr_handle {
 
 // The fused projection keeps the winning raw index per cell in LDS (k_project_fused).
 static int fused_lds(const DevCfg& c) { return c.HW * (int)sizeof(int); }
+static int label_band_lds(const DevCfg& c) { return c.lbl_band * c.W * (int)sizeof(int); }
 static bool use_fused(const llsr_handle* h) { return h->dc.ccl_lds != 0; }
 
 static int32_t fail(llsr_handle* h, int32_t code, const std::string& msg) {
@@ -227,6 +228,7 @@ static void make_devcfg(const llsr_config& c, DevCfg& d) {
   d.gnd_cos[1] = llsr_libm::ground_cos_threshold(60.0f);
   d.gnd_cos[2] = llsr_libm::ground_cos_threshold(25.0f);
   d.ccl_lds = (d.H <= 16 && d.HW <= 32000) ? 1 : 0;
+  d.lbl_band = std::max(1, std::min(d.H, 36864 / std::max(1, d.W)));
   d.dbg_phase = 1 << 30;
 }
 
@@ -339,6 +341,12 @@ extern "C" int32_t llsr_create(const llsr_config* cfg, int32_t hip_device, int32
     for (auto& e : set)
       if (hipEventCreate(&e) != hipSuccess) { llsr_destroy(h); return LLSR_ENODEV; }
   if (hipEventCreateWithFlags(&h->last_done, hipEventDisableTiming) != hipSuccess) {
+    llsr_destroy(h);
+    return LLSR_ENODEV;
+  }
+  if (!h->dc.ccl_lds &&
+      hipFuncSetAttribute((const void*)k_label<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          label_band_lds(h->dc)) != hipSuccess) {
     llsr_destroy(h);
     return LLSR_ENODEV;
   }
@@ -499,7 +507,7 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   if (c.ccl_lds)
     k_label<true><<<B, 1024, c.HW * sizeof(int), s>>>(c, h->d);
   else
-    k_label<false><<<B, 1024, 0, s>>>(c, h->d);
+    k_label<false><<<B, 1024, label_band_lds(c), s>>>(c, h->d);
   mark();
   k_segment<<<B, 1024, 0, s>>>(c, pts, d_offsets, h->d);
   mark();
@@ -616,7 +624,7 @@ extern "C" float llsr_debug_phase_ms(llsr_handle* h, int32_t k, int32_t phase, i
       case 6: k_segment<<<B, 1024, 0, s>>>(c, nullptr, nullptr, h->d); break;
       case 5:
         if (c.ccl_lds) k_label<true><<<B, 1024, c.HW * sizeof(int), s>>>(c, h->d);
-        else k_label<false><<<B, 1024, 0, s>>>(c, h->d);
+        else k_label<false><<<B, 1024, label_band_lds(c), s>>>(c, h->d);
         break;
       case 4: k_ground_elev_ransac<<<B, 1024, 0, s>>>(c, h->d); break;
       case 3: k_ground_add<<<dim3((c.H + 3) / 4, B), 256, 0, s>>>(c, h->d); break;

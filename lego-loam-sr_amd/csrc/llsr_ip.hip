@@ -909,25 +909,72 @@ __global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
   int* lab = d.label + base;
   LdsAcc P{kLds ? lds_parent : d.ccl_a + base};
 
-  // label_mat init (IP:752-759): -1 for ground or empty, else 0 -> union-find singleton
-  for (int cell = tid; cell < HW; cell += nt) {
-    const bool l0 = !(g[cell] == 1 || rng[cell] == FLT_MAX);
-    P.st(cell, l0 ? cell : -1);
-  }
-  __syncthreads();
-  if (c.dbg_phase <= 0) return;
-  for (int cell = tid; cell < HW; cell += nt) {
-    if (P.ld(cell) < 0) continue;
-    const int i = cell / W, j = cell - i * W;
-    const float r = rng[cell];
-    const int right = (j + 1 < W) ? cell + 1 : cell + 1 - W;  // wrap (IP:884-886)
-    if (P.ld(right) >= 0 && seg_edge(c, r, rng[right], true)) uf_unite(P, cell, right);
-    if (i + 1 < H) {
-      const int down = cell + W;
-      if (P.ld(down) >= 0 && seg_edge(c, r, rng[down], false)) uf_unite(P, cell, down);
+  if constexpr (kLds) {
+    // label_mat init (IP:752-759): -1 for ground or empty, else 0 -> union-find singleton
+    for (int cell = tid; cell < HW; cell += nt) {
+      const bool l0 = !(g[cell] == 1 || rng[cell] == FLT_MAX);
+      P.st(cell, l0 ? cell : -1);
     }
+    __syncthreads();
+    if (c.dbg_phase <= 0) return;
+    for (int cell = tid; cell < HW; cell += nt) {
+      if (P.ld(cell) < 0) continue;
+      const int i = cell / W, j = cell - i * W;
+      const float r = rng[cell];
+      const int right = (j + 1 < W) ? cell + 1 : cell + 1 - W;  // wrap (IP:884-886)
+      if (P.ld(right) >= 0 && seg_edge(c, r, rng[right], true)) uf_unite(P, cell, right);
+      if (i + 1 < H) {
+        const int down = cell + W;
+        if (P.ld(down) >= 0 && seg_edge(c, r, rng[down], false)) uf_unite(P, cell, down);
+      }
+    }
+    __syncthreads();
+  } else {
+    // H*W does not fit LDS: bands of lbl_band rows are united in LDS (local indices, link to the
+    // smaller root, so a band root is its band component's smallest cell), their roots written to
+    // the global parent array (every cell -> its band root), then only the down edges across band
+    // boundaries are united there. Same components, same roots (the smallest cell) as one
+    // union-find over the whole image; the global atomics touch ~H / lbl_band rows instead of all.
+    const int R = c.lbl_band;
+    LdsAcc L{lds_parent};
+    for (int r0 = 0; r0 < H; r0 += R) {
+      const int r1 = r0 + R < H ? r0 + R : H;
+      const int c0 = r0 * W, nb = (r1 - r0) * W;
+      for (int q = tid; q < nb; q += nt) {
+        const int cell = c0 + q;
+        const bool l0 = !(g[cell] == 1 || rng[cell] == FLT_MAX);
+        L.st(q, l0 ? q : -1);
+      }
+      __syncthreads();
+      for (int q = tid; q < nb; q += nt) {
+        if (L.ld(q) < 0) continue;
+        const int cell = c0 + q;
+        const int i = cell / W, j = cell - i * W;
+        const float r = rng[cell];
+        const int rq = (j + 1 < W) ? q + 1 : q + 1 - W;  // wrap (IP:884-886)
+        if (L.ld(rq) >= 0 && seg_edge(c, r, rng[c0 + rq], true)) uf_unite(L, q, rq);
+        if (i + 1 < r1) {
+          const int dq = q + W;
+          if (L.ld(dq) >= 0 && seg_edge(c, r, rng[c0 + dq], false)) uf_unite(L, q, dq);
+        }
+      }
+      __syncthreads();
+      for (int q = tid; q < nb; q += nt) {  // read-only walks: the band is final
+        int x = L.ld(q);
+        if (x >= 0)
+          for (int px = L.ld(x); px != x; px = L.ld(x)) x = px;
+        P.st(c0 + q, x < 0 ? -1 : c0 + x);
+      }
+      __syncthreads();
+    }
+    if (c.dbg_phase <= 0) return;
+    for (int r1 = R; r1 < H; r1 += R)
+      for (int j = tid; j < W; j += nt) {
+        const int a = (r1 - 1) * W + j, bc = r1 * W + j;
+        if (P.ld(a) >= 0 && P.ld(bc) >= 0 && seg_edge(c, rng[a], rng[bc], false)) uf_unite(P, a, bc);
+      }
+    __syncthreads();
   }
-  __syncthreads();
   if (c.dbg_phase <= 1) return;
   if constexpr (kLds) {
     // Everything stays in the LDS word of each cell: -1 = not label 0; a member holds its root's
@@ -1000,14 +1047,30 @@ __global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
   __syncthreads();
   for (int cell = tid; cell < HW; cell += nt) {
     const int root = lab[cell];
-    if (root < 0) continue;
     const int row = cell / W;
     if (kLds) {
+      if (root < 0) continue;
       atomicAdd(&stat[root], 1 << 16);
       if (cell != root) atomicOr(&stat[root], 1 << row);
     } else {
-      atomicAdd(&stat[root], 1);
-      if (cell != root) atomicOr(&rowm[root], 1ull << row);
+      // a wave holds 64 consecutive cells, mostly of one or two segments: one size atomic per
+      // distinct root of the wave (same-address global atomics serialise at L2), one row-mask
+      // atomic per (root, row) of its non-seed members
+      const int l = lane_id();
+      unsigned long long pend = __ballot(root >= 0);
+      while (pend) {
+        const int leader = __ffsll((long long)pend) - 1;
+        const int lr = __shfl(root, leader, 64);
+        const int lrow = __shfl(row, leader, 64);
+        const unsigned long long grp = __ballot(root == lr) & pend;
+        const unsigned long long same = __ballot(root == lr && cell != lr && row == lrow) & pend;
+        if (l == leader) {
+          atomicAdd(&stat[lr], (int)__popcll(grp));
+          if (same) atomicOr(&rowm[lr], 1ull << lrow);
+        }
+        if (((grp >> l) & 1ull) && cell != lr && row != lrow) atomicOr(&rowm[lr], 1ull << row);
+        pend &= ~grp;
+      }
     }
   }
   __syncthreads();
