@@ -24,6 +24,14 @@ def test_header_declares_expected_surface():
     assert set(llsr.EXPORTS) == set(_declared())
 
 
+def test_integration_maps_every_entry_point():
+    """INTEGRATION.md §1 names every entry point of the header next to the reference function it
+    replaces (or marks it as a diagnostic)."""
+    text = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    missing = [f for f in _declared() if f not in text]
+    assert not missing, missing
+
+
 def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", llsr.LIB_PATH], check=True,
                          capture_output=True, text=True).stdout
