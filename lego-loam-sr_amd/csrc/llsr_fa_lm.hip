@@ -440,6 +440,14 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
         const bool knn = it % 5 == 0;
         // the ring-constrained tripod search around a found nearest neighbour (FA:1588-1647 /
         // FA:1737-1803) and the correspondence indices it leaves in idx
+        // the nearest neighbour (index, squared distance) of query q, parked in idx; the tripod
+        // searches then run from ONE call site below (one inlined copy of the walks keeps the
+        // kernel at 128 VGPRs with fewer spills than three copies)
+        auto park = [&](int q, int nn, float nd) {
+          int* ix = idx + 3 * q;
+          ix[0] = nn;
+          ix[1] = __float_as_int(nd);
+        };
         auto finish = [&](int q, float4 sel, int nn, float nd) {
           int i1, i2, i3 = -1;
           if (surf) {
@@ -476,7 +484,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
               else corner_brute<4>(lcl, Nc, qs, bd, bi);
 #pragma unroll
               for (int j = 0; j < kMulti; ++j)
-                if (q0 + j * kThreads < Q) finish(q0 + j * kThreads, qs[j], bi[j], bd[j]);
+                if (q0 + j * kThreads < Q) park(q0 + j * kThreads, bi[j], bd[j]);
             }
           }
           for (int q = tid; q < Q && !(!surf && corner_lds); q += kThreads) {
@@ -485,14 +493,14 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
             float nd;
             const bool ok = nn1_shells(surf ? gs : gc, p, sel, a.dist_sqr, nn, nd);
             if (ok) {
-              finish(q, sel, nn, nd);
+              park(q, nn, nd);
             } else {
               const int k = atomicAdd(&nfb, 1);
               if (k < kFbMax) {
                 fbq[k] = q;
               } else {  // overflow of the queue: the serial scan (same result)
                 nn1_scan(surf ? sl : clg, surf ? Ns : Nc, sel, nn, nd);
-                finish(q, sel, nn, nd);
+                park(q, nn, nd);
               }
             }
           }
@@ -511,11 +519,16 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
             nn1_block_multi(surf ? sl : clg, surf ? Ns : Nc, qs, m, nn, nd, red_d, red_i);
 #pragma unroll
             for (int j = 0; j < kMulti; ++j)
-              if (j < m && tid == j) finish(fbq[k0 + j], qs[j], nn[j], nd[j]);
+              if (j < m && tid == j) park(fbq[k0 + j], nn[j], nd[j]);
           }
           if (tid == 0) nfb = 0;
           __syncthreads();
           LLSR_STAMP(tF);
+          for (int q = tid; q < Q; q += kThreads) {
+            const int* ix = idx + 3 * q;
+            finish(q, to_start(tl, qry[q]), ix[0], __int_as_float(ix[1]));
+          }
+          __syncthreads();
         }
         int nval = 0;
         for (int q = tid; q < Q; q += kThreads) {
