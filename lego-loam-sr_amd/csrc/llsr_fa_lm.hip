@@ -128,7 +128,7 @@ __device__ __forceinline__ void nn1_scan(const float4* pts, int n, float4 q, int
 // slice of the cloud in index order against every query, then each query's (d, index) minima are
 // reduced with the index tie-break — equal to nn1_scan per query, with one pass over the cloud
 // for kMulti queries. Contains barriers: every thread of the block must call it.
-constexpr int kMulti = 4;
+constexpr int kMulti = 2;  // 2 (from 4): 113 instead of 166 spilled VGPRs at the 4-waves bound
 __device__ void nn1_block_multi(const float4* pts, int n, const float4* qs, int nq, int* bi, float* bd,
                                 float (*red_d)[kThreads / 64], int (*red_i)[kThreads / 64]) {
   float d[kMulti];
@@ -479,6 +479,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
               const int wq = Q - (q0 - lane_id());
               const int nj = wq > 3 * kThreads ? 4 : wq > 2 * kThreads ? 3 : wq > kThreads ? 2 : 1;
               if (nj == 1) corner_brute<1>(lcl, Nc, qs, bd, bi);
+              else if constexpr (kMulti == 2) corner_brute<2>(lcl, Nc, qs, bd, bi);
               else if (nj == 2) corner_brute<2>(lcl, Nc, qs, bd, bi);
               else if (nj == 3) corner_brute<3>(lcl, Nc, qs, bd, bi);
               else corner_brute<4>(lcl, Nc, qs, bd, bi);
