@@ -175,9 +175,10 @@ __device__ void is_push(IsRange r, IsRange* nxt, int* n_nxt, IsRange* leaves, in
   else leaves[atomicAdd(n_leaves, 1)] = r;
 }
 
-__global__ __launch_bounds__(kIsT) void k_is_level(unsigned long long* kk, const IsRange* in, int n_in, IsRange* nxt,
-                                                   int* n_nxt, IsRange* leaves, int* n_leaves, int* Lb, int* Rb) {
-  if ((int)blockIdx.x >= n_in) return;
+__global__ __launch_bounds__(kIsT) void k_is_level(unsigned long long* kk, const IsRange* in, const int* n_in,
+                                                   IsRange* nxt, int* n_nxt, IsRange* leaves, int* n_leaves, int* Lb,
+                                                   int* Rb) {
+  if ((int)blockIdx.x >= *n_in) return;  // the grid is an upper bound on this level's ranges
   const IsRange r = in[blockIdx.x];
   unsigned long long* a = kk + r.f;
   int* Lp = Lb + r.f;
@@ -523,7 +524,7 @@ int32_t vg_run(llsr_map* m, const std::vector<VgCloud>& cl, float4* d_out, long 
     const size_t capA = (size_t)(N / kIsLeaf) + S + 2;
     const size_t capL = 84 * ((size_t)(N / kIsLeaf) + 1) + S + 2;
     const size_t o_b = align256(capA * sizeof(IsRange)), o_l = o_b + o_b,
-                 o_c = o_l + align256(capL * sizeof(IsRange)), bytes_is = o_c + 256;
+                 o_c = o_l + align256(capL * sizeof(IsRange)), bytes_is = o_c + 256;  // dcnt: 4 ints
     MAP_OK(m, grow(m->isbuf, m->cap_isbuf, bytes_is));
     if (!m->hcnt) MAP_OK(m, hipHostMalloc((void**)&m->hcnt, 4 * sizeof(int)));
     IsRange* lA = reinterpret_cast<IsRange*>(m->isbuf);
@@ -544,20 +545,33 @@ int32_t vg_run(llsr_map* m, const std::vector<VgCloud>& cl, float4* d_out, long 
       std::memcpy(m->htab + o_h, small.data(), small.size() * sizeof(IsRange));
       MAP_OK(m, hipMemcpyAsync(lL, m->htab + o_h, small.size() * sizeof(IsRange), hipMemcpyHostToDevice, s));
     }
-    m->hcnt[0] = 0;
-    m->hcnt[1] = (int)small.size();
-    MAP_OK(m, hipMemcpyAsync(dcnt, m->hcnt, 2 * sizeof(int), hipMemcpyHostToDevice, s));
-    MAP_OK(m, hipStreamSynchronize(s));
     int nA = (int)big.size();
+    m->hcnt[0] = nA;                 // dcnt[0]: ranges of the current level (device-side)
+    m->hcnt[1] = (int)small.size();  // dcnt[1]: leaves
+    m->hcnt[2] = 0;                  // dcnt[2]: ranges of the next level
+    MAP_OK(m, hipMemcpyAsync(dcnt, m->hcnt, 3 * sizeof(int), hipMemcpyHostToDevice, s));
+    MAP_OK(m, hipStreamSynchronize(s));
+    // partition levels in batches of kLevels launches between host checks: each launch's grid is
+    // an upper bound on its level's ranges (a range pushes at most two; capA bounds them all, the
+    // ranges above kIsLeaf being disjoint), blocks past the device-side count exit at once
+    constexpr int kLevels = 4;
+    int* dA = dcnt;
+    int* dB = dcnt + 2;
     while (nA > 0) {
-      MAP_OK(m, hipMemsetAsync(dcnt, 0, sizeof(int), s));
-      k_is_level<<<nA, kIsT, 0, s>>>(m->key, lA, nA, lB, dcnt, lL, dcnt + 1, m->flag, m->rank);
-      MAP_OK(m, hipGetLastError());
-      MAP_OK(m, hipMemcpyAsync(m->hcnt, dcnt, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+      int bound = nA;
+      for (int k = 0; k < kLevels; ++k) {
+        MAP_OK(m, hipMemsetAsync(dB, 0, sizeof(int), s));
+        k_is_level<<<bound, kIsT, 0, s>>>(m->key, lA, dA, lB, dB, lL, dcnt + 1, m->flag, m->rank);
+        MAP_OK(m, hipGetLastError());
+        std::swap(lA, lB);
+        std::swap(dA, dB);
+        bound = (int)std::min<size_t>(2 * (size_t)bound, capA);
+      }
+      MAP_OK(m, hipMemcpyAsync(m->hcnt, dA, sizeof(int), hipMemcpyDeviceToHost, s));
+      MAP_OK(m, hipMemcpyAsync(m->hcnt + 1, dcnt + 1, sizeof(int), hipMemcpyDeviceToHost, s));
       MAP_OK(m, hipStreamSynchronize(s));
       nA = m->hcnt[0];
       if ((size_t)nA > capA || (size_t)m->hcnt[1] > capL) return mfail(m, LLSR_EIO, "voxel grid: introsort range lists overflow");
-      std::swap(lA, lB);
     }
     const int nLeaves = m->hcnt[1];
     if (nLeaves > 0) k_is_leaf<<<nLeaves, 64, 0, s>>>(m->key, lL);
