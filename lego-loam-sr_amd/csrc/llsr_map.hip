@@ -532,25 +532,25 @@ int32_t vg_run(llsr_map* m, const std::vector<VgCloud>& cl, float4* d_out, long 
     IsRange* lL = reinterpret_cast<IsRange*>(m->isbuf + o_l);
     int* dcnt = reinterpret_cast<int*>(m->isbuf + o_c);
     // the host tables above were uploaded from htab asynchronously: stage the ranges after them
-    const size_t o_h = align256(bytes) , hneed = o_h + align256(std::max(big.size(), small.size()) * sizeof(IsRange) + 1);
+    const size_t o_h = align256(bytes), o_h2 = o_h + align256(big.size() * sizeof(IsRange) + 1),
+                 hneed = o_h2 + align256(small.size() * sizeof(IsRange) + 1);  // big, then small ranges
     MAP_OK(m, hipStreamSynchronize(s));
     MAP_OK(m, host_grow(m->htab, m->cap_htab, hneed + align256((S + 1) * sizeof(long long))));
     // (host_grow may have moved htab: re-stage the offsets area after the sort, below)
     if (!big.empty()) {
       std::memcpy(m->htab + o_h, big.data(), big.size() * sizeof(IsRange));
       MAP_OK(m, hipMemcpyAsync(lA, m->htab + o_h, big.size() * sizeof(IsRange), hipMemcpyHostToDevice, s));
-      MAP_OK(m, hipStreamSynchronize(s));
     }
     if (!small.empty()) {
-      std::memcpy(m->htab + o_h, small.data(), small.size() * sizeof(IsRange));
-      MAP_OK(m, hipMemcpyAsync(lL, m->htab + o_h, small.size() * sizeof(IsRange), hipMemcpyHostToDevice, s));
+      std::memcpy(m->htab + o_h2, small.data(), small.size() * sizeof(IsRange));
+      MAP_OK(m, hipMemcpyAsync(lL, m->htab + o_h2, small.size() * sizeof(IsRange), hipMemcpyHostToDevice, s));
     }
     int nA = (int)big.size();
     m->hcnt[0] = nA;                 // dcnt[0]: ranges of the current level (device-side)
     m->hcnt[1] = (int)small.size();  // dcnt[1]: leaves
     m->hcnt[2] = 0;                  // dcnt[2]: ranges of the next level
+    // (the pinned staging above is not touched again before the next synchronisation below)
     MAP_OK(m, hipMemcpyAsync(dcnt, m->hcnt, 3 * sizeof(int), hipMemcpyHostToDevice, s));
-    MAP_OK(m, hipStreamSynchronize(s));
     // partition levels in batches of kLevels launches between host checks: each launch's grid is
     // an upper bound on its level's ranges (a range pushes at most two; capA bounds them all, the
     // ranges above kIsLeaf being disjoint), blocks past the device-side count exit at once
