@@ -286,7 +286,9 @@ int32_t llsr_scan2scan_stats(llsr_handle* h, llsr_s2s_stats* out);
  * each kind with b % W == r) and writes int64 fixed-point partial sums, LLSR_NE_WORDS per
  * problem: AtA upper triangle (21, row-major), AtB (6), sum |coeff.intensity|, #corner, #surf
  * correspondences, 2 spare; every term is rounded once to a multiple of 2^-30 before it is
- * added. Integer sums are associative, so the summed words, and therefore every pose, are
+ * added. Range: a term must satisfy |v| < 2^32 and the sums stay exact while sum |term| < 2^33 per
+ * word (e.g. 20k correspondences with |J|^2 up to 4e5, points ~600 m away); a non-finite or
+ * out-of-range term contributes 0, is counted, and the step returns LLSR_ERANGE. Integer sums are associative, so the summed words, and therefore every pose, are
  * bit-identical for any W and any all-reduce order (they differ from llsr_scan2map_batch's float
  * sums only by that rounding: well inside the 1e-4 pose tolerance). Per batch:
  *   llsr_scan2map_shard_begin(h, batch, stream)              (reserve as for llsr_scan2map_batch)
