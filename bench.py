@@ -80,13 +80,101 @@ def cpu_baseline(scans: list[np.ndarray], budget_s: float) -> dict:
             "ip_ms": ip_ms / n, "fa_features_ms": fa_ms / n}
 
 
-def lm_traffic(kernel: str, problems: int):
+def _ipfa_cpu_worker(args):
+    """One process of the headline's all-core CPU baseline: the oracle IP + FA-feature path over
+    the given scans (cycled) for `budget` seconds, one thread; returns (scans, busy seconds)."""
+    scans, budget = args
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle_py
+    from llsr import _abi
+    ora = oracle_py.Oracle(_abi.config_for("vlp16"), pcl_voxel_order=True)
+    ora.process(scans[0])
+    n, t0 = 0, time.perf_counter()
+    while True:
+        ora.process(scans[n % len(scans)])
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget and n >= 10:
+            return n, el
+
+
+def cpu_baseline_all_cores(scans: list[np.ndarray], budget_s: float) -> dict:
+    """all-core throughput of the headline path = independent single-threaded
+    pipelines, one per host core the job is granted (16 on the GPU pool), each cycling the scans."""
+    import multiprocessing as mp
+    nproc = min(16, os.cpu_count() or 1)
+    t1 = time.perf_counter()
+    with mp.get_context("spawn").Pool(nproc) as pool:
+        res = pool.map(_ipfa_cpu_worker, [(scans, budget_s)] * nproc)
+    wall = time.perf_counter() - t1
+    n = sum(r[0] for r in res)
+    busy = max(r[1] for r in res)
+    return {"value": round(n / busy, 1), "unit": "scans/s", "cores": nproc, "kind": "port", "cpu": cpu_model(),
+            "sample": f"{nproc} processes x the oracle IP+FA-feature path, {n} scans in all, slowest process "
+                      f"{busy:.1f} s busy ({wall:.1f} s wall incl. start-up)"}
+
+
+def cpu_stage_times(budget_s: float, frames: int = 40) -> dict:
+    """BASELINE.md §2 per-stage CPU times of the whole reference pipeline on one VLP-16 drive
+    through the oracle chain (oracle_py.OracleMapping, MapOptimization in the lm_applied mode):
+    t_IP (ImageProjection), t_FA (feature stage + scan-to-scan LM + integrate + last clouds), t_MO
+    (OdometryToTransform .. saveKeyFramesAndFactor incl. the local map); frames after the second
+    (the first scan sends no AssociationOut, the second meets an empty map). Sequential scans/s =
+    1 / (t_IP + t_FA + t_MO), pipelined (one thread per node, as the reference runs) = 1 / max."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle_py
+    from llsr import _abi, synth
+    cfg = _abi.config_for("vlp16")
+    cfg.mode = _abi.LLSR_MODE_LM_APPLIED
+    om = oracle_py.OracleMapping(cfg, _abi.LLSR_MODE_LM_APPLIED)
+    odo_process = om.odo.process
+    t_odo = [0.0]
+
+    def timed_odo(x):
+        t1 = time.perf_counter()
+        r = odo_process(x)
+        t_odo[0] = time.perf_counter() - t1
+        return r
+
+    om.odo.process = timed_odo
+    ip = fa = mo = 0.0
+    n, spent = 0, 0.0
+    for k in range(frames):
+        scan = synth.make_scan(1 + k, "vlp16")
+        t1 = time.perf_counter()
+        om.process(scan)
+        tot = time.perf_counter() - t1
+        if k < 2:
+            continue
+        t_ip = om.odo.ora.stage_ms()[0] * 1e-3
+        ip += t_ip
+        fa += t_odo[0] - t_ip
+        mo += tot - t_odo[0]
+        n += 1
+        spent += tot
+        if spent >= budget_s and n >= 3:
+            break
+    ip, fa, mo = ip / n * 1e3, fa / n * 1e3, mo / n * 1e3
+    return {"per_stage_ms": {"IP": round(ip, 3), "FA": round(fa, 3), "MO_lm_applied": round(mo, 3)},
+            "sequential_scans_per_s": round(1e3 / (ip + fa + mo), 2),
+            "pipelined_scans_per_s": round(1e3 / max(ip, fa, mo), 2),
+            "cores": 1, "cpu": cpu_model(), "mo_mode": "lm_applied",
+            "sample": f"frames 3..{n + 2} of one VLP-16 drive through oracle_py.OracleMapping (C++ restatement, "
+                      "1 thread per stage)"}
+
+
+def lm_traffic(kernel: str, problems: int, leg: str | None = None):
     """PMC-measured HBM bytes per launch of an LM kernel (scripts/pmc_lm.sh, committed as
-    profiles/traffic_lm_latest.json), or None when it was measured at another batch size."""
+    profiles/traffic_lm_latest.json; records keyed "kernel" or "kernel@leg"), or None when it was
+    measured at another batch size."""
     f = os.environ.get("LLSR_TRAFFIC_LM_JSON", os.path.join(REPO, "profiles", "traffic_lm_latest.json"))
     if not os.path.exists(f):
         return None
-    rec = json.load(open(f)).get("kernels", {}).get(kernel)
+    ks = json.load(open(f)).get("kernels", {})
+    rec = ks.get(f"{kernel}@{leg}") if leg else None
+    rec = rec or ks.get(kernel)
+    if rec and leg and rec.get("leg_key", leg) != leg:
+        return None
     return rec["hbm_bytes_per_launch"] if rec and rec.get("problems") == problems else None
 
 
@@ -191,9 +279,9 @@ def scan2map_leg(dev, mode_name: str, P: int, steps: int, warmup: int, dist, run
                      "traffic": lm_traffic("k_s2m_iter", P), "algorithmic_bytes_per_step": lm_bytes,
                      "algorithmic_bytes_per_launch": lm_bytes / max(1, launches_per_batch),
                      "avg_launch_ms": round(per_launch_ms, 4),
-                     "note": "iterate window includes the host's convergence polls (every 4 launches); "
-                             "traffic = PMC HBM bytes per launch: the kNN-5 walks of 27 cells per query "
-                             "read far more than the 96 B per query of SURVEY 8(d)"},
+                     "note": "bytes = SURVEY 8(d) B_lm per iteration; iterate window includes the host's "
+                             "convergence polls (every 4 launches); traffic = PMC HBM bytes per launch "
+                             "(the kNN-5 cell walks and the maps beyond the XCD L2s)"},
     }
     if run_cpu:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -229,7 +317,8 @@ def scan2map_allreduce_leg(dev, P: int, steps: int, warmup: int, dist, check: bo
     """configs[4]: B = P scans per step, every scan's scan-to-map correspondences split over all
     ranks (llsr_scan2map_shard_*), ONE RCCL all-reduce of the [P][32] int64 normal equations per
     LM iteration (llsr.dist.sharded_scan2map); every rank solves the same 6x6 systems. The total
-    work is fixed as N grows (strong scaling of one batch); at N = 1 no collective runs."""
+    work is fixed as N grows (strong scaling of one batch); at N = 1 the all-reduce still runs
+    through RCCL on a one-rank group (an in-place identity), so allreduce_us is RCCL's latency."""
     import torch
     from llsr import Pipeline, _abi, default_config
     from llsr.dist import HipShardEngine, allreduce_latency_us, max_over_ranks, sharded_scan2map
@@ -270,7 +359,8 @@ def scan2map_allreduce_leg(dev, P: int, steps: int, warmup: int, dist, check: bo
 
     def step():
         pose.copy_(pose0)
-        iters.append(sharded_scan2map(eng, ne, cfg.iterCountThres, poll=2))
+        # the all-reduce runs through RCCL at every world size (at N = 1: a one-rank group)
+        iters.append(sharded_scan2map(eng, ne, cfg.iterCountThres, poll=2, force_collective=True))
 
     for _ in range(warmup):
         step()
@@ -360,13 +450,15 @@ def odometry_leg(dev, lidar: str, B: int, seqs: int, frames: int, steps: int, wa
     st = pipe.scan2scan_stats()
     pipe.set_profiling(False)
     cnt = pipe.batch_counts(B)  # N, S, O, M, sharp, F, L, K of the last batch
-    # LM bytes per problem: every iteration reads each query (16 B) and writes its
-    # Jacobian row + residual (16 B); every 5th iteration also gathers the tripod (3 x 16 B) from
-    # the last clouds; the grids are rebuilt once per scan (32 B per last-cloud point)
+    # k_s2s_lm's compulsory HBM bytes per launch: each query (sharp + flat + shadow,
+    # 16 B) and each point of the two last clouds' cell-sorted copies (16 B) read once; the
+    # per-iteration re-reads stay on chip (LDS / L2) and are not counted, so this is a lower bound
+    # that the PMC `traffic` must meet (model <= traffic)
     reps = [pipe.odometry_fetch(b)["lm"] for b in range(0, B, max(1, B // 64))]
     q_mean = float(np.mean(cnt[:, 4] + cnt[:, 5] + 160))
     it_mean = float(np.mean([r["surf_iterations"] + r["corner_iterations"] for r in reps]))
-    lm_bytes = B * q_mean * (32.0 * it_mean + 48.0 * np.ceil(it_mean / 5.0))
+    last_mean = float(np.mean(cnt[:, 3] + cnt[:, 6] + 160))  # M + L + shadow: the next frame's last clouds
+    lm_bytes = B * 16.0 * (q_mean + last_mean)
     lm_ms = st["lm_ms"] / max(1, st["batches"])
     N = float(cnt[:, 0].sum())
     proj_ms = kt["k_project"] + kt["k_gather_column"]
@@ -384,10 +476,11 @@ def odometry_leg(dev, lidar: str, B: int, seqs: int, frames: int, steps: int, wa
            "sequences_per_gpu": B, "steps": steps, "ms_per_step": round(el / steps * 1e3, 3),
            "slot0_frames": s0["frames"], "slot0_lm_iterations": [s0["lm"]["surf_iterations"], s0["lm"]["corner_iterations"]],
            "roofline": {**roof("k_s2s_lm", lm_bytes, lm_ms,
-                                "dominant kernel of the leg; bytes = queries x (32 B per iteration + 48 B "
-                                "tripod gather every 5th), latency-bound (one workgroup per scan, ordered "
-                                "sums); traffic = PMC HBM bytes per launch (the ring-window walks)"),
-                         "traffic": lm_traffic("k_s2s_lm", B)},
+                                "dominant kernel of the leg; compulsory bytes = 16 B per query + 16 B per "
+                                "last-cloud point, each read once per launch (iterations re-read on chip); "
+                                "latency-bound (one workgroup per scan, ordered sums); traffic = PMC HBM "
+                                "bytes per launch"),
+                         "traffic": lm_traffic("k_s2s_lm", B, "odometry " + lidar)},
            "roofline_projection": roof("k_project" if not hdl else "k_project+k_gather_column", bpc_proj, proj_ms,
                                        "SURVEY 8(d) B_pc projection part 20 N + 24 HW (+ 5 HW raw intensity "
                                        "and ground) over the projection kernels"),
@@ -729,6 +822,11 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
+    rccl1 = None  # world 1: a one-rank RCCL group for the configs[4] leg's per-iteration all-reduce
+    if world == 1 and args.allreduce_scans > 0:
+        import torch.distributed as rccl1
+        rccl1.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1,
+                                 device_id=torch.device("cuda", dev))
 
     from llsr import Pipeline, default_config, synth
     cfg = default_config("vlp16")
@@ -867,7 +965,7 @@ def main():
 
     allred = None
     if args.allreduce_scans > 0:
-        allred = scan2map_allreduce_leg(dev, args.allreduce_scans, args.s2m_steps, 1, dist,
+        allred = scan2map_allreduce_leg(dev, args.allreduce_scans, args.s2m_steps, 1, dist or rccl1,
                                         rank == 0 and not args.no_cpu)
 
     if rank == 0:
@@ -908,12 +1006,18 @@ def main():
         if not args.no_cpu and world == 1:
             scans = [pts[off[k]:off[k + 1]] for k in range(min(args.distinct, B))]
             out["cpu_baseline"] = cpu_baseline(scans, args.cpu_seconds)
+            out["cpu_baseline"]["cpu"] = cpu_model()
             out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
+            out["cpu_baseline_all_cores"] = cpu_baseline_all_cores(scans, min(args.cpu_seconds, 10.0))
+            out["speedup_vs_cpu_all_cores"] = round(value / out["cpu_baseline_all_cores"]["value"], 1)
+            out["cpu_pipeline_stages"] = cpu_stage_times(min(args.cpu_seconds, 10.0))
         print(json.dumps(out), flush=True)
     for p_ in pipes:
         p_.close()
     if dist:
         dist.destroy_process_group()
+    elif rccl1 is not None:
+        rccl1.destroy_process_group()
 
 
 if __name__ == "__main__":

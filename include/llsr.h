@@ -345,13 +345,14 @@ int32_t llsr_odometry_reset(llsr_handle* h);
 
 /* ---- MapOptimization local map (llsr_map.hip) ----
  * The keyframe store of saveKeyFramesAndFactor (MO:1686-1752) kept in HBM, the local-map assembly
- * of extractSurroundingKeyFrames (MO:1151-1231, loop closure disabled as in every config block,
- * CFG:23) and the downSizeFilter* VoxelGrids (MO:92-104; downsampleCurrentScan MO:1234-1267), on
- * the device. A llsr_map is independent of any llsr_handle, one per mapped sequence; it owns a
- * non-blocking stream used when hip_stream is NULL. Point clouds are float4 x, y, z, intensity.
- * VoxelGrid = pcl::VoxelGrid<PointXYZI>::filter (downsample_all_data, 0 min points): same voxel
- * set and output order (ascending voxel index) as PCL; each centroid sums its voxel's points in
- * input order (PCL sums them in std::sort's order: float rounding only). */
+ * of extractSurroundingKeyFrames (MO:1096-1231, both branches: the key-pose radius search of the
+ * VLP-16 block, enable_loop_closure false at CFG:23, and the recent-keyframe queue of the VLP-32c /
+ * HDL-64E blocks, enable_loop_closure true at CFG:91, 159) and the downSizeFilter* VoxelGrids
+ * (MO:92-104; downsampleCurrentScan MO:1234-1267), on the device. A llsr_map is independent of any
+ * llsr_handle, one per mapped sequence; it owns a non-blocking stream used when hip_stream is NULL.
+ * Point clouds are float4 x, y, z, intensity. VoxelGrid = pcl::VoxelGrid<PointXYZI>::filter
+ * (downsample_all_data, 0 min points): same voxel set and output order (ascending voxel index) as
+ * PCL, each centroid summed in the order libstdc++'s std::sort leaves PCL's index_vector. */
 typedef struct llsr_map llsr_map;
 typedef struct llsr_map_config {
   float surrounding_radius;  /* surrounding_keyframe_search_radius, 50 m (CFG:26) */
@@ -359,8 +360,20 @@ typedef struct llsr_map_config {
   float corner_leaf;         /* downSizeFilterCorner, 0.2 (MO:92) */
   float surf_leaf;           /* downSizeFilterSurf, 0.4 (MO:93) */
   float outlier_leaf;        /* downSizeFilterOutlier, 0.4 (MO:94) */
+  /* mapping.enable_loop_closure (CFG:23 / 91 / 159). Non-zero selects the branch of
+   * extractSurroundingKeyFrames at MO:1099-1151: the local map is the last
+   * surrounding_keyframe_search_num keyframes, refilled from the newest backwards while the queue
+   * is short, then one pop-oldest / push-newest per call whenever the newest keyframe index changed
+   * (latestFrameID, MO:1126-1134). The loop-closure ICP thread itself is commented out in the
+   * reference (MO:174), so this flag changes only the local map. */
+  int32_t enable_loop_closure;
+  int32_t surrounding_keyframe_search_num;  /* 50 (CFG:27 / 95 / 163) */
 } llsr_map_config;
+/* VLP-16 block: radius branch (enable_loop_closure 0), search num 50, the leaves above. */
 int32_t llsr_map_config_default(llsr_map_config* cfg);
+/* The block of loam_config.yaml for `lidar` (LLSR_LIDAR_VLP16: CFG:20-27; LLSR_LIDAR_HDL64E:
+ * CFG:156-163, enable_loop_closure 1). */
+int32_t llsr_map_config_lidar(llsr_map_config* cfg, int32_t lidar);
 llsr_map* llsr_map_create(const llsr_map_config* cfg, int32_t hip_device);
 void llsr_map_destroy(llsr_map* m);
 const char* llsr_map_last_error(const llsr_map* m);
@@ -389,10 +402,12 @@ int32_t llsr_map_add_keyframe(llsr_map* m, const float pose[6], const float* cor
                               void* hip_stream);
 int32_t llsr_map_num_keyframes(const llsr_map* m);
 typedef struct llsr_map_report {
-  int32_t n_in_radius;     /* key poses within surrounding_radius (MO:1157-1164) */
-  int32_t n_poses_ds;      /* surroundingKeyPosesDS size (MO:1166-1167) */
-  int32_t n_keyframes;     /* surroundingExistingKeyPosesID size after the update */
-  int32_t n_transformed;   /* keyframes newly added to the list this call (MO:1205-1220) */
+  int32_t n_in_radius;     /* key poses within surrounding_radius (MO:1157-1164); 0 with loop closure */
+  int32_t n_poses_ds;      /* surroundingKeyPosesDS size (MO:1166-1167); 0 with loop closure */
+  int32_t n_keyframes;     /* surroundingExistingKeyPosesID size after the update (loop closure:
+                              recentCornerCloudKeyFrames size) */
+  int32_t n_transformed;   /* keyframes newly added to the list this call (MO:1205-1220; loop
+                              closure: pushed onto the queue, MO:1115-1120 / 1138-1143) */
   int64_t n_corner_map;    /* laserCloudCornerFromMap before / after VoxelGrid */
   int64_t n_surf_map;      /* laserCloudSurfFromMap (surf + outlier keyframe clouds) */
   int64_t n_corner_ds;
@@ -400,18 +415,21 @@ typedef struct llsr_map_report {
   float ms;                /* wall time of the call */
 } llsr_map_report;
 /* extractSurroundingKeyFrames (MO:1096-1232) around robot_pos (currentRobotPosPoint = x, y, z of
- * transformAftMapped): the corner / surf local maps (…FromMapDS) into d_corner / d_surf (device,
- * capacities in points; LLSR_ERANGE with the sizes in rep when they do not fit). Synchronises. */
+ * transformAftMapped; unused with loop closure): the corner / surf local maps (…FromMapDS) into
+ * d_corner / d_surf (device, capacities in points; LLSR_ERANGE with the sizes in rep when they do
+ * not fit). Synchronises. */
 int32_t llsr_map_extract(llsr_map* m, const float robot_pos[3], float* d_corner, int64_t cap_corner, float* d_surf,
                          int64_t cap_surf, llsr_map_report* rep, void* hip_stream);
-/* surroundingExistingKeyPosesID after the last extract; returns its length. */
+/* surroundingExistingKeyPosesID (loop closure: the queue's keyframe indices, oldest first) after the
+ * last extract; returns its length. */
 int32_t llsr_map_keyframe_ids(const llsr_map* m, int32_t* out, int32_t cap);
 
 /* ---- Mapping chain: ImageProjection -> FeatureAssociation -> MapOptimization::run ----
- * (mapOptmization.cpp:1854-1896, one AssociationOut per odometry frame, mapping_frequency_divider
- * 1, loop closure disabled as in every config block.) Each llsr_mapping_batch call runs
- * llsr_odometry_batch on the B slots and then, for every slot past its first scan (the first
- * scan sends no AssociationOut, FA:2781-2784): OdometryToTransform of the published odometry
+ * (mapOptmization.cpp:1854-1896.) Each llsr_mapping_batch call runs llsr_odometry_batch on the B
+ * slots and then, for every slot that sends an AssociationOut this frame — FA counts the frames
+ * after the first (the first scan sends nothing, FA:2781-2784) and sends on every
+ * mapping_frequency_divider-th of them (FA:2818-2821; llsr_config.mapping_frequency_divider, 1 in
+ * every config block; a value < 1 never sends, as in the reference) — OdometryToTransform of the published odometry
  * (tf2 round trip, FA:2612-2625 / utility.h:99-113), transformAssociateToMap (MO:458-581),
  * extractSurroundingKeyFrames on the slot's keyframe store (MO:1096-1232), downsampleCurrentScan
  * of the AssociationOut clouds (corner / surf last, the adjustOutlierCloud'ed IP outliers
@@ -422,7 +440,11 @@ int32_t llsr_map_keyframe_ids(const llsr_map* m, int32_t* out, int32_t cap);
  * iSAM2's estimate at the initial values, so the key pose is transformTobeMapped for the first
  * keyframe and transformAftMapped after). Requires the handle's mode LLSR_MODE_LM_APPLIED
  * (the odometry's); `mo_mode` selects MapOptimization's own LM mode (LLSR_MODE_FAITHFUL: the pose
- * update at MO:1539-1545 stays commented out, as in the reference). Synchronises per call. */
+ * update at MO:1539-1545 stays commented out, as in the reference). map_cfg NULL selects the
+ * config block of the handle's lidar (llsr_map_config_lidar: HDL-64E when num_vertical_scans is
+ * 64, else VLP-16), which decides the local-map branch (enable_loop_closure). Synchronises per
+ * call. An error from the MapOptimization part of a call (after the odometry advanced) leaves every
+ * slot's MapOptimization members (poses, keyframes, local-map queue, LM members) as before the call. */
 typedef struct llsr_mapping_slot {
   int32_t frames;               /* scans consumed by the slot (odometry frames) */
   int32_t mo_frames;            /* MapOptimization::run iterations = frames - 1 once frames >= 2 */

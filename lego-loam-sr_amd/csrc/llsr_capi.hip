@@ -66,8 +66,13 @@ struct llsr_handle {
   float4* d_in = nullptr;      // single-scan staging
   int64_t* d_off = nullptr;
   hipStream_t stream = nullptr;
-  hipStream_t last_stream = nullptr;
+  hipStream_t last_stream = nullptr;  // compared, never used: the caller may destroy its streams
   hipEvent_t last_done = nullptr;  // recorded after each batch: the next one (any stream) waits on it
+  // Handle-owned completion events of the last work enqueued on a caller's stream, per kind
+  // (feature batches / odometry / mapping, scan-to-scan, scan-to-map): buffer re-allocation and
+  // llsr_destroy wait on these, so a stream the caller destroyed since is never touched.
+  hipEvent_t s2s_done = nullptr, mo_done = nullptr;
+  bool last_rec = false, s2s_rec = false, mo_rec = false;
   int last_B = 0;
   const float4* last_pts = nullptr;  // inputs of the last batch (diagnostic re-launches only)
   const int64_t* last_off = nullptr;
@@ -91,7 +96,6 @@ struct llsr_handle {
     llsr_s2m_stats stats{};
     S2MArgs sh{};                // the open split-correspondence batch (llsr_scan2map_shard_*)
     bool sh_live = false;
-    hipStream_t last = nullptr;  // stream of the last scan-to-map launch
   } mo;
   // scan-to-scan (llsr_scan2scan_*)
   struct {
@@ -101,7 +105,6 @@ struct llsr_handle {
     int* host_flag = nullptr;
     void* stage = nullptr;
     size_t stage_bytes = 0;
-    hipStream_t last = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     hipEvent_t p0 = nullptr, p1 = nullptr, p2 = nullptr;  // profiling: start, grids built, LM done
     llsr_s2s_stats stats{};
@@ -131,6 +134,7 @@ struct llsr_handle {
     llsr_map* map = nullptr;           // keyframe store (cornerCloudKeyFrames etc., cloudKeyPoses6D)
     float robot[3] = {0, 0, 0};        // currentRobotPosPoint
     int frames = 0, mo_frames = 0, lm_ran = 0, n_cq = 0, n_sq = 0;
+    int cycle = 0;                     // FeatureAssociation's _cycle_count (FA:2818-2821)
     llsr_lm_report lm{};
     llsr_map_report mrep{};
     std::vector<float> keyposes;       // [keyframes][6]
@@ -143,9 +147,11 @@ struct llsr_handle {
     std::vector<MapSlot> slot;
     float4 *outl = nullptr, *ds = nullptr, *tot = nullptr, *cmap = nullptr;  // cmap: empty-map base
     size_t cap_outl = 0, cap_ds = 0, cap_tot = 0, cap_cmap = 0;
-    void* small = nullptr;             // device: pose [B][6], report [B], deg [B], matP [B][36], off [5][B+1]
+    void* small = nullptr;             // device: pose [B][6], report [B], deg [B], matP [B][36], off [5][B+1],
+                                       // and the deg / matP of the frame before (rollback)
     void* hsmall = nullptr;            // pinned host mirror
     float* d_pose = nullptr; llsr_lm_report* d_rep = nullptr; int* d_deg = nullptr; float* d_matP = nullptr;
+    int* d_deg_bak = nullptr; float* d_matP_bak = nullptr;
     int64_t* d_off = nullptr;
     float* h_pose = nullptr; llsr_lm_report* h_rep = nullptr; int64_t* h_off = nullptr; int* h_frames = nullptr;
     float* h_tsum = nullptr;
@@ -238,6 +244,8 @@ static T* carve(char*& p, size_t n) {
   p += (n * sizeof(T) + 255) & ~size_t(255);
   return r;
 }
+
+static void mapping_free(llsr_handle* h);
 
 // Wait for every stream this handle has launched work on (before its buffers are re-allocated):
 // stream-scoped, so other handles' streams on the device keep running.
@@ -340,7 +348,9 @@ extern "C" int32_t llsr_create(const llsr_config* cfg, int32_t hip_device, int32
   for (auto& set : h->ev)
     for (auto& e : set)
       if (hipEventCreate(&e) != hipSuccess) { llsr_destroy(h); return LLSR_ENODEV; }
-  if (hipEventCreateWithFlags(&h->last_done, hipEventDisableTiming) != hipSuccess) {
+  if (hipEventCreateWithFlags(&h->last_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->s2s_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->mo_done, hipEventDisableTiming) != hipSuccess) {
     llsr_destroy(h);
     return LLSR_ENODEV;
   }
@@ -368,12 +378,12 @@ extern "C" int32_t llsr_create(const llsr_config* cfg, int32_t hip_device, int32
 extern "C" void llsr_destroy(llsr_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
-  if (h->stream) (void)hipStreamSynchronize(h->stream);
-  if (h->last_stream) (void)hipStreamSynchronize(h->last_stream);
+  (void)sync_handle_streams(h);
   for (auto& set : h->ev)
     for (auto& e : set)
       if (e) (void)hipEventDestroy(e);
-  if (h->last_done) (void)hipEventDestroy(h->last_done);
+  for (hipEvent_t e : {h->last_done, h->s2s_done, h->mo_done})
+    if (e) (void)hipEventDestroy(e);
   if (h->pool) (void)hipFree(h->pool);
   if (h->mo.pool) (void)hipFree(h->mo.pool);
   if (h->s2s.pool) (void)hipFree(h->s2s.pool);
@@ -392,12 +402,9 @@ extern "C" void llsr_destroy(llsr_handle* h) {
   if (h->mo.e1) (void)hipEventDestroy(h->mo.e1);
   for (hipEvent_t e : {h->mo.p0, h->mo.p1, h->mo.p2})
     if (e) (void)hipEventDestroy(e);
-  for (auto& sl : h->mp.slot)
-    if (sl.map) llsr_map_destroy(sl.map);
-  if (h->mp.vg) llsr_map_destroy(h->mp.vg);
-  for (void* p : {(void*)h->mp.outl, (void*)h->mp.ds, (void*)h->mp.tot, (void*)h->mp.cmap, h->mp.small})
+  mapping_free(h);
+  for (void* p : {(void*)h->mp.outl, (void*)h->mp.ds, (void*)h->mp.tot, (void*)h->mp.cmap})
     if (p) (void)hipFree(p);
-  if (h->mp.hsmall) (void)hipHostFree(h->mp.hsmall);
   if (h->d_in) (void)hipFree(h->d_in);
   if (h->d_off) (void)hipFree(h->d_off);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -405,9 +412,15 @@ extern "C" void llsr_destroy(llsr_handle* h) {
 }
 
 static hipError_t sync_handle_streams(llsr_handle* h) {
-  for (hipStream_t st : {h->stream, h->last_stream, h->s2s.last, h->mo.last}) {
-    if (!st) continue;
-    const hipError_t e = hipStreamSynchronize(st);
+  if (h->stream) {
+    const hipError_t e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return e;
+  }
+  const std::pair<hipEvent_t, bool> evs[] = {{h->last_done, h->last_rec}, {h->s2s_done, h->s2s_rec},
+                                             {h->mo_done, h->mo_rec}};
+  for (const auto& ev : evs) {
+    if (!ev.first || !ev.second) continue;
+    const hipError_t e = hipEventSynchronize(ev.first);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -524,6 +537,7 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   mark();
   HIP_OK(h, hipGetLastError());
   HIP_OK(h, hipEventRecord(h->last_done, s));
+  h->last_rec = true;
   if (h->profiling) {
     h->ring_head = (h->ring_head + 1) % llsr_handle::kRing;
     h->ring_used += 1;
@@ -537,7 +551,8 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
 
 static int32_t sync_last(llsr_handle* h) {
   HIP_OK(h, hipSetDevice(h->device));
-  HIP_OK(h, hipStreamSynchronize(h->last_stream ? h->last_stream : h->stream));
+  if (h->last_rec) HIP_OK(h, hipEventSynchronize(h->last_done));
+  else HIP_OK(h, hipStreamSynchronize(h->stream));
   return LLSR_OK;
 }
 
@@ -609,7 +624,7 @@ extern "C" float llsr_debug_phase_ms(llsr_handle* h, int32_t k, int32_t phase, i
   c.dbg_phase = phase;
   const int B = h->last_B;
   hipEvent_t e0 = h->ev[0][0], e1 = h->ev[0][1];
-  if (hipStreamSynchronize(h->last_stream ? h->last_stream : s) != hipSuccess) return -1.f;
+  if (sync_last(h) != LLSR_OK) return -1.f;
   (void)hipEventRecord(e0, s);
   for (int r = 0; r < reps; ++r) {
     switch (k) {
@@ -750,11 +765,15 @@ extern "C" int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t P, int32_t mc, 
   m.blocks = m.blocks_c + (qs + 255) / 256;
   if (m.blocks == 0) m.blocks = 1;  // one (empty) block still runs each iteration's solve
   const size_t Tc = (size_t)1 << m.log2T_c, Ts = (size_t)1 << m.log2T_s;
+  // Eigen's GEMM depth blocks of up to qc + qs rows: kc >= 344 once k exceeds max_kc = 680
+  // (llsr_eigen::gemm_kc), so at most ceil(N / 344) blocks; k_s2m_solve keeps 64 in LDS
+  const long long n_rows = (long long)qc + qs;
+  const int spill_cap = std::max(0, (int)((n_rows + 343) / 344) - 64);
   const size_t bytes = sizeof(S2MProb) * P + sizeof(CellSlot) * P * (Tc + Ts) +
                        sizeof(float4) * P * ((size_t)mc + ms) + sizeof(int2) * P * ((size_t)mc + ms) +
                        sizeof(int) * 2 * P +
                        sizeof(float4) * 2 * 256 * (size_t)P * m.blocks + sizeof(int) * (size_t)P * m.blocks +
-                       4096 + 10 * 256;
+                       sizeof(float) * 29 * (size_t)P * spill_cap + 4096 + 11 * 256;
   if (hipMalloc(&m.pool, bytes) != hipSuccess) {
     m.pool = nullptr;
     m.P = 0;
@@ -784,6 +803,8 @@ extern "C" int32_t llsr_scan2map_reserve(llsr_handle* h, int32_t P, int32_t mc, 
       hipSuccess)
     return fail(h, LLSR_ENODEV, "k_s2m_solve LDS attribute");
   a.bcnt = carve<int>(q, (size_t)P * m.blocks);
+  a.blk_spill = carve<float>(q, 29 * (size_t)P * spill_cap);
+  a.spill_cap = spill_cap;
   a.n_active = carve<int>(q, 2);
   a.error = a.n_active + 1;
   a.cap_qc = qc; a.cap_qs = qs; a.cap_mc = mc; a.cap_ms = ms;
@@ -825,10 +846,14 @@ static int32_t s2m_prepare(llsr_handle* h, const llsr_s2m_batch* b, hipStream_t 
   a.deg_in = opt.deg_in; a.matP_in = opt.matP_in;
   a.deg_out = opt.deg_out; a.matP_out = opt.matP_out;
   a.iter_max = h->cfg.iterCountThres;
-  {
+#ifdef LLSR_S2S_PROF
+  {  // diagnostics build only: k_s2m_solve stops after stage LLSR_S2M_DBG (scripts/)
     const char* dbg = std::getenv("LLSR_S2M_DBG");
     a.dbg = dbg ? std::atoi(dbg) : 0;
   }
+#else
+  a.dbg = 0;
+#endif
   a.step_size = h->cfg.step_size;
   a.stop_thres = h->cfg.stop_thres;
   a.cq = b->corner_q; a.cq_off = b->corner_q_off;
@@ -857,8 +882,11 @@ static int32_t s2m_batch(llsr_handle* h, const llsr_s2m_batch* b, hipStream_t s,
   if (h->profiling && m.pool) HIP_OK(h, hipEventRecord(m.p0, s));
   S2MArgs a{};
   m.sh_live = false;  // one scan-to-map batch per handle at a time: this one replaces a shard batch
-  m.last = s;
+  // the scan-to-map buffers are the handle's: start after its previous scan-to-map work (any stream)
+  if (h->mo_rec) HIP_OK(h, hipStreamWaitEvent(s, h->mo_done, 0));
   int32_t rc = s2m_prepare(h, b, s, a, opt);
+  h->mo_rec = true;
+  HIP_OK(h, hipEventRecord(h->mo_done, s));
   if (rc != LLSR_OK) return rc;
   const int P = a.P;
   if (h->profiling) HIP_OK(h, hipEventRecord(m.p1, s));
@@ -882,6 +910,7 @@ static int32_t s2m_batch(llsr_handle* h, const llsr_s2m_batch* b, hipStream_t s,
   if (h->profiling) HIP_OK(h, hipEventRecord(m.p2, s));
   k_s2m_finish<<<(P + 63) / 64, 64, 0, s>>>(a);
   HIP_OK(h, hipGetLastError());
+  HIP_OK(h, hipEventRecord(h->mo_done, s));
   if (h->profiling) {
     float g = 0.f, it = 0.f;
     HIP_OK(h, hipEventSynchronize(m.p2));
@@ -912,8 +941,10 @@ extern "C" int32_t llsr_scan2map_shard_begin(llsr_handle* h, const llsr_s2m_batc
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
   auto& m = h->mo;
   m.sh_live = false;
-  m.last = s;
+  if (h->mo_rec) HIP_OK(h, hipStreamWaitEvent(s, h->mo_done, 0));
   int32_t rc = s2m_prepare(h, b, s, m.sh);
+  h->mo_rec = true;
+  HIP_OK(h, hipEventRecord(h->mo_done, s));
   if (rc != LLSR_OK) return rc;
   m.sh_live = true;
   return LLSR_OK;
@@ -931,11 +962,13 @@ extern "C" int32_t llsr_scan2map_shard_partial(llsr_handle* h, int32_t rank, int
   a.rank = rank;
   a.world = world;
   a.ne = reinterpret_cast<long long*>(d_ne);
+  HIP_OK(h, hipStreamWaitEvent(s, h->mo_done, 0));
   HIP_OK(h, hipMemsetAsync(d_ne, 0, sizeof(int64_t) * LLSR_NE_WORDS * (size_t)a.P, s));
   const int bs = m.blocks - m.blocks_c;
   const int nb = (m.blocks_c + world - 1) / world + (bs + world - 1) / world;
   if (nb > 0) k_s2m_iter_fx<<<8 * ((a.P + 7) / 8) * nb, 256, 0, s>>>(a, nb);  // XCD-aware (llsr_mo.hip)
   HIP_OK(h, hipGetLastError());
+  HIP_OK(h, hipEventRecord(h->mo_done, s));
   return LLSR_OK;
 }
 
@@ -948,8 +981,10 @@ extern "C" int32_t llsr_scan2map_shard_step(llsr_handle* h, const int64_t* d_ne,
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
   S2MArgs a = m.sh;
   a.ne = const_cast<long long*>(reinterpret_cast<const long long*>(d_ne));
+  HIP_OK(h, hipStreamWaitEvent(s, h->mo_done, 0));
   k_s2m_solve_fx<<<(a.P + 63) / 64, 64, 0, s>>>(a);
   HIP_OK(h, hipGetLastError());
+  HIP_OK(h, hipEventRecord(h->mo_done, s));
   if (n_active) {
     HIP_OK(h, hipMemcpyAsync(m.host_flags, a.n_active, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_OK(h, hipStreamSynchronize(s));
@@ -967,8 +1002,10 @@ extern "C" int32_t llsr_scan2map_shard_end(llsr_handle* h, void* hip_stream) {
   if (!m.sh_live) return fail(h, LLSR_EINVAL, "llsr_scan2map_shard_begin not called");
   HIP_OK(h, hipSetDevice(h->device));
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+  HIP_OK(h, hipStreamWaitEvent(s, h->mo_done, 0));
   k_s2m_finish<<<(m.sh.P + 63) / 64, 64, 0, s>>>(m.sh);
   HIP_OK(h, hipGetLastError());
+  HIP_OK(h, hipEventRecord(h->mo_done, s));
   m.sh_live = false;
   return LLSR_OK;
 }
@@ -1143,6 +1180,7 @@ extern "C" int32_t llsr_scan2scan_batch(llsr_handle* h, const llsr_s2s_batch* b,
   if (h->profiling && !m.p0 &&
       (hipEventCreate(&m.p0) != hipSuccess || hipEventCreate(&m.p1) != hipSuccess || hipEventCreate(&m.p2) != hipSuccess))
     return fail(h, LLSR_ENODEV, "events");
+  if (h->s2s_rec) HIP_OK(h, hipStreamWaitEvent(s, h->s2s_done, 0));  // shared buffers: after the last batch
   if (h->profiling) HIP_OK(h, hipEventRecord(m.p0, s));
   grid_build(a.grids, s);
   if (h->profiling) HIP_OK(h, hipEventRecord(m.p1, s));
@@ -1153,7 +1191,8 @@ extern "C" int32_t llsr_scan2scan_batch(llsr_handle* h, const llsr_s2s_batch* b,
   else
     k_s2s_lm<2048, 2048><<<P, kS2SThreads, 0, s>>>(a);
   HIP_OK(h, hipGetLastError());
-  m.last = s;
+  HIP_OK(h, hipEventRecord(h->s2s_done, s));
+  h->s2s_rec = true;
   if (h->profiling) {
     float g = 0.f, lm = 0.f;
     HIP_OK(h, hipEventRecord(m.p2, s));
@@ -1178,7 +1217,8 @@ extern "C" int32_t llsr_scan2scan_check(llsr_handle* h) {
   auto& m = h->s2s;
   if (!m.pool) return LLSR_OK;
   HIP_OK(h, hipSetDevice(h->device));
-  hipStream_t s = m.last ? m.last : h->stream;
+  hipStream_t s = h->stream;  // the handle's stream, after the last scan-to-scan batch
+  if (h->s2s_rec) HIP_OK(h, hipStreamWaitEvent(s, h->s2s_done, 0));
   HIP_OK(h, hipMemcpyAsync(m.host_flag, m.a.error, sizeof(int), hipMemcpyDeviceToHost, s));
   HIP_OK(h, hipStreamSynchronize(s));
   if (*m.host_flag) {
@@ -1395,6 +1435,7 @@ extern "C" int32_t llsr_odometry_batch(llsr_handle* h, const float* d_xyzi, cons
   k_odo_finish<<<B, 256, 0, s>>>(a);
   HIP_OK(h, hipGetLastError());
   HIP_OK(h, hipEventRecord(h->last_done, s));
+  h->last_rec = true;
   o.cur = nxt;
   h->last_stream = s;
   return LLSR_OK;
@@ -1484,86 +1525,79 @@ extern "C" int32_t llsr_mapping_reset(llsr_handle* h) {
   return LLSR_OK;
 }
 
+// Release every mapping-chain allocation (slot stores, engine, state); mp.live becomes false.
+static void mapping_free(llsr_handle* h) {
+  auto& mp = h->mp;
+  for (auto& sl : mp.slot)
+    if (sl.map) llsr_map_destroy(sl.map);
+  mp.slot.clear();
+  if (mp.vg) llsr_map_destroy(mp.vg);
+  mp.vg = nullptr;
+  if (mp.small) (void)hipFree(mp.small);
+  if (mp.hsmall) (void)hipHostFree(mp.hsmall);
+  mp.small = mp.hsmall = nullptr;
+  mp.live = false;
+}
+
 extern "C" int32_t llsr_mapping_init(llsr_handle* h, int32_t mo_mode, const llsr_map_config* map_cfg) {
   if (!h) return LLSR_EINVAL;
   if (mo_mode != LLSR_MODE_FAITHFUL && mo_mode != LLSR_MODE_LM_APPLIED) return fail(h, LLSR_EINVAL, "mo_mode");
   if (h->cfg.mode != LLSR_MODE_LM_APPLIED)
     return fail(h, LLSR_ENOSYS, "the mapping chain runs the odometry, which needs LLSR_MODE_LM_APPLIED");
+  llsr_map_config mcfg;
+  if (map_cfg) mcfg = *map_cfg;  // NULL: the YAML block of the handle's lidar
+  else llsr_map_config_lidar(&mcfg, h->dc.H == 64 ? LLSR_LIDAR_HDL64E : LLSR_LIDAR_VLP16);
+  if (mcfg.enable_loop_closure && mcfg.surrounding_keyframe_search_num < 1)
+    return fail(h, LLSR_EINVAL, "surrounding_keyframe_search_num must be >= 1 with loop closure");
   HIP_OK(h, hipSetDevice(h->device));
   int32_t rc = odo_alloc(h);
   if (rc != LLSR_OK) return rc;
   auto& mp = h->mp;
+  HIP_OK(h, sync_handle_streams(h));
+  mapping_free(h);  // a repeated init rebuilds everything with the new map config
   mp.mode = mo_mode;
-  if (map_cfg) mp.mcfg = *map_cfg;
-  else llsr_map_config_default(&mp.mcfg);
-  if (!mp.live) {
-    const int B = h->max_batch;
-    mp.slot.resize(B);
-    for (auto& sl : mp.slot)
-      if (!(sl.map = llsr_map_create(&mp.mcfg, h->device))) return fail(h, LLSR_ENOMEM, "llsr_map_create");
-    if (!(mp.vg = llsr_map_create(&mp.mcfg, h->device))) return fail(h, LLSR_ENOMEM, "llsr_map_create");
-    const size_t nb = (size_t)B + 1;
-    const size_t dbytes = sizeof(float) * 6 * B + sizeof(llsr_lm_report) * B + sizeof(int) * B +
-                          sizeof(float) * 36 * B + sizeof(int64_t) * 5 * nb + 8 * 256;
-    const size_t hbytes = sizeof(float) * 6 * B + sizeof(llsr_lm_report) * B + sizeof(int64_t) * 5 * nb +
-                          sizeof(int) * B + sizeof(float) * 6 * B + 8 * 256;
-    if (hipMalloc(&mp.small, dbytes) != hipSuccess) { mp.small = nullptr; return fail(h, LLSR_ENOMEM, "mapping state"); }
-    if (hipHostMalloc(&mp.hsmall, hbytes) != hipSuccess) { mp.hsmall = nullptr; return fail(h, LLSR_ENOMEM, "mapping staging"); }
-    char* q = (char*)mp.small;
-    mp.d_pose = carve<float>(q, 6 * (size_t)B);
-    mp.d_rep = carve<llsr_lm_report>(q, B);
-    mp.d_deg = carve<int>(q, B);
-    mp.d_matP = carve<float>(q, 36 * (size_t)B);
-    mp.d_off = carve<int64_t>(q, 5 * nb);
-    q = (char*)mp.hsmall;
-    mp.h_pose = carve<float>(q, 6 * (size_t)B);
-    mp.h_rep = carve<llsr_lm_report>(q, B);
-    mp.h_off = carve<int64_t>(q, 5 * nb);
-    mp.h_frames = carve<int>(q, B);
-    mp.h_tsum = carve<float>(q, 6 * (size_t)B);
-    mp.live = true;
-  } else {
-    for (auto& sl : mp.slot) {  // a new map config: rebuild the stores
-      llsr_map_destroy(sl.map);
-      if (!(sl.map = llsr_map_create(&mp.mcfg, h->device))) return fail(h, LLSR_ENOMEM, "llsr_map_create");
-    }
-    llsr_map_destroy(mp.vg);
-    if (!(mp.vg = llsr_map_create(&mp.mcfg, h->device))) return fail(h, LLSR_ENOMEM, "llsr_map_create");
-  }
+  mp.mcfg = mcfg;
+  const int B = h->max_batch;
+  mp.slot.resize(B);
+  for (auto& sl : mp.slot)
+    if (!(sl.map = llsr_map_create(&mp.mcfg, h->device))) { mapping_free(h); return fail(h, LLSR_ENOMEM, "llsr_map_create"); }
+  if (!(mp.vg = llsr_map_create(&mp.mcfg, h->device))) { mapping_free(h); return fail(h, LLSR_ENOMEM, "llsr_map_create"); }
+  const size_t nb = (size_t)B + 1;
+  const size_t dbytes = sizeof(float) * 6 * B + sizeof(llsr_lm_report) * B + 2 * sizeof(int) * B +
+                        2 * sizeof(float) * 36 * B + sizeof(int64_t) * 5 * nb + 10 * 256;
+  const size_t hbytes = sizeof(float) * 6 * B + sizeof(llsr_lm_report) * B + sizeof(int64_t) * 5 * nb +
+                        sizeof(int) * B + sizeof(float) * 6 * B + 8 * 256;
+  if (hipMalloc(&mp.small, dbytes) != hipSuccess) { mp.small = nullptr; mapping_free(h); return fail(h, LLSR_ENOMEM, "mapping state"); }
+  if (hipHostMalloc(&mp.hsmall, hbytes) != hipSuccess) { mp.hsmall = nullptr; mapping_free(h); return fail(h, LLSR_ENOMEM, "mapping staging"); }
+  char* q = (char*)mp.small;
+  mp.d_pose = carve<float>(q, 6 * (size_t)B);
+  mp.d_rep = carve<llsr_lm_report>(q, B);
+  mp.d_deg = carve<int>(q, B);
+  mp.d_matP = carve<float>(q, 36 * (size_t)B);
+  mp.d_off = carve<int64_t>(q, 5 * nb);
+  mp.d_deg_bak = carve<int>(q, B);
+  mp.d_matP_bak = carve<float>(q, 36 * (size_t)B);
+  q = (char*)mp.hsmall;
+  mp.h_pose = carve<float>(q, 6 * (size_t)B);
+  mp.h_rep = carve<llsr_lm_report>(q, B);
+  mp.h_off = carve<int64_t>(q, 5 * nb);
+  mp.h_frames = carve<int>(q, B);
+  mp.h_tsum = carve<float>(q, 6 * (size_t)B);
+  mp.live = true;
   return llsr_mapping_reset(h);
 }
 
-extern "C" int32_t llsr_mapping_batch(llsr_handle* h, const float* d_xyzi, const int64_t* d_offsets, int32_t B,
-                                      void* hip_stream) {
-  if (!h) return LLSR_EINVAL;
+// MapOptimization::run for the slots in `step` (their pose glue already applied by the caller).
+static int32_t mapping_mo(llsr_handle* h, int32_t B, hipStream_t s, const std::vector<char>& step) {
   auto& mp = h->mp;
-  if (!mp.live) return fail(h, LLSR_EINVAL, "llsr_mapping_init not called");
-  if (B < 1 || B > h->max_batch) return fail(h, LLSR_ERANGE, "batch size outside [1, max_batch]");
-  HIP_OK(h, hipSetDevice(h->device));
-  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
-  int32_t rc = llsr_odometry_batch(h, d_xyzi, d_offsets, B, s);
-  if (rc != LLSR_OK) return rc;
   auto& o = h->odo;
+  int32_t rc = LLSR_OK;
   const int NB = o.B, nb = NB + 1;
   // this frame's AssociationOut clouds (the batch flipped o.cur to them)
   const int64_t* hs = o.h_off;                     // cloud_corner_scan (sharp, TransformToEnd)
   const int64_t* hf = o.h_off + nb;                // cloud_surf_scan (flat + shadow, TransformToEnd)
   const int64_t* hlc = o.h_off + (2 + o.cur) * nb; // cloud_corner_last
   const int64_t* hls = o.h_off + (4 + o.cur) * nb; // cloud_surf_last (+ shadow)
-  HIP_OK(h, hipMemcpyAsync(mp.h_frames, o.frames, sizeof(int) * B, hipMemcpyDeviceToHost, s));
-  HIP_OK(h, hipMemcpyAsync(mp.h_tsum, o.tsum, sizeof(float) * 6 * B, hipMemcpyDeviceToHost, s));
-  HIP_OK(h, hipStreamSynchronize(s));
-  rc = llsr_scan2scan_check(h);
-  if (rc != LLSR_OK) return rc;
-  std::vector<char> step(NB, 0);  // slots that receive an AssociationOut this call
-  for (int b = 0; b < B; ++b) {
-    auto& sl = mp.slot[b];
-    sl.frames = mp.h_frames[b];
-    step[b] = sl.frames >= 2;
-    if (!step[b]) continue;
-    llsr_mapping::odometry_roundtrip(mp.h_tsum + 6 * b, sl.pose.transformSum);  // OdometryToTransform
-    llsr_mapping::transform_associate_to_map(sl.pose);
-  }
   // adjustOutlierCloud of this frame's IP outliers (FA:2720)
   int64_t* hol = mp.h_off + 4 * (size_t)nb;
   hol[0] = 0;
@@ -1725,7 +1759,85 @@ extern "C" int32_t llsr_mapping_batch(llsr_handle* h, const float* d_xyzi, const
     sl.keyposes.insert(sl.keyposes.end(), kp, kp + 6);
     sl.mo_frames += 1;
   }
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_mapping_batch(llsr_handle* h, const float* d_xyzi, const int64_t* d_offsets, int32_t B,
+                                      void* hip_stream) {
+  if (!h) return LLSR_EINVAL;
+  auto& mp = h->mp;
+  if (!mp.live) return fail(h, LLSR_EINVAL, "llsr_mapping_init not called");
+  if (B < 1 || B > h->max_batch) return fail(h, LLSR_ERANGE, "batch size outside [1, max_batch]");
+  HIP_OK(h, hipSetDevice(h->device));
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+  int32_t rc = llsr_odometry_batch(h, d_xyzi, d_offsets, B, s);
+  if (rc != LLSR_OK) return rc;
+  auto& o = h->odo;
+  HIP_OK(h, hipMemcpyAsync(mp.h_frames, o.frames, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+  HIP_OK(h, hipMemcpyAsync(mp.h_tsum, o.tsum, sizeof(float) * 6 * B, hipMemcpyDeviceToHost, s));
+  HIP_OK(h, hipStreamSynchronize(s));
+  rc = llsr_scan2scan_check(h);
+  if (rc != LLSR_OK) return rc;
+  // MapOptimization's members of the B slots before this frame: an error below restores them
+  struct Snap {
+    llsr_handle::MapSlot slot;  // (keyposes: only its length is restored)
+    size_t n_keyposes;
+    int n_keyframes;
+    llsr_mapping::MapSel sel;
+  };
+  std::vector<Snap> snap(B);
+  for (int b = 0; b < B; ++b) {
+    const auto& sl = mp.slot[b];
+    snap[b].slot.pose = sl.pose;
+    std::memcpy(snap[b].slot.robot, sl.robot, sizeof sl.robot);
+    snap[b].slot.mo_frames = sl.mo_frames; snap[b].slot.lm_ran = sl.lm_ran;
+    snap[b].slot.n_cq = sl.n_cq; snap[b].slot.n_sq = sl.n_sq; snap[b].slot.cycle = sl.cycle;
+    snap[b].slot.lm = sl.lm; snap[b].slot.mrep = sl.mrep;
+    snap[b].n_keyposes = sl.keyposes.size();
+    snap[b].n_keyframes = llsr_map_num_keyframes(sl.map);
+    snap[b].sel = llsr_mapping::map_selection(sl.map);
+  }
+  std::vector<char> step(o.B, 0);  // slots that receive an AssociationOut this call
+  for (int b = 0; b < B; ++b) {
+    auto& sl = mp.slot[b];
+    sl.frames = mp.h_frames[b];
+    // FA:2781-2784: the first scan sends nothing; FA:2818-2821: every mapping_frequency_divider-th
+    // frame after it sends an AssociationOut
+    if (sl.frames >= 2 && ++sl.cycle == h->cfg.mapping_frequency_divider) {
+      sl.cycle = 0;
+      step[b] = 1;
+    }
+    if (!step[b]) continue;
+    llsr_mapping::odometry_roundtrip(mp.h_tsum + 6 * b, sl.pose.transformSum);  // OdometryToTransform
+    llsr_mapping::transform_associate_to_map(sl.pose);
+  }
+  bool any = false;
+  for (char c : step) any |= c != 0;
+  if (any) {  // the LM members (isDegenerate, matP) before this frame, restored if it fails
+    HIP_OK(h, hipMemcpyAsync(mp.d_deg_bak, mp.d_deg, sizeof(int) * o.B, hipMemcpyDeviceToDevice, s));
+    HIP_OK(h, hipMemcpyAsync(mp.d_matP_bak, mp.d_matP, sizeof(float) * 36 * o.B, hipMemcpyDeviceToDevice, s));
+  }
+  rc = any ? mapping_mo(h, B, s, step) : LLSR_OK;
+  if (rc != LLSR_OK) {
+    const std::string msg = h->err;
+    (void)hipStreamSynchronize(s);
+    for (int b = 0; b < B; ++b) {
+      auto& sl = mp.slot[b];
+      const auto& sn = snap[b].slot;
+      sl.pose = sn.pose;
+      std::memcpy(sl.robot, sn.robot, sizeof sl.robot);
+      sl.mo_frames = sn.mo_frames; sl.lm_ran = sn.lm_ran; sl.n_cq = sn.n_cq; sl.n_sq = sn.n_sq;
+      sl.cycle = sn.cycle; sl.lm = sn.lm; sl.mrep = sn.mrep;
+      sl.keyposes.resize(snap[b].n_keyposes);
+      llsr_mapping::truncate_keyframes(sl.map, snap[b].n_keyframes);
+      llsr_mapping::set_map_selection(sl.map, snap[b].sel);
+    }
+    (void)hipMemcpy(mp.d_deg, mp.d_deg_bak, sizeof(int) * o.B, hipMemcpyDeviceToDevice);
+    (void)hipMemcpy(mp.d_matP, mp.d_matP_bak, sizeof(float) * 36 * o.B, hipMemcpyDeviceToDevice);
+    return fail(h, rc, msg);
+  }
   HIP_OK(h, hipEventRecord(h->last_done, s));
+  h->last_rec = true;
   h->last_stream = s;
   return LLSR_OK;
 }

@@ -1,7 +1,8 @@
 // llsr_map.hip — MapOptimization's local map on the device: the keyframe store
-// (saveKeyFramesAndFactor, mapOptmization.cpp:1686-1752), extractSurroundingKeyFrames with loop
-// closure disabled (MO:1151-1231), downsampleCurrentScan (MO:1234-1267), and the segmented
-// VoxelGrid they all run on.
+// (saveKeyFramesAndFactor, mapOptmization.cpp:1686-1752), extractSurroundingKeyFrames in both of
+// its branches (the loop-closure queue of recent keyframes MO:1099-1151, the key-pose radius search
+// MO:1152-1223) with the local-map VoxelGrids (MO:1224-1231), downsampleCurrentScan
+// (MO:1234-1267), and the segmented VoxelGrid they all run on.
 //
 // VoxelGrid (pcl::VoxelGrid<PointXYZI>::applyFilter, PCL 1.10, downsample_all_data) of S clouds at
 // once, every step a device pass over HBM:
@@ -10,9 +11,10 @@
 //   k_vg_params    per cloud: the (max - min) * inv + 1 product check (over INT32_MAX: PCL returns
 //                  the input unchanged — here every point becomes its own voxel, idx = its index,
 //                  which reproduces that bit for bit), min_b = floor(min * inv), the div products;
-//   k_vg_keys      64-bit key (cloud << 32 | idx), value = index in the cloud;
-//   radix sort     hipcub::DeviceRadixSort (rocPRIM onesweep; stable, so a voxel's points stay in
-//                  input order); bits = 32 + ceil(log2 S);
+//   k_vg_keys      PCL's index_vector entries (voxel idx << 32 | point index), in input order;
+//   k_is_level /   libstdc++'s std::sort of every cloud's index_vector by voxel idx, exactly
+//   k_is_leaf      (equal ids in introsort's order, which is the order PCL sums a voxel in);
+//   k_vg_unpack    (cloud << 32 | voxel idx) keys + point indices for the passes below;
 //   k_vg_heads     run heads, exclusive scan -> output slot of every voxel (ascending idx per
 //                  cloud, the PCL output order; the per-cloud output offsets fall out of the scan);
 //   k_vg_centroid  one lane per voxel sums its run in float (x, y, z, intensity) and divides by
@@ -390,7 +392,10 @@ struct llsr_map {
   size_t store_cap = 0, store_used = 0;
   struct Kf { float pose[6]; long long off[3]; int n[3]; };  // corner, surf, outlier
   std::vector<Kf> kf;
-  std::vector<int> existing;   // surroundingExistingKeyPosesID
+  // the local map's keyframe list: surroundingExistingKeyPosesID (radius branch) or the indices of
+  // recent{Corner,Surf,Outlier}CloudKeyFrames, oldest first (loop-closure branch); with the
+  // latestFrameID of MO:1126-1134 (0 from the constructor, MO:301)
+  llsr_mapping::MapSel sel;
   // VoxelGrid scratch
   unsigned long long *key = nullptr, *key2 = nullptr;
   int *val = nullptr, *val2 = nullptr, *flag = nullptr, *rank = nullptr;
@@ -603,12 +608,34 @@ extern "C" int32_t llsr_map_config_default(llsr_map_config* c) {
   c->corner_leaf = 0.2f;
   c->surf_leaf = 0.4f;
   c->outlier_leaf = 0.4f;
+  c->enable_loop_closure = 0;               // CFG:23
+  c->surrounding_keyframe_search_num = 50;  // CFG:27
   return LLSR_OK;
 }
+
+extern "C" int32_t llsr_map_config_lidar(llsr_map_config* c, int32_t lidar) {
+  if (!c) return LLSR_EINVAL;
+  if (lidar != LLSR_LIDAR_VLP16 && lidar != LLSR_LIDAR_HDL64E) return LLSR_EINVAL;
+  llsr_map_config_default(c);  // radius 50 and search num 50 in both blocks (CFG:26-27, 162-163)
+  c->enable_loop_closure = lidar == LLSR_LIDAR_HDL64E ? 1 : 0;  // CFG:159
+  return LLSR_OK;
+}
+
+namespace llsr_mapping {
+MapSel map_selection(const llsr_map* m) { return m->sel; }
+void set_map_selection(llsr_map* m, const MapSel& s) { m->sel = s; }
+void truncate_keyframes(llsr_map* m, int keep) {
+  if (keep < 0 || keep >= (int)m->kf.size()) return;
+  m->store_used = (size_t)m->kf[keep].off[0];
+  m->kf.resize(keep);
+}
+}  // namespace llsr_mapping
 
 extern "C" llsr_map* llsr_map_create(const llsr_map_config* cfg, int32_t dev) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || dev < 0 || dev >= n) return nullptr;
+  // a loop-closure queue of fewer than one keyframe would pop from an empty deque (MO:1130)
+  if (cfg && cfg->enable_loop_closure && cfg->surrounding_keyframe_search_num < 1) return nullptr;
   llsr_map* m = new (std::nothrow) llsr_map();
   if (!m) return nullptr;
   if (cfg) m->cfg = *cfg;
@@ -641,7 +668,7 @@ extern "C" const char* llsr_map_last_error(const llsr_map* m) { return m ? m->er
 extern "C" int32_t llsr_map_reset(llsr_map* m) {
   if (!m) return LLSR_EINVAL;
   m->kf.clear();
-  m->existing.clear();
+  m->sel = llsr_mapping::MapSel{};
   m->store_used = 0;
   return LLSR_OK;
 }
@@ -745,13 +772,14 @@ int32_t llsr_mapping::extract_multi(llsr_map* eng, llsr_map* const* maps, int n,
   if (!m || n < 1) return LLSR_EINVAL;
   const auto t0 = std::chrono::steady_clock::now();
   // radiusSearch (MO:1157-1159): d^2 = ((0 + dx^2) + dy^2) + dz^2 < float(r^2), over K poses
+  // (radius-branch maps only; a loop-closure map selects no poses here)
   std::vector<float4> sel;
   std::vector<long long> sel_off(n + 1, 0);
   for (int i = 0; i < n; ++i) {
     llsr_map* mi = maps[i];
     std::memset(&reps[i], 0, sizeof reps[i]);
     const float r2 = (float)((double)mi->cfg.surrounding_radius * (double)mi->cfg.surrounding_radius);
-    const int K = (int)mi->kf.size();
+    const int K = mi->cfg.enable_loop_closure ? 0 : (int)mi->kf.size();
     const size_t s0 = sel.size();
     for (int k = 0; k < K; ++k) {
       const float* p = mi->kf[k].pose;
@@ -790,27 +818,49 @@ int32_t llsr_mapping::extract_multi(llsr_map* eng, llsr_map* const* maps, int n,
   std::vector<long long> rc_off(n + 1, 0), rs_off(n + 1, 0);
   for (int i = 0; i < n; ++i) {
     llsr_map* mi = maps[i];
-    reps[i].n_poses_ds = (int32_t)ds_ids[i].size();
-    std::vector<int> kept;
-    for (int id : mi->existing)
-      for (int d : ds_ids[i])
-        if (d == id) { kept.push_back(id); break; }
-    mi->existing.swap(kept);
+    std::vector<int>& ids = mi->sel.ids;
     const int K = (int)mi->kf.size();
-    for (int d : ds_ids[i]) {
-      bool found = false;
-      for (int id : mi->existing)
-        if (id == d) { found = true; break; }
-      if (!found) {
-        if (d < 0 || d >= K) return mfail(m, LLSR_ERANGE, "extract: key pose index out of range");
-        mi->existing.push_back(d);
-        ++reps[i].n_transformed;
+    if (mi->cfg.enable_loop_closure) {
+      // MO:1099-1145. cloudKeyPoses3D[i].intensity == i (MO:1695-1697), so thisKeyInd == i.
+      const int N = mi->cfg.surrounding_keyframe_search_num;
+      if ((int)ids.size() < N) {
+        // queue not full: rebuild it from the newest keyframe backwards, push_front until N
+        std::vector<int> q;
+        for (int k = K - 1; k >= 0; --k) {
+          q.push_back(k);
+          if ((int)q.size() >= N) break;
+        }
+        ids.assign(q.rbegin(), q.rend());
+        reps[i].n_transformed = (int32_t)ids.size();
+      } else if (mi->sel.latest_frame_id != K - 1) {
+        // full: pop the oldest, push the newest (only when a keyframe was added since)
+        ids.erase(ids.begin());
+        mi->sel.latest_frame_id = K - 1;
+        ids.push_back(K - 1);
+        reps[i].n_transformed = 1;
+      }
+    } else {
+      reps[i].n_poses_ds = (int32_t)ds_ids[i].size();
+      std::vector<int> kept;
+      for (int id : ids)
+        for (int d : ds_ids[i])
+          if (d == id) { kept.push_back(id); break; }
+      ids.swap(kept);
+      for (int d : ds_ids[i]) {
+        bool found = false;
+        for (int id : ids)
+          if (id == d) { found = true; break; }
+        if (!found) {
+          if (d < 0 || d >= K) return mfail(m, LLSR_ERANGE, "extract: key pose index out of range");
+          ids.push_back(d);
+          ++reps[i].n_transformed;
+        }
       }
     }
-    reps[i].n_keyframes = (int32_t)mi->existing.size();
+    reps[i].n_keyframes = (int32_t)ids.size();
     long long nc = 0, ns = 0;
-    for (int id : mi->existing) nc += mi->kf[id].n[0];
-    for (int id : mi->existing) ns += mi->kf[id].n[1] + mi->kf[id].n[2];
+    for (int id : ids) nc += mi->kf[id].n[0];
+    for (int id : ids) ns += mi->kf[id].n[1] + mi->kf[id].n[2];
     reps[i].n_corner_map = nc;
     reps[i].n_surf_map = ns;
     rc_off[i + 1] = rc_off[i] + nc;
@@ -831,7 +881,7 @@ int32_t llsr_mapping::extract_multi(llsr_map* eng, llsr_map* const* maps, int n,
       }
       dst += k.n[a];
     };
-    for (int id : mi->existing) {
+    for (int id : mi->sel.ids) {
       add(mi->kf[id], 0, dc);
       add(mi->kf[id], 1, dsf);
       add(mi->kf[id], 2, dsf);
@@ -899,7 +949,7 @@ extern "C" int32_t llsr_map_extract(llsr_map* m, const float pos[3], float* d_co
 
 extern "C" int32_t llsr_map_keyframe_ids(const llsr_map* m, int32_t* out, int32_t cap) {
   if (!m) return LLSR_EINVAL;
-  const int n = (int)m->existing.size();
-  for (int k = 0; k < n && k < cap; ++k) out[k] = m->existing[k];
+  const int n = (int)m->sel.ids.size();
+  for (int k = 0; k < n && k < cap; ++k) out[k] = m->sel.ids[k];
   return n;
 }

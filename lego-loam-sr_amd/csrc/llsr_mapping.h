@@ -12,10 +12,25 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <vector>
 
 #include "../../include/llsr.h"
 
 namespace llsr_mapping {
+
+// Which keyframes make up a llsr_map's local map between extractSurroundingKeyFrames calls
+// (MO:1096-1232): the radius branch's surroundingExistingKeyPosesID, or the loop-closure branch's
+// queue of recent keyframes (their indices, oldest first) and latestFrameID. The queue holds
+// indices rather than the transformed clouds of MO:1115-1143: a key pose never changes after
+// saveKeyFramesAndFactor stores it (correctPoses acts only after a closed loop, MO:1758, and the
+// loop-closure thread is commented out, MO:174), so transforming at extract time gives the same
+// points.
+struct MapSel {
+  std::vector<int> ids;
+  int latest_frame_id = 0;
+};
+MapSel map_selection(const llsr_map* m);
+void set_map_selection(llsr_map* m, const MapSel& s);
 
 // Segmented VoxelGrid (llsr_map.hip's engine) over S clouds src[k] (device, n[k] points, leaf[k]):
 // results packed into `out` (capacity sum n) in segment order, offsets out_off[S+1] on the host.
@@ -28,6 +43,8 @@ int32_t voxel_multi(llsr_map* m, const float4* const* src, const long long* n, c
 // empty maps (the caller skips the call for it, MO:1097). Synchronises s.
 int32_t extract_multi(llsr_map* eng, llsr_map* const* maps, int n, const float* pos, llsr_map_report* reps,
                       const float4** out, long long* off_c, long long* off_s, hipStream_t s);
+// Drop keyframes from index `keep` on (a failed frame's keyframe, llsr_mapping_batch rollback).
+void truncate_keyframes(llsr_map* m, int keep);
 
 // tf2::Quaternion::setRPY (tf2/LinearMath/Quaternion.h), double. The reference's GCC -O3 build
 // merges each tf2Cos(a) / tf2Sin(a) pair into one glibc sincos(a) call (GCC's sincos pass), and

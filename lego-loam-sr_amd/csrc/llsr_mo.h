@@ -47,6 +47,8 @@ struct S2MArgs {
   // construction MO:285-286): isDegenerate / matP in at setup and out at finish (mapping chain;
   // null: a fresh optimiser per problem)
   int solve_rows;              // matA rows k_s2m_solve stages in LDS at a time
+  float* blk_spill;            // [P][spill_cap][29] Eigen depth-block sums beyond the 64 kept in LDS
+  int spill_cap;               // depth blocks per problem in blk_spill
   int dbg;                     // diagnostics (LLSR_S2M_DBG): k_s2m_solve stops after stage dbg (0: never)
   const int* deg_in; const float* matP_in;
   int* deg_out; float* matP_out;

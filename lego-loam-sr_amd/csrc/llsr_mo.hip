@@ -17,7 +17,7 @@
 // (MO:1279 / MO:1386), so a 1 m grid over the 27 neighbouring cells finds them exactly. Each
 // thread keeps the five smallest (d^2, map index) pairs: identical to inserting candidates in
 // index order with strict '<' (the restatement in oracle/oracle_mo.cpp), independent of the
-// order the cells are visited. The per-correspondence arithmetic repeats the reference's float
+// order the cells are visited; cells that cannot hold a better pair are not probed (knn5). The per-correspondence arithmetic repeats the reference's float
 // and double operations one for one (-ffp-contract=off, glibc sinf/cosf ports, Eigen 3.3.7
 // restatements in llsr_eigen.h), so correspondences and coefficients are bit-identical to the
 // oracle, and the normal equations are summed in the reference's Eigen order: the float path is
@@ -35,6 +35,13 @@
 #include "llsr_lm.h"
 #include "llsr_mo.h"
 
+// LLSR_S2M_DBG stage stops of k_s2m_solve exist only in the diagnostic build (make prof)
+#ifdef LLSR_S2S_PROF
+#define S2M_DBG(a) ((a).dbg)
+#else
+#define S2M_DBG(a) 0
+#endif
+
 namespace llsr {
 
 using llsr_libm::bitsf;
@@ -51,17 +58,46 @@ struct Best5 {
   int i[5];
 };
 
+// The 27 neighbour cells in the order kNN-5 visits them: the query's own cell, the 6 face
+// neighbours, the 12 edge and the 8 corner neighbours (packed as (dx+1) | (dy+1) << 2 | (dz+1) << 4),
+// so the 5th-best distance tightens early and prunes the farther cells.
+__constant__ unsigned char kCellOrder[27] = {
+    21,                                          // (0, 0, 0)
+    20, 22, 17, 25, 5, 37,                       // faces
+    16, 18, 24, 26, 4, 6, 36, 38, 1, 9, 33, 41,  // edges
+    0, 2, 8, 10, 32, 34, 40, 42};                // corners
+
 // kNN-5 with d^2 < 1.0 around q in one map; returns true when five were found.
+// The result is the five smallest (d^2, index) pairs of the cells' points with d^2 < 1.0, in any
+// visiting order. A cell is skipped when no point in it can enter that set: its box lies at squared
+// distance LB from q, every point's float d^2 (three rounded differences, squares and sums) is at
+// least LB (1 - 5 eps) minus the rounding of the box gaps (< 1e-7 absolute), so a cell with
+// LB > lim (1 + 1e-5) + 4e-6 holds only points with d^2 > lim, where lim = 1.0, or the current 5th
+// distance once five are held (a tie at lim would need d^2 == lim). Exact, therefore, and typically
+// 7 of the 27 cells are probed (the center, the faces and a few edges; tests/test_gpu_mo.py).
 __device__ bool knn5(const CellSlot* __restrict__ tab, int log2T, const float4* __restrict__ pts,
                      float qx, float qy, float qz, Best5& b) {
 #pragma unroll
   for (int k = 0; k < 5; ++k) { b.d[k] = INFINITY; b.i[k] = INT_MAX; }
   const int cx = cell_coord(qx), cy = cell_coord(qy), cz = cell_coord(qz);
-  // cells visited one at a time (not unrolled): keeps the kernel at ~71 VGPRs / 7 waves per
-  // SIMD, which beat issuing all 27 probes up front (96+ VGPRs) on MI355X
+  // distances from q to its cell's lower / upper faces per axis (cell_coord's sentinel cell for
+  // NaN / huge coordinates: gaps become NaN / huge, no cell is skipped wrongly since LB > lim fails
+  // for NaN and a huge q finds nothing anyway)
+  const float lx = qx - floorf(qx), ly = qy - floorf(qy), lz = qz - floorf(qz);
+  const float ux = 1.0f - lx, uy = 1.0f - ly, uz = 1.0f - lz;
+  // cells visited one at a time (not unrolled): keeps the kernel's VGPRs low, which beat issuing
+  // all probes up front on MI355X (latency-bound gathers, 8 waves per SIMD)
 #pragma unroll 1
   for (int c = 0; c < 27; ++c) {
-    const int s = grid_find(tab, log2T, cell_key(cx + c / 9 - 1, cy + (c / 3) % 3 - 1, cz + c % 3 - 1));
+    const int o = kCellOrder[c];
+    const int ox = (o & 3) - 1, oy = ((o >> 2) & 3) - 1, oz = (o >> 4) - 1;
+    const float gx = ox < 0 ? lx : (ox > 0 ? ux : 0.0f);
+    const float gy = oy < 0 ? ly : (oy > 0 ? uy : 0.0f);
+    const float gz = oz < 0 ? lz : (oz > 0 ? uz : 0.0f);
+    const float lb = gx * gx + gy * gy + gz * gz;
+    const float lim = b.d[4] < 1.0f ? b.d[4] : 1.0f;
+    if (lb > lim * 1.00001f + 4e-6f) continue;
+    const int s = grid_find(tab, log2T, cell_key(cx + ox, cy + oy, cz + oz));
     if (s < 0) continue;
     const int st = tab[s].start, n = tab[s].count;
     for (int j = st; j < st + n; ++j) {
@@ -362,15 +398,22 @@ __device__ void stage_rows(const S2MArgs& a, int p, const int* pre, int r0, int 
 __device__ void s2m_assemble_solve(const S2MArgs& a, int p, int* pre, int* tmp, float4* lrow) {
   S2MProb& st = a.prob[p];
   block_prefix(a, p, pre, tmp);
-  if (a.dbg == 1) return;
+  if (S2M_DBG(a) == 1) return;
   const int N = pre[a.blocks];
   const int nc = pre[a.blocks_c];
   const int t = threadIdx.x, wv = t >> 6, ln = t & 63;
-  constexpr int kMaxDepthBlocks = 64;
-  __shared__ float s_blk[kMaxDepthBlocks][kRedWords];
+  // per-depth-block sums: the first kLdsDepthBlocks in LDS, the rest (N above ~44k rows) in the
+  // problem's global spill rows (a.blk_spill, sized at reserve for the reserved query counts)
+  constexpr int kLdsDepthBlocks = 64;
+  __shared__ float s_blk[kLdsDepthBlocks][kRedWords];
   __shared__ float s_b[7];
+  float* spill = a.blk_spill + (size_t)p * a.spill_cap * kRedWords;
+  auto blk = [&](int x, int e) -> float& {
+    return x < kLdsDepthBlocks ? s_blk[x][e] : spill[(size_t)(x - kLdsDepthBlocks) * kRedWords + e];
+  };
   const int kc = N >= 50 ? llsr_eigen::gemm_kc(N, 6, 6) : 1;
   const int nkb = N >= 50 ? (N + kc - 1) / kc : 0;
+  const bool fits = nkb <= kLdsDepthBlocks + a.spill_cap;  // always, for clouds within the reserve
   // lane roles: wave 0 lanes < 7 -> matB / CF; waves 1..3 lanes < 29 -> AtA
   int ia = 0, ib = 0;
   bool sw = false;
@@ -391,9 +434,9 @@ __device__ void s2m_assemble_solve(const S2MArgs& a, int p, int* pre, int* tmp, 
       const int d = min(a.solve_rows, N - r0);
       stage_rows(a, p, pre, r0, d, lrow);
       __syncthreads();
-      if (a.dbg == 2) continue;
+      if (S2M_DBG(a) == 2 || !fits) continue;
       const float* lr = reinterpret_cast<const float*>(lrow);
-      if (busy && wv == 0 && a.dbg != 5) {
+      if (busy && wv == 0 && S2M_DBG(a) != 5) {
         // the products do not depend on the running sum: load 8 rows ahead, then add in order;
         // loads unconditional and the CF lane's factor a select, so the loop has no branch
         const int ib2 = ln < 6 ? 6 : 7, ia2 = ln < 6 ? ia : 7;
@@ -418,7 +461,7 @@ __device__ void s2m_assemble_solve(const S2MArgs& a, int p, int* pre, int* tmp, 
           const float x = lr[8 * q + ia2], y = lr[8 * q + ib2];
           c = c + x * (mul ? y : 1.0f);
         }
-      } else if (wv > 0 && a.dbg != 4 && d == N) {
+      } else if (wv > 0 && S2M_DBG(a) != 4 && d == N) {
         // every row is in LDS: each depth block runs on 53 lanes of one wave without selects —
         // lanes 0..20 the upper-triangle entries (c = c + a_i a_j over the block), lanes 21..52 the
         // 8 swapped entries x 4 accumulators (lane u sums rows q = u mod 4 below endk4), merged as
@@ -451,17 +494,17 @@ __device__ void s2m_assemble_solve(const S2MArgs& a, int p, int* pre, int* tmp, 
           const float a0 = __shfl(acc, base & 63), a1 = __shfl(acc, (base + 1) & 63);
           const float a2 = __shfl(acc, (base + 2) & 63), a3 = __shfl(acc, (base + 3) & 63);
           if (ln < 21) {
-            if (x < kMaxDepthBlocks) s_blk[x][ln] = acc;
+            blk(x, ln) = acc;
           } else if (ln < 53 && u4 == 0) {
             float cc = (a0 + a1) + (a2 + a3);
             for (int qq = endk4; qq < db; ++qq) {
               const float* row = lr + 8 * (k2 + qq);
               cc = row[fb] * row[fa] + cc;
             }
-            if (x < kMaxDepthBlocks) s_blk[x][21 + e8] = cc;
+            blk(x, 21 + e8) = cc;
           }
         }
-      } else if (busy && wv > 0 && a.dbg != 4) {
+      } else if (busy && wv > 0 && S2M_DBG(a) != 4) {
         // the rows stream in chunks: the depth-block segments of this chunk that belong to this wave
         for (int g = r0; g < r0 + d;) {
           const int x = g / kc, k2 = x * kc, db = min(kc, N - k2);
@@ -497,7 +540,7 @@ __device__ void s2m_assemble_solve(const S2MArgs& a, int p, int* pre, int* tmp, 
             }
             if (ge == k2 + db) {  // the depth block is complete
               const float v = (sw && endk4 == db) ? (C0 + C1) + (C2 + C3) : c;
-              if (x < kMaxDepthBlocks) s_blk[x][ln] = v;
+              blk(x, ln) = v;
               c = 0.0f; C0 = 0.0f; C1 = 0.0f; C2 = 0.0f; C3 = 0.0f;
             }
           }
@@ -509,17 +552,17 @@ __device__ void s2m_assemble_solve(const S2MArgs& a, int p, int* pre, int* tmp, 
     if (wv == 0 && ln < 7) s_b[ln] = c;
   }
   __syncthreads();
-  if (t != 0 || (a.dbg >= 2 && a.dbg <= 5)) return;
+  if (t != 0 || (S2M_DBG(a) >= 2 && S2M_DBG(a) <= 5)) return;
   st.iter += 1;
   const int iterCount = st.iter - 1;
   st.nc = nc;
   st.ns = N - nc;
   bool conv = false;
-  if (N >= 50 && nkb <= kMaxDepthBlocks) {  // MO:1453
+  if (N >= 50 && fits) {  // MO:1453
     float wsum[kRedWords];
     for (int e = 0; e < kRedWords; ++e) wsum[e] = 0.0f;
     for (int x = 0; x < nkb; ++x)
-      for (int e = 0; e < kRedWords; ++e) wsum[e] = wsum[e] + 1.0f * s_blk[x][e];
+      for (int e = 0; e < kRedWords; ++e) wsum[e] = wsum[e] + 1.0f * blk(x, e);
     float AtA[36];
     int e = 0;
     for (int r = 0; r < 6; ++r)
@@ -528,7 +571,7 @@ __device__ void s2m_assemble_solve(const S2MArgs& a, int p, int* pre, int* tmp, 
       for (int q = 0; q < 4; ++q, ++e) AtA[r + 6 * q] = wsum[e];
     conv = llsr_lm::lm_update_full(st, AtA, s_b, s_b[6], N, iterCount, a.applied != 0, a.stop_thres);
   } else if (N >= 50) {
-    atomicOr(a.error, 1);  // more depth blocks than kMaxDepthBlocks (> ~21k correspondences)
+    atomicOr(a.error, 4);  // more depth blocks than reserved (not reachable within the reserve)
   }
   if (conv) st.converged = 1;
   if (conv || st.iter >= a.iter_max) {

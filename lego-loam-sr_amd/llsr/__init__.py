@@ -37,7 +37,7 @@ EXPORTS = [
     "llsr_shadow_points", "llsr_scan2scan_reserve", "llsr_scan2scan_batch", "llsr_scan2scan_check",
     "llsr_scan2scan", "llsr_scan2map_shard_begin", "llsr_scan2map_shard_partial",
     "llsr_scan2map_shard_step", "llsr_scan2map_shard_end", "llsr_odometry_batch", "llsr_odometry_fetch",
-    "llsr_odometry_reset", "llsr_map_config_default", "llsr_map_create", "llsr_map_destroy",
+    "llsr_odometry_reset", "llsr_map_config_default", "llsr_map_config_lidar", "llsr_map_create", "llsr_map_destroy",
     "llsr_map_last_error", "llsr_map_reset", "llsr_map_voxel_grid", "llsr_map_downsample_scan",
     "llsr_map_add_keyframe", "llsr_map_num_keyframes", "llsr_map_extract", "llsr_map_keyframe_ids",
     "llsr_decode_pointcloud2", "llsr_kitti_count", "llsr_kitti_read", "llsr_kitti_load",
@@ -101,6 +101,7 @@ def lib():
         L.llsr_odometry_fetch.argtypes = [C.c_void_p, C.c_int32, C.POINTER(_abi.OdomSlot)] + [C.c_void_p] * 4
         L.llsr_odometry_reset.argtypes = [C.c_void_p]
         L.llsr_map_config_default.argtypes = [C.POINTER(_abi.MapConfig)]
+        L.llsr_map_config_lidar.argtypes = [C.POINTER(_abi.MapConfig), C.c_int32]
         L.llsr_map_create.argtypes = [C.POINTER(_abi.MapConfig), C.c_int32]
         L.llsr_map_destroy.argtypes = [C.c_void_p]
         L.llsr_map_last_error.argtypes = [C.c_void_p]
@@ -513,9 +514,16 @@ class ImageProjection:
         }
 
 
-def map_config(**kw) -> _abi.MapConfig:
+def map_config(lidar: str | None = None, **kw) -> _abi.MapConfig:
+    """llsr_map_config_default (lidar None) or the loam_config.yaml block of `lidar`
+    (llsr_map_config_lidar: "hdl64e" enables the loop-closure local map), then the overrides."""
     c = _abi.MapConfig()
-    lib().llsr_map_config_default(C.byref(c))
+    if lidar is None:
+        lib().llsr_map_config_default(C.byref(c))
+    else:
+        code = {"vlp16": _abi.LLSR_LIDAR_VLP16, "hdl64e": _abi.LLSR_LIDAR_HDL64E}[lidar]
+        if lib().llsr_map_config_lidar(C.byref(c), code) != 0:
+            raise LlsrError("llsr_map_config_lidar failed")
     for k, v in kw.items():
         setattr(c, k, v)
     return c

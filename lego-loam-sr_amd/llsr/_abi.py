@@ -224,7 +224,8 @@ class FusionState(C.Structure):
 class MapConfig(C.Structure):
     """llsr_map_config (include/llsr.h): MapOptimization's local-map parameters."""
     _fields_ = [("surrounding_radius", C.c_float), ("keypose_leaf", C.c_float), ("corner_leaf", C.c_float),
-                ("surf_leaf", C.c_float), ("outlier_leaf", C.c_float)]
+                ("surf_leaf", C.c_float), ("outlier_leaf", C.c_float), ("enable_loop_closure", C.c_int32),
+                ("surrounding_keyframe_search_num", C.c_int32)]
 
 
 class MapReport(C.Structure):

@@ -59,18 +59,21 @@ class HipShardEngine:
         self.pipe.scan2map_shard_end(self.stream)
 
 
-def sharded_scan2map(engine, ne, iter_max: int, group=None, poll: int = 4) -> int:
+def sharded_scan2map(engine, ne, iter_max: int, group=None, poll: int = 4, force_collective: bool = False) -> int:
     """Run one split-correspondence scan-to-map batch; `ne` is the [P, NE_WORDS] int64 exchange
     buffer (on the engine's device for RCCL, a CPU tensor for gloo). The engine must be bound to
     the same stream torch uses for the collective (the current stream). Returns the LM
-    iterations run (the loop stops early once every problem converged)."""
+    iterations run (the loop stops early once every problem converged). At world 1 the
+    all-reduce is an identity and is skipped unless force_collective (which runs it through the
+    initialised process group, e.g. a one-rank RCCL group)."""
     import torch.distributed as dist
     world, rank = world_and_rank(group)
+    collective = world > 1 or (force_collective and dist.is_available() and dist.is_initialized())
     engine.begin()
     it = 0
     while it < iter_max:
         engine.partial(rank, world, ne)
-        if world > 1:
+        if collective:
             dist.all_reduce(ne, op=dist.ReduceOp.SUM, group=group)
         it += 1
         active = engine.step(ne, poll=(it % poll == 0 or it == iter_max))
@@ -93,11 +96,11 @@ def max_over_ranks(seconds: float, device=None, group=None) -> float:
 
 
 def allreduce_latency_us(ne, reps: int = 50, group=None) -> float:
-    """Mean wall time of one all-reduce of the exchange buffer (synchronised per call)."""
+    """Mean wall time of one all-reduce of the exchange buffer (synchronised per call); 0.0 when no
+    process group is initialised (a one-rank group is measured: RCCL still runs the collective)."""
     import torch
     import torch.distributed as dist
-    world, _ = world_and_rank(group)
-    if world == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return 0.0
     cuda = ne.is_cuda
     ne.zero_()

@@ -94,8 +94,10 @@ int64_t oracle_voxel_grid(const float* in, int64_t n, float leaf, int32_t stable
 int32_t oracle_keypose_radius(const float* poses4, int32_t K, const float* pos, float radius, int32_t* out);
 /* MapOptimization keyframe store + extractSurroundingKeyFrames (oracle_map.cpp). */
 typedef struct oracle_map oracle_map;
-oracle_map* oracle_map_create(float radius, float keypose_leaf, float corner_leaf, float surf_leaf);
+oracle_map* oracle_map_create(float radius, float keypose_leaf, float corner_leaf, float surf_leaf,
+                              int32_t loop_closure, int32_t search_num);
 void oracle_map_destroy(oracle_map* m);
+void oracle_transform_cloud(const float* pose6, const float* in, int64_t n, float* out);
 int32_t oracle_map_add_keyframe(oracle_map* m, const float* pose6, const float* corner, int32_t n_corner,
                                 const float* surf, int32_t n_surf, const float* outlier, int32_t n_outlier);
 int32_t oracle_map_extract(oracle_map* m, const float* pos, int32_t stable, float* corner_out, int64_t cap_corner,

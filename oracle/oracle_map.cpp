@@ -1,7 +1,7 @@
 // oracle_map.cpp — TEST INFRASTRUCTURE ONLY (see oracle.h).
 //
-// Scalar CPU restatement of MapOptimization's local-map assembly, loop closure disabled (the
-// setting of every config block, CFG:23):
+// Scalar CPU restatement of MapOptimization's local-map assembly, both branches of
+// extractSurroundingKeyFrames (MO:1096-1232):
 //   * the keyframe store of saveKeyFramesAndFactor (MO:1686-1752): key pose x, y, z, roll, pitch,
 //     yaw (cloudKeyPoses3D / 6D, intensity = keyframe index) + the corner / surf / outlier clouds;
 //   * extractSurroundingKeyFrames (MO:1151-1231): radiusSearch of the key poses around the robot
@@ -9,7 +9,11 @@
 //     155-175, the distance being ((0 + dx^2) + dy^2) + dz^2 of L2_Simple_Adaptor), VoxelGrid 1.0 of
 //     those poses (MO:1166-1167), the surroundingExistingKeyPosesID list kept in the reference's
 //     erase / append order (MO:1169-1222), transformPointCloud (MO:671-701) of every listed keyframe
-//     and the concatenation + VoxelGrid 0.2 / 0.4 (MO:1224-1231).
+//     and the concatenation + VoxelGrid 0.2 / 0.4 (MO:1224-1231);
+//   * with enable_loop_closure (the VLP-32c / HDL-64E blocks, CFG:91, 159), MO:1099-1151 as written:
+//     three deques of clouds transformed when pushed (recent{Corner,Surf,Outlier}CloudKeyFrames),
+//     rebuilt from the newest keyframe backwards while shorter than surrounding_keyframe_search_num,
+//     else pop-front / push-back of the newest when latestFrameID changed.
 // The radius search is brute force here: the result SET is what matters, because the VoxelGrid of
 // the selected poses only keeps the integer mean of their indices (exact in float for any summation
 // order below 2^24). The _ref build (-DLLSR_ORACLE_NANOFLANN) also exports ref_keypose_radius over
@@ -17,6 +21,7 @@
 // sin / cos are the host glibc float functions the reference calls on the float pose fields.
 #include <algorithm>
 #include <array>
+#include <deque>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -56,9 +61,14 @@ void transform_cloud(const std::vector<float>& in, const float* t, std::vector<f
 
 struct oracle_map {
   float radius, kp_leaf, corner_leaf, surf_leaf;
+  int loop_closure = 0, search_num = 50;                   // _loop_closure_enabled, _surrounding_keyframe_search_num
   std::vector<std::array<float, 6>> pose;                  // x, y, z, roll, pitch, yaw
   std::vector<std::vector<float>> corner, surf, outlier;   // per keyframe, x y z i
   std::vector<int> existing;                               // surroundingExistingKeyPosesID
+  // loop-closure branch (mapOptimization.h:139-142): transformed clouds + their keyframe indices
+  std::deque<std::vector<float>> recent_corner, recent_surf, recent_outlier;
+  std::deque<int> recent_id;
+  int latestFrameID = 0;                                    // MO:301
 };
 
 #ifdef LLSR_ORACLE_NANOFLANN
@@ -121,8 +131,11 @@ int32_t ref_keypose_radius(const float* poses4, int32_t K, const float* pos, flo
 #endif
 
 #ifndef LLSR_ORACLE_NANOFLANN
-oracle_map* oracle_map_create(float radius, float keypose_leaf, float corner_leaf, float surf_leaf) {
+oracle_map* oracle_map_create(float radius, float keypose_leaf, float corner_leaf, float surf_leaf,
+                              int32_t loop_closure, int32_t search_num) {
   oracle_map* m = new oracle_map();
+  m->loop_closure = loop_closure;
+  m->search_num = search_num;
   m->radius = radius;
   m->kp_leaf = keypose_leaf;
   m->corner_leaf = corner_leaf;
@@ -131,6 +144,13 @@ oracle_map* oracle_map_create(float radius, float keypose_leaf, float corner_lea
 }
 
 void oracle_map_destroy(oracle_map* m) { delete m; }
+
+// transformPointCloud (MO:671-701) of n points by a key pose (x, y, z, roll, pitch, yaw).
+void oracle_transform_cloud(const float* pose6, const float* in, int64_t n, float* out) {
+  std::vector<float> src(in, in + 4 * (size_t)n), dst;
+  transform_cloud(src, pose6, dst);
+  if (!dst.empty()) std::memcpy(out, dst.data(), dst.size() * sizeof(float));
+}
 
 int32_t oracle_map_add_keyframe(oracle_map* m, const float* pose6, const float* c, int32_t nc, const float* s,
                                 int32_t ns, const float* o, int32_t no) {
@@ -156,6 +176,60 @@ int32_t oracle_map_extract(oracle_map* m, const float* pos, int32_t stable, floa
   for (int k = 0; k < 4; ++k) raw_counts[k] = 0;
   const int K = (int)m->pose.size();
   if (K == 0) return LLSR_OK;  // MO:1097
+  if (m->loop_closure) {
+    std::vector<float> cm, sm;
+    if ((int)m->recent_corner.size() < m->search_num) {  // MO:1101-1123
+      m->recent_corner.clear();
+      m->recent_surf.clear();
+      m->recent_outlier.clear();
+      m->recent_id.clear();
+      const int numPoses = K;
+      for (int i = numPoses - 1; i >= 0; --i) {
+        const int thisKeyInd = i;  // (int)cloudKeyPoses3D->points[i].intensity, = i (MO:1695-1697)
+        std::vector<float> c, s, o;
+        transform_cloud(m->corner[thisKeyInd], m->pose[thisKeyInd].data(), c);
+        transform_cloud(m->surf[thisKeyInd], m->pose[thisKeyInd].data(), s);
+        transform_cloud(m->outlier[thisKeyInd], m->pose[thisKeyInd].data(), o);
+        m->recent_corner.push_front(c);
+        m->recent_surf.push_front(s);
+        m->recent_outlier.push_front(o);
+        m->recent_id.push_front(thisKeyInd);
+        if ((int)m->recent_corner.size() >= m->search_num) break;
+      }
+    } else if (m->latestFrameID != K - 1) {  // MO:1124-1144
+      m->recent_corner.pop_front();
+      m->recent_surf.pop_front();
+      m->recent_outlier.pop_front();
+      m->recent_id.pop_front();
+      m->latestFrameID = K - 1;
+      std::vector<float> c, s, o;
+      transform_cloud(m->corner[m->latestFrameID], m->pose[m->latestFrameID].data(), c);
+      transform_cloud(m->surf[m->latestFrameID], m->pose[m->latestFrameID].data(), s);
+      transform_cloud(m->outlier[m->latestFrameID], m->pose[m->latestFrameID].data(), o);
+      m->recent_corner.push_back(c);
+      m->recent_surf.push_back(s);
+      m->recent_outlier.push_back(o);
+      m->recent_id.push_back(m->latestFrameID);
+    }
+    for (size_t i = 0; i < m->recent_corner.size(); ++i) {  // MO:1147-1151
+      cm.insert(cm.end(), m->recent_corner[i].begin(), m->recent_corner[i].end());
+      sm.insert(sm.end(), m->recent_surf[i].begin(), m->recent_surf[i].end());
+      sm.insert(sm.end(), m->recent_outlier[i].begin(), m->recent_outlier[i].end());
+    }
+    raw_counts[0] = (int64_t)(cm.size() / 4);
+    raw_counts[1] = (int64_t)(sm.size() / 4);
+    std::vector<float> cds, sds;
+    oracle_voxel::voxel_grid(cm.data(), cm.size() / 4, m->corner_leaf, cds, stable != 0);
+    oracle_voxel::voxel_grid(sm.data(), sm.size() / 4, m->surf_leaf, sds, stable != 0);
+    *n_corner = (int64_t)(cds.size() / 4);
+    *n_surf = (int64_t)(sds.size() / 4);
+    *n_ids = (int32_t)m->recent_id.size();
+    if (*n_corner > cap_c || *n_surf > cap_s || *n_ids > cap_ids) return LLSR_ERANGE;
+    if (!cds.empty()) std::memcpy(corner_out, cds.data(), cds.size() * sizeof(float));
+    if (!sds.empty()) std::memcpy(surf_out, sds.data(), sds.size() * sizeof(float));
+    for (int k = 0; k < *n_ids; ++k) ids[k] = m->recent_id[k];
+    return LLSR_OK;
+  }
   std::vector<float> p4(4 * (size_t)K);
   for (int k = 0; k < K; ++k) {
     for (int a = 0; a < 3; ++a) p4[4 * k + a] = m->pose[k][a];

@@ -68,8 +68,9 @@ def lib():
         L.oracle_keypose_radius.restype = C.c_int32
         L.oracle_keypose_radius.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_float, C.c_void_p]
         L.oracle_map_create.restype = C.c_void_p
-        L.oracle_map_create.argtypes = [C.c_float] * 4
+        L.oracle_map_create.argtypes = [C.c_float] * 4 + [C.c_int32] * 2
         L.oracle_map_destroy.argtypes = [C.c_void_p]
+        L.oracle_transform_cloud.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
         L.oracle_map_add_keyframe.restype = C.c_int32
         L.oracle_map_add_keyframe.argtypes = [C.c_void_p, C.c_void_p] + [C.c_void_p, C.c_int32] * 3
         L.oracle_map_extract.restype = C.c_int32
@@ -443,11 +444,22 @@ def keypose_radius(poses4, pos, radius: float, knn: str = "brute") -> np.ndarray
     return out[:n].copy()
 
 
+def transform_keyframe(pose6, xyzi) -> np.ndarray:
+    """transformPointCloud (MO:671-701) of a keyframe cloud by its key pose (x, y, z, roll, pitch, yaw)."""
+    p = np.ascontiguousarray(pose6, np.float32)
+    a = _f4(xyzi)
+    out = np.zeros_like(a)
+    if len(a):
+        lib().oracle_transform_cloud(p.ctypes.data, a.ctypes.data, len(a), out.ctypes.data)
+    return out
+
+
 class OracleMap:
     """MapOptimization keyframe store + extractSurroundingKeyFrames (oracle_map.cpp)."""
 
-    def __init__(self, radius=50.0, keypose_leaf=1.0, corner_leaf=0.2, surf_leaf=0.4, stable=False):
-        self._m = lib().oracle_map_create(radius, keypose_leaf, corner_leaf, surf_leaf)
+    def __init__(self, radius=50.0, keypose_leaf=1.0, corner_leaf=0.2, surf_leaf=0.4, stable=False,
+                 loop_closure: bool = False, search_num: int = 50):
+        self._m = lib().oracle_map_create(radius, keypose_leaf, corner_leaf, surf_leaf, int(loop_closure), search_num)
         self.stable = stable
         self._nc = self._ns = 0
 
@@ -551,12 +563,20 @@ class OracleMapping:
     device does; `stable` = True would sum each voxel in input order instead (diagnostics)."""
 
     def __init__(self, cfg: _abi.Config, mo_mode: int, radius=50.0, keypose_leaf=1.0, corner_leaf=0.2,
-                 surf_leaf=0.4, outlier_leaf=0.4, stable: bool = False, pcl_voxel_order: bool = False):
+                 surf_leaf=0.4, outlier_leaf=0.4, stable: bool = False, pcl_voxel_order: bool = False,
+                 loop_closure: bool | None = None, search_num: int = 50):
+        """loop_closure None: the config block of the lidar (enable_loop_closure true for the
+        HDL-64E block, CFG:159; false for VLP-16, CFG:23)."""
         import copy
         self.odo = OracleOdometry(cfg, pcl_voxel_order)
         self.cfg_mo = copy.copy(cfg)
         self.cfg_mo.mode = mo_mode
-        self.map = OracleMap(radius, keypose_leaf, corner_leaf, surf_leaf, stable=stable)
+        if loop_closure is None:
+            loop_closure = cfg.num_vertical_scans == 64
+        self.map = OracleMap(radius, keypose_leaf, corner_leaf, surf_leaf, stable=stable,
+                             loop_closure=loop_closure, search_num=search_num)
+        self.divider = cfg.mapping_frequency_divider
+        self.cycle = 0  # FeatureAssociation::_cycle_count (FA:92, 2818-2821)
         self.leaf = (corner_leaf, surf_leaf, outlier_leaf)
         self.stable = stable
         z = lambda: np.zeros(6, np.float32)  # noqa: E731
@@ -575,6 +595,10 @@ class OracleMapping:
         out = {"odo": o, "step": False, "frames": o["frames"]}
         if o["lm"] is None:  # checkSystemInitialization: no AssociationOut (FA:2781-2784)
             return out
+        self.cycle += 1  # FA:2818-2821: an AssociationOut on every divider-th frame
+        if self.cycle != self.divider:
+            return out
+        self.cycle = 0
         lc, ls, lo = self.leaf
         # OdometryToTransform + transformAssociateToMap (MO:1878-1880)
         self.transform_sum = odometry_to_transform(o["transform_sum"])

@@ -1,18 +1,41 @@
 // consumer.cpp — TEST HARNESS: a C++ caller of the drop-in boundary, built against include/llsr.h
 // and linked with libllsr.so exactly as INTEGRATION.md §2 tells a maintainer to (one TU, the
-// header, -lllsr). It follows ImageProjection::cloudHandler's replacement: the scan arrives as
-// PCL PointXYZI records (32 bytes: x y z _ intensity _ _ _, pcl/point_types.h layout), is repacked
-// to float4, handed to llsr_process_scan, and the outputs that fill CloudInfo / ProjectionOut and
-// the FA feature clouds are written to a file the test compares with the ctypes path.
+// header, -lllsr), making the calls INTEGRATION.md §2 shows the ROS nodes making. Each mode writes
+// its outputs to a file that tests/test_gpu_consumer.py compares with the oracle (and, for ipfa,
+// with the ctypes path too).
 //
-// usage: consumer <scans.bin> <out.bin>
-//   scans.bin: int32 n_scans, then per scan int32 n + n x float32[4] (x, y, z, intensity)
-//   out.bin:   per scan int32[8] counts {n_points, S, O, M, Ms, F, L, H}, float32[3] orientation,
-//              int32[H] start_ring, int32[H] end_ring, float32[4S] seg_xyzi, uint8[S] ground flag,
-//              uint32[S] col_ind, float32[S] range, float32[4O] outlier_xyzi, float32[4S] loam_xyzi,
-//              int32[M] less_sharp_ind, int32[Ms] sharp_ind, int32[F] flat_ind, float32[4L] less_flat
+// usage: consumer <mode> <in.bin> <out.bin>
+//   ipfa     ImageProjection::cloudHandler's replacement: the scan arrives as PCL PointXYZI records
+//            (32 bytes: x y z _ intensity _ _ _, pcl/point_types.h layout), is repacked to float4
+//            and handed to llsr_process_scan; the outputs that fill CloudInfo / ProjectionOut and
+//            the FA feature clouds are written out.
+//              in:  int32 n_scans, then per scan int32 n + n x float32[4] (x, y, z, intensity)
+//              out: per scan int32[8] counts {n_points, S, O, M, Ms, F, L, H}, float32[3]
+//                   orientation, int32[H] start_ring, int32[H] end_ring, float32[4S] seg_xyzi,
+//                   uint8[S] ground flag, uint32[S] col_ind, float32[S] range, float32[4O]
+//                   outlier_xyzi, float32[4S] loam_xyzi, int32[M] less_sharp_ind, int32[Ms]
+//                   sharp_ind, int32[F] flat_ind, float32[4L] less_flat
+//   s2s      FeatureAssociation::updateTransformation's replacement (llsr_scan2scan) on a sequence
+//            of problems; transformCur / isDegenerate are the node's members, carried from one
+//            problem to the next as in the reference.
+//              in:  int32 P, float32[6] transformCur, int32 isDegenerate, then per problem
+//                   int32[4] sizes + the float4 clouds cornerPointsSharp, surfPointsFlat,
+//                   laserCloudCornerLast, laserCloudSurfLast
+//              out: per problem float32[6] transformCur, int32 isDegenerate, llsr_s2s_report
+//   s2m      MapOptimization::scan2MapOptimization's replacement (llsr_scan2map)
+//              in:  int32 P, then per problem int32[4] sizes + the float4 clouds CornerScanDS,
+//                   SurfTotalLastDS, CornerFromMapDS, SurfFromMapDS, float32[6] transformTobeMapped
+//              out: per problem float32[6] transformTobeMapped, llsr_lm_report
+//   mapping  the whole chain for one drive through the device-resident entry points
+//            (llsr_mapping_init / _batch / _fetch / _keyposes), scans uploaded with hipMemcpy
+//              in:  int32 mo_mode, int32 n_scans, then per scan int32 n + float4 points
+//              out: per scan llsr_mapping_slot, then int32 K + float32[6K] key poses
+#include <hip/hip_runtime.h>
+
 #include <cstdint>
 #include <cstdio>
+#include <cstring>
+#include <string>
 #include <vector>
 
 #include "llsr.h"
@@ -27,16 +50,151 @@ template <class T>
 void put(FILE* f, const T* p, size_t n) {
   if (n) fwrite(p, sizeof(T), n, f);
 }
+
+template <class T>
+bool get(FILE* f, T* p, size_t n) {
+  return n == 0 || fread(p, sizeof(T), n, f) == n;
+}
+
+bool get_cloud(FILE* f, std::vector<float>& c, int32_t n) {
+  if (n < 0) return false;
+  c.resize(4 * (size_t)n);
+  return get(f, c.data(), c.size());
+}
+
+const float* ptr(const std::vector<float>& c) { return c.empty() ? nullptr : c.data(); }
+
+// FeatureAssociation::updateTransformation: the node's transformCur and
+// isDegenerate members go in and come back through the call
+int run_s2s(FILE* in, FILE* out) {
+  int32_t P = 0, deg = 0;
+  float tcur[6];
+  if (!get(in, &P, 1) || !get(in, tcur, 6) || !get(in, &deg, 1)) return 2;
+  llsr_config cfg;
+  llsr_config_default(&cfg, LLSR_LIDAR_VLP16);
+  cfg.mode = LLSR_MODE_LM_APPLIED;
+  llsr_handle* h = nullptr;
+  if (llsr_create(&cfg, 0, 1, 1, &h) != LLSR_OK) return 4;
+  std::vector<float> c[4];
+  for (int p = 0; p < P; ++p) {
+    int32_t n[4];
+    if (!get(in, n, 4)) return 2;
+    for (int k = 0; k < 4; ++k)
+      if (!get_cloud(in, c[k], n[k])) return 2;
+    llsr_s2s_report rep;
+    const int32_t rc = llsr_scan2scan(h, ptr(c[0]), n[0], ptr(c[1]), n[1], ptr(c[2]), n[2], ptr(c[3]), n[3], tcur,
+                                      &deg, &rep);
+    if (rc != LLSR_OK) {
+      fprintf(stderr, "llsr_scan2scan: %d %s\n", rc, llsr_last_error(h));
+      return 5;
+    }
+    put(out, tcur, 6);
+    put(out, &deg, 1);
+    put(out, &rep, 1);
+  }
+  llsr_destroy(h);
+  return 0;
+}
+
+// MapOptimization::scan2MapOptimization: transformTobeMapped in / out
+int run_s2m(FILE* in, FILE* out) {
+  int32_t P = 0;
+  if (!get(in, &P, 1)) return 2;
+  llsr_config cfg;
+  llsr_config_default(&cfg, LLSR_LIDAR_VLP16);
+  cfg.mode = LLSR_MODE_LM_APPLIED;
+  llsr_handle* h = nullptr;
+  if (llsr_create(&cfg, 0, 1, 1, &h) != LLSR_OK) return 4;
+  std::vector<float> c[4];
+  for (int p = 0; p < P; ++p) {
+    int32_t n[4];
+    float pose[6];
+    if (!get(in, n, 4)) return 2;
+    for (int k = 0; k < 4; ++k)
+      if (!get_cloud(in, c[k], n[k])) return 2;
+    if (!get(in, pose, 6)) return 2;
+    llsr_lm_report rep;
+    const int32_t rc = llsr_scan2map(h, ptr(c[0]), n[0], ptr(c[1]), n[1], ptr(c[2]), n[2], ptr(c[3]), n[3], pose, &rep);
+    if (rc != LLSR_OK) {
+      fprintf(stderr, "llsr_scan2map: %d %s\n", rc, llsr_last_error(h));
+      return 5;
+    }
+    put(out, pose, 6);
+    put(out, &rep, 1);
+  }
+  llsr_destroy(h);
+  return 0;
+}
+
+// The mapping chain of one drive: scans uploaded to HBM (what a node holding the decoded cloud on
+// the device would pass), one llsr_mapping_batch per scan, the slot state and key poses read back
+int run_mapping(FILE* in, FILE* out) {
+  int32_t mo_mode = 0, n_scans = 0;
+  if (!get(in, &mo_mode, 1) || !get(in, &n_scans, 1)) return 2;
+  llsr_config cfg;
+  llsr_config_default(&cfg, LLSR_LIDAR_VLP16);
+  cfg.mode = LLSR_MODE_LM_APPLIED;  // the odometry's mode; mo_mode is MapOptimization's
+  llsr_handle* h = nullptr;
+  if (llsr_create(&cfg, 0, 1, 40000, &h) != LLSR_OK) return 4;
+  if (llsr_mapping_init(h, mo_mode, nullptr) != LLSR_OK) {
+    fprintf(stderr, "llsr_mapping_init: %s\n", llsr_last_error(h));
+    return 5;
+  }
+  float* d_pts = nullptr;
+  int64_t* d_off = nullptr;
+  if (hipMalloc(&d_pts, 40000 * 16) != hipSuccess || hipMalloc(&d_off, 2 * sizeof(int64_t)) != hipSuccess) return 4;
+  std::vector<float> c;
+  for (int s = 0; s < n_scans; ++s) {
+    int32_t n = 0;
+    if (!get(in, &n, 1) || n > 40000 || !get_cloud(in, c, n)) return 2;
+    const int64_t off[2] = {0, n};
+    if (hipMemcpy(d_pts, c.data(), c.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_off, off, sizeof off, hipMemcpyHostToDevice) != hipSuccess)
+      return 4;
+    int32_t rc = llsr_mapping_batch(h, d_pts, d_off, 1, nullptr);
+    llsr_mapping_slot slot;
+    if (rc == LLSR_OK) rc = llsr_mapping_fetch(h, 0, &slot);
+    if (rc != LLSR_OK) {
+      fprintf(stderr, "llsr_mapping: %d %s\n", rc, llsr_last_error(h));
+      return 5;
+    }
+    put(out, &slot, 1);
+  }
+  const int32_t K = llsr_mapping_keyposes(h, 0, nullptr, 0);
+  std::vector<float> kp(6 * (size_t)(K > 0 ? K : 1));
+  llsr_mapping_keyposes(h, 0, kp.data(), K);
+  put(out, &K, 1);
+  put(out, kp.data(), 6 * (size_t)K);
+  (void)hipFree(d_pts);
+  (void)hipFree(d_off);
+  llsr_destroy(h);
+  return 0;
+}
 }  // namespace
 
+int run_ipfa(FILE* in, FILE* out);
+
 int main(int argc, char** argv) {
-  if (argc != 3) {
-    fprintf(stderr, "usage: %s scans.bin out.bin\n", argv[0]);
+  if (argc != 4) {
+    fprintf(stderr, "usage: %s ipfa|s2s|s2m|mapping in.bin out.bin\n", argv[0]);
     return 2;
   }
-  FILE* in = fopen(argv[1], "rb");
-  FILE* out = fopen(argv[2], "wb");
+  const std::string mode = argv[1];
+  FILE* in = fopen(argv[2], "rb");
+  FILE* out = fopen(argv[3], "wb");
   if (!in || !out) return 2;
+  int rc = 2;
+  if (mode == "ipfa") rc = run_ipfa(in, out);
+  else if (mode == "s2s") rc = run_s2s(in, out);
+  else if (mode == "s2m") rc = run_s2m(in, out);
+  else if (mode == "mapping") rc = run_mapping(in, out);
+  fclose(out);
+  fclose(in);
+  return rc;
+}
+
+// ImageProjection::cloudHandler + the FA feature stage
+int run_ipfa(FILE* in, FILE* out) {
   int32_t n_scans = 0;
   if (fread(&n_scans, 4, 1, in) != 1) return 2;
 
@@ -106,7 +264,5 @@ int main(int argc, char** argv) {
     put(out, lflat.data(), 4 * (size_t)o.n_less_flat);
   }
   llsr_destroy(h);
-  fclose(out);
-  fclose(in);
   return 0;
 }

@@ -107,3 +107,30 @@ def test_extract_surrounding_keyframes_sequence(require_gpu):
         assert np.array_equal(_bits(_np(gs)), _bits(rs)), k
     assert dropped, "the path must take keyframes out of the surrounding list"
     m.close()
+
+
+@pytest.mark.parametrize("search_num", [4, 50])
+def test_extract_loop_closure_queue_sequence(require_gpu, search_num):
+    """enable_loop_closure (the HDL-64E / VLP-32c blocks): the recent-keyframe queue of
+    MO:1099-1151 — refilled while short, then pop oldest / push newest per new keyframe, kept on a
+    repeated call (latestFrameID) — keyframe ids, raw sizes and both local maps bit-exact."""
+    from llsr import map_config
+    frames = synth.make_keyframes(60 if search_num == 50 else 14, seed=8)
+    m = LocalMap(0, map_config("hdl64e", surrounding_keyframe_search_num=search_num))
+    om = oracle_py.OracleMap(loop_closure=True, search_num=search_num)
+    popped = False
+    for k, (pose, c, s, o) in enumerate(frames):
+        assert m.add_keyframe(pose, c, s, o) == k
+        om.add_keyframe(pose, c, s, o)
+        for _ in range(2 if k % 5 == 3 else 1):
+            pos = np.full(3, 1e4, np.float32)  # unused by this branch
+            gc, gs, rep = m.extract(pos)
+            rc, rs, ids, orep = om.extract(pos)
+            assert m.keyframe_ids().tolist() == ids.tolist(), k
+            popped |= len(ids) == search_num and ids[0] > 0
+            for key in ("n_in_radius", "n_poses_ds", "n_keyframes", "n_corner_map", "n_surf_map"):
+                assert rep[key] == orep[key], (k, key)
+            assert np.array_equal(_bits(_np(gc)), _bits(rc)), k
+            assert np.array_equal(_bits(_np(gs)), _bits(rs)), k
+    assert popped
+    m.close()

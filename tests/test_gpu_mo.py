@@ -173,3 +173,31 @@ def test_scan2map_degenerate(require_gpu, mode):
             errs.append(f"problem {k}: a degenerate problem moved the pose")
     pipe.close()
     assert not errs, "\n".join(errs)
+
+
+def test_scan2map_more_depth_blocks_than_lds(require_gpu):
+    """A problem with ~50k correspondences: Eigen's GEMM splits matAt * matA into 74 depth blocks of
+    kc = 680 rows, more than the 64 k_s2m_solve keeps in LDS; the rest go through the
+    problem's spill rows. Bit-exact against the oracle, no LLSR_ERANGE."""
+    rng = np.random.default_rng(17)
+    g = np.arange(-60.0, 60.0, 0.35, dtype=np.float32)
+    xx, yy = np.meshgrid(g, g, indexing="ij")
+    surf_map = np.stack([xx.ravel(), yy.ravel(), rng.normal(0, 0.01, xx.size), np.zeros(xx.size)], 1)
+    surf_map = surf_map.astype(np.float32)
+    n = 50000
+    surf_q = np.stack([rng.uniform(-55, 55, n), rng.uniform(-55, 55, n), rng.normal(0, 0.02, n),
+                       np.zeros(n)], 1).astype(np.float32)
+    corner_map = np.stack([np.full(40, 5.0), np.full(40, 5.0), np.linspace(0, 4, 40), np.zeros(40)], 1)
+    corner_map = corner_map.astype(np.float32)
+    corner_q = np.zeros((0, 4), np.float32)
+    pose0 = np.array([0.01, -0.02, 0.015, 0.1, 0.05, -0.2], np.float32)
+    cfg = _cfg(_abi.LLSR_MODE_LM_APPLIED)
+    cfg.iterCountThres = 3
+    pipe = Pipeline(cfg)
+    gm = pipe.scan2map(corner_q, surf_q, corner_map, surf_map, pose0)
+    om = oracle_py.scan2map(cfg, corner_q, surf_q, corner_map, surf_map, pose0)
+    pipe.close()
+    assert om["n_surf_corr"] > 44000, om["n_surf_corr"]  # > 64 depth blocks of 680 rows
+    for k in ("pose", "matX0", "min_lambda", "cf_mean", "iterations", "converged", "degenerate",
+              "n_corner_corr", "n_surf_corr"):
+        assert np.array_equal(np.asarray(gm[k]), np.asarray(om[k])), (k, gm[k], om[k])

@@ -185,3 +185,31 @@ def test_batch_scan_longer_than_max_points(require_gpu, lidar):
         errs = compare(pipe.fetch(b), o)
         assert not errs, f"slot {b}:\n  " + "\n  ".join(errs)
     pipe.close()
+
+
+def test_batches_queued_on_two_streams_before_fetch(require_gpu):
+    """three batches enqueued back to back on alternating streams with no fetch in
+    between. Only the handle's completion event orders them (hipStreamWaitEvent on last_done), so
+    the FA carry-over state of the first two batches must reach the third: its slots equal the
+    oracle's after the same three scans per slot."""
+    import torch
+    cfg = default_config("vlp16")
+    B = 3
+    pipe = Pipeline(cfg, max_batch=B, max_points=40000)
+    oracles = [oracle_py.Oracle(cfg) for _ in range(B)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    keep = []
+    for rep in range(3):
+        pts, off = synth.make_batch(B, "vlp16", distinct=B, seed0=51 + 7 * rep)
+        s = streams[rep % 2]
+        with torch.cuda.stream(s):
+            d_pts = torch.from_numpy(pts).to("cuda", non_blocking=False)
+            d_off = torch.from_numpy(off).to("cuda", non_blocking=False)
+        s.synchronize()
+        keep.append((d_pts, d_off))  # the inputs stay alive until the batches ran
+        pipe.process_batch(d_pts.data_ptr(), d_off.data_ptr(), B, s.cuda_stream)
+        last = [oracles[b].process(pts[off[b]:off[b + 1]]) for b in range(B)]
+    for b in range(B):
+        errs = compare(pipe.fetch(b), last[b])
+        assert not errs, f"slot {b}:\n  " + "\n  ".join(errs)
+    pipe.close()

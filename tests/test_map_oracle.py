@@ -14,6 +14,10 @@ import oracle_py
 from llsr import synth
 
 
+def _bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
 def _vg_scalar(pts, leaf):
     """Independent statement of PCL VoxelGrid with a stable sort (sum in input order)."""
     pts = np.asarray(pts, np.float32)
@@ -109,3 +113,41 @@ def test_extract_keyframe_list_semantics():
         assert rep["n_corner_map"] == sum(len(frames[i][1]) for i in existing)
         assert rep["n_surf_map"] == sum(len(frames[i][2]) + len(frames[i][3]) for i in existing)
     assert saw_drop and saw_avg, "the synthetic path must exercise list removal and index averaging"
+
+
+@pytest.mark.parametrize("search_num", [1, 4, 50])
+def test_extract_loop_closure_queue(search_num):
+    """enable_loop_closure (CFG:91, 159): the local map is the recent-keyframe queue of MO:1099-1151.
+    Checked against a list statement: while the queue is shorter than search_num it holds the
+    newest min(K, search_num) keyframes (rebuilt every call); once full, one pop-oldest / push-newest
+    per new keyframe; a repeated call without a new keyframe keeps it (latestFrameID, MO:1126). The
+    local map is the VoxelGrid of the queue's transformed clouds in queue order, surf + outlier per
+    keyframe (MO:1147-1151, 1224-1231)."""
+    frames = synth.make_keyframes(12, seed=5, corner=30, surf=60, outlier=15)
+    om = oracle_py.OracleMap(loop_closure=True, search_num=search_num)
+    radius = oracle_py.OracleMap(radius=1e-3)  # a radius branch that would select nothing near
+    q = []
+    latest = 0
+    for k, (pose, c, s, o) in enumerate(frames):
+        om.add_keyframe(pose, c, s, o)
+        radius.add_keyframe(pose, c, s, o)
+        for rep_call in range(2 if k in (3, 7) else 1):
+            K = k + 1
+            if len(q) < search_num:
+                q = list(range(max(0, K - search_num), K))
+            elif latest != K - 1:
+                q = q[1:] + [K - 1]
+                latest = K - 1
+            cmap, smap, ids, rep = om.extract(np.full(3, 1e4, np.float32))  # position unused
+            assert ids.tolist() == q, (k, rep_call)
+            assert rep["n_in_radius"] == 0 and rep["n_poses_ds"] == 0 and rep["n_keyframes"] == len(q)
+            assert rep["n_corner_map"] == sum(len(frames[i][1]) for i in q)
+            assert rep["n_surf_map"] == sum(len(frames[i][2]) + len(frames[i][3]) for i in q)
+            # the same keyframes through the radius branch's transform + VoxelGrid path
+            cm = [oracle_py.transform_keyframe(frames[i][0], frames[i][1]) for i in q]
+            sm = [x for i in q for x in (oracle_py.transform_keyframe(frames[i][0], frames[i][2]),
+                                         oracle_py.transform_keyframe(frames[i][0], frames[i][3]))]
+            assert np.array_equal(_bits(cmap), _bits(oracle_py.voxel_grid(np.concatenate(cm), 0.2)))
+            assert np.array_equal(_bits(smap), _bits(oracle_py.voxel_grid(np.concatenate(sm), 0.4)))
+    _, _, ids_r, _ = radius.extract(np.full(3, 1e4, np.float32))
+    assert len(ids_r) == 0
