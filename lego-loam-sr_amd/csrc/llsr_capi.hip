@@ -625,6 +625,21 @@ extern "C" float llsr_debug_phase_ms(llsr_handle* h, int32_t k, int32_t phase, i
   const int B = h->last_B;
   hipEvent_t e0 = h->ev[0][0], e1 = h->ev[0][1];
   if (sync_last(h) != LLSR_OK) return -1.f;
+  if (k == 8) {
+    // k_select_ring consumes the picked / label state k_fa_points leaves (and overwrites it):
+    // k_fa_points restores it before every timed launch, so each phase sees the batch's real work
+    float tot = 0.f;
+    for (int r = 0; r < reps; ++r) {
+      k_fa_points<<<B, 512, 0, s>>>(h->dc, h->d);
+      (void)hipEventRecord(e0, s);
+      k_select_ring<<<dim3(c.H, B), 256, 0, s>>>(c, h->d);
+      (void)hipEventRecord(e1, s);
+      float ms = 0.f;
+      if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) return -1.f;
+      tot += ms;
+    }
+    return tot / reps;
+  }
   (void)hipEventRecord(e0, s);
   for (int r = 0; r < reps; ++r) {
     switch (k) {

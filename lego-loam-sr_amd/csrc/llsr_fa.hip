@@ -195,110 +195,134 @@ __global__ __launch_bounds__(512) void k_fa_points(DevCfg c, DevBufs d) {
 constexpr int kRingMax = 2048;  // >= max W
 constexpr int kWin = kRingMax + 16;
 
-// Block bitonic sort of n2 (power of two) 64-bit keys in LDS, ascending.
-// Two consecutive stages (j, j/2) of one merge step run on groups of four keys {t, t+h, t+j, t+j+h}
-// (h = j/2, t with zeros at bits log2 h and log2 j) held in registers: the same compare-exchanges
-// as the one-stage network, half the LDS round trips and barriers.
-__device__ __forceinline__ void bitonic_cx(uint64_t& a, uint64_t& e, bool up) {
-  if ((a > e) == up) { const uint64_t t = a; a = e; e = t; }
-}
-__device__ __forceinline__ void bitonic_sort_u64(uint64_t* key, int n2, int kfrom = 2) {
-  const int half = n2 >> 1, quarter = n2 >> 2;
-  for (int k = kfrom; k <= n2; k <<= 1) {
-    int j = k >> 1;
-    while (j >= 2) {
-      const int h = j >> 1;
-      for (int p = threadIdx.x; p < quarter; p += blockDim.x) {
-        const int a = ((p & ~(h - 1)) << 1) | (p & (h - 1));  // 0 inserted at bit log2(h)
-        const int t = ((a & ~(j - 1)) << 1) | (a & (j - 1));  // and at bit log2(j)
-        const bool up = (t & k) == 0;
-        uint64_t v0 = key[t], v1 = key[t + h], v2 = key[t + j], v3 = key[t + j + h];
-        bitonic_cx(v0, v2, up);
-        bitonic_cx(v1, v3, up);
-        bitonic_cx(v0, v1, up);
-        bitonic_cx(v2, v3, up);
-        key[t] = v0; key[t + h] = v1; key[t + j] = v2; key[t + j + h] = v3;
-      }
-      __syncthreads();
-      j >>= 2;
-    }
-    if (j == 1) {
-      for (int p = threadIdx.x; p < half; p += blockDim.x) {
-        const int t = p << 1;
-        const bool up = (t & k) == 0;
-        uint64_t v0 = key[t], v1 = key[t + 1];
-        bitonic_cx(v0, v1, up);
-        key[t] = v0; key[t + 1] = v1;
-      }
-      __syncthreads();
-    }
+// Block sort of n2 (power of two, 256 <= n2 <= 64 * 4 * 8) keys (u64 or u32) in LDS, ascending, by
+// the 4 waves of the workgroup, the bitonic network with every stage whose partners lie in one wave
+// run in registers: lane exchanges through DPP row / quad permutations and gfx950's
+// v_permlane16/32_swap (VALU ops; ds_bpermute sits in the LDS queue), partners 64 or more apart
+// between a lane's own registers. Only the stages that pair different waves' quarters read the LDS
+// (each wave computes its own positions' results from the values it needs), so a sort costs five
+// barriers. The full bitonic network's compare-exchanges (padding ~0 keys stay at the end).
+template <int J>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v) {  // v of lane (lane ^ J), J < 64
+  const int l = threadIdx.x & 63;
+  if constexpr (J == 1) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+  } else if constexpr (J == 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+  } else if constexpr (J == 4) {  // row_ror:n: lane i reads lane (i - n) mod 16 of its row
+    const uint32_t a = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xf, 0xf, false);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x12C, 0xf, 0xf, false);
+    return (l & 4) ? a : b;
+  } else if constexpr (J == 8) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false);
+  } else if constexpr (J == 16) {  // odd 16-lane rows of the first operand <-> even rows of the second
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (l & 16) ? r[0] : r[1];
+  } else {  // upper 32 lanes of the first operand <-> lower 32 of the second
+    static_assert(J == 32, "lane_xor: J < 64");
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (l & 32) ? r[0] : r[1];
   }
 }
-
-// Block sort of n2 (power of two, 256 <= n2 <= 2048) 64-bit keys in LDS, ascending: each of the 4
-// waves sorts its quarter in registers (bitonic: stages below 64 with lane shuffles, the rest
-// between a lane's own registers; no barrier), then the last two bitonic merge levels run in LDS.
-// Same result as bitonic_sort_u64 (padding ~0 keys stay at the end).
-__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
-  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
-  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
-  return ((uint64_t)hi << 32) | lo;
+template <int J>
+__device__ __forceinline__ uint64_t lane_xor(uint64_t v) {
+  return ((uint64_t)lane_xor<J>((uint32_t)(v >> 32)) << 32) | lane_xor<J>((uint32_t)v);
 }
-template <int K>
-__device__ __forceinline__ void wave_bitonic(uint64_t (&v)[K]) {
+// One compare-exchange of a key with its partner's value o: the min when this position takes the
+// min (lower index of an ascending pair or upper of a descending one), else the max. Equal keys
+// are interchangeable. One compare, the mask flip and a select per 32-bit word.
+template <class T>
+__device__ __forceinline__ T cx(T v, T o, bool want_min) {
+  return ((o < v) == want_min) ? o : v;
+}
+// Stages J, J/2, ..., 1 of a bitonic merge of size SZ on the keys v[k] at positions base + 64 k + lane
+// (SZ <= 64 K: direction from the position; SZ > 64 K: `up` for the whole wave).
+template <int K, int SZ, int J, class T>
+__device__ __forceinline__ void wave_merge(T (&v)[K], int base, bool up_all) {
   const int lane = threadIdx.x & 63;
+  if constexpr (J >= 64) {
 #pragma unroll
-  for (int size = 2; size <= 64 * K; size <<= 1) {
-#pragma unroll
-    for (int j = size >> 1; j > 0; j >>= 1) {
-      if (j >= 64) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          const int kp = k ^ (j >> 6);
-          if (kp > k) {
-            const bool up = ((k * 64 + lane) & size) == 0;
-            const uint64_t a = v[k], b = v[kp];
-            const bool sw = (a > b) == up;
-            v[k] = sw ? b : a;
-            v[kp] = sw ? a : b;
-          }
-        }
-      } else {
-        const bool lower = (lane & j) == 0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          const uint64_t o = shfl_xor64(v[k], j);
-          const bool up = ((k * 64 + lane) & size) == 0;
-          const uint64_t mn = v[k] < o ? v[k] : o, mx = v[k] < o ? o : v[k];
-          v[k] = (lower == up) ? mn : mx;
-        }
+    for (int k = 0; k < K; ++k) {
+      constexpr int d = J >> 6;
+      if ((k & d) == 0) {
+        const bool up = SZ > 64 * K ? up_all : (((base + k * 64) & SZ) == 0);
+        const T a = v[k], b = v[k + d];
+        const bool sw = (b < a) == up;
+        v[k] = sw ? b : a;
+        v[k + d] = sw ? a : b;
       }
     }
+  } else {
+    const bool lower = (lane & J) == 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const bool up = SZ > 64 * K ? up_all : (((base + k * 64 + lane) & SZ) == 0);
+      v[k] = cx(v[k], lane_xor<J>(v[k]), lower == up);
+    }
   }
+  if constexpr (J > 1) wave_merge<K, SZ, J / 2>(v, base, up_all);
 }
-template <int K>
-__device__ void block4_sort_k(uint64_t* key) {
-  constexpr int Q = 64 * K;  // keys per wave
+template <int K, int SZ, class T>
+__device__ __forceinline__ void wave_sort_from(T (&v)[K], int base) {
+  wave_merge<K, SZ, SZ / 2>(v, base, true);
+  if constexpr (SZ < 64 * K) wave_sort_from<K, SZ * 2>(v, base);
+}
+template <int K, class T>
+__device__ void block4_sort_k(T* key) {
+  constexpr int Q = 64 * K;  // keys per wave, position w Q + 64 k + lane
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint64_t v[K];
+  T v[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) v[k] = key[w * Q + k * 64 + lane];
-  wave_bitonic<K>(v);
-  // the four sorted quarters, odd ones reversed, are the input of the bitonic network's last two
-  // merge levels (sizes 2Q and 4Q: up = (t & k) == 0 makes [0, 2Q) ascending and [2Q, 4Q)
-  // descending, then the whole range ascending): 2 log2(Q) + 1 stage pairs in LDS (measured
-  // 0.748 -> 0.728 ms per 1024 scans against ranking each key in the other quarters by binary search)
+  // every quarter sorted with the full network's directions below size Q (up = position & size == 0)
+  wave_sort_from<K, 2>(v, w * Q);
+  // merge of size 2Q (ascending for waves 0-1, descending for 2-3): stage Q pairs wave w with w ^ 1
+  const bool up2 = (w & 2) == 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) key[w * Q + k * 64 + lane] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = cx(v[k], key[(w ^ 1) * Q + k * 64 + lane], ((w & 1) == 0) == up2);
+  wave_merge<K, 2 * Q, Q / 2>(v, w * Q, up2);
+  __syncthreads();
+  // merge of size 4Q, ascending: stages 2Q (w with w ^ 2) and Q (w with w ^ 1) from the four values
+  // of the position group, then the in-wave stages
+#pragma unroll
+  for (int k = 0; k < K; ++k) key[w * Q + k * 64 + lane] = v[k];
+  __syncthreads();
+  const bool lo2 = (w & 2) == 0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const int i = k * 64 + lane;
-    key[w * Q + ((w & 1) ? Q - 1 - i : i)] = v[k];
+    const int p = k * 64 + lane;
+    const T a = cx(v[k], key[(w ^ 2) * Q + p], lo2);                // this position after stage 2Q
+    const T b = cx(key[(w ^ 1) * Q + p], key[(w ^ 3) * Q + p], lo2);  // its stage-Q partner after 2Q
+    v[k] = cx(a, b, (w & 1) == 0);
+  }
+  wave_merge<K, 4 * Q, Q / 2>(v, w * Q, true);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) key[w * Q + k * 64 + lane] = v[k];
+  __syncthreads();
+}
+// n2 <= 128 keys: wave 0 alone, in registers
+template <int K, class T>
+__device__ void wave0_sort_k(T* key) {
+  if (threadIdx.x < 64) {
+    T v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = key[k * 64 + threadIdx.x];
+    wave_sort_from<K, 2>(v, 0);
+#pragma unroll
+    for (int k = 0; k < K; ++k) key[k * 64 + threadIdx.x] = v[k];
   }
   __syncthreads();
-  bitonic_sort_u64(key, 4 * Q, 2 * Q);
 }
-// n2 = 4 * 64 * K for K in {1, 2, 4, 8}
-__device__ void block4_sort_u64(uint64_t* key, int n2) {
+// n2 = 64 * K for K in {1, 2, 4, 8, 16, 32}
+template <class T>
+__device__ void block4_sort(T* key, int n2) {
   switch (n2) {
+    case 64: wave0_sort_k<1>(key); break;
+    case 128: wave0_sort_k<2>(key); break;
     case 256: block4_sort_k<1>(key); break;
     case 512: block4_sort_k<2>(key); break;
     case 1024: block4_sort_k<4>(key); break;
@@ -364,7 +388,7 @@ __device__ __forceinline__ int greedy_wave(Order order, int nc, int ws, uint8_t*
   return nsel;
 }
 
-__global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
+__global__ __launch_bounds__(256, 4) void k_select_ring(DevCfg c, DevBufs d) {
   // LDS 36 KB -> 4 workgroups per CU. The window arrays are dead once the less-flat candidates are
   // compacted, so the VoxelGrid's voxel ids reuse their bytes; the greedy passes read the visiting
   // order straight from the sorted keys.
@@ -560,10 +584,10 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
   __syncthreads();
   if (c.dbg_phase <= 0) return;
   int nE = s_cnt;
-  int n2 = pow2_ceil(nE);
+  int n2 = max(pow2_ceil(nE), 64);
   for (int t = nE + tid; t < n2; t += nt) key[t] = 0ull;
   __syncthreads();
-  bitonic_sort_u64(key, n2);
+  block4_sort<uint64_t>(key, n2);
   if (c.dbg_phase <= 1) return;
   // (n2 - nE zero keys sort first: the eligible keys are key[n2 - nE, n2))
   if (ties(n2 - nE, n2)) {
@@ -594,10 +618,10 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
     append(false);
     __syncthreads();
     const int nF = s_cnt;
-    n2 = pow2_ceil(nF);
+    n2 = max(pow2_ceil(nF), 64);
     for (int t = nF + tid; t < n2; t += nt) key[t] = ~0ull;
     __syncthreads();
-    bitonic_sort_u64(key, n2);
+    block4_sort<uint64_t>(key, n2);
     if (ties(0, nF)) {
       exact_sort();
       if (tid < 64) {
@@ -771,11 +795,11 @@ __global__ __launch_bounds__(256) void k_select_ring(DevCfg c, DevBufs d) {
       key[ro] = ((uint64_t)vk[t] << 32) | (uint32_t)ro;
     }
     if (tid == 0) rstart[R] = (uint16_t)L;
-    const int R2 = max(pow2_ceil(R), 256);
+    const int R2 = max(pow2_ceil(R), 64);
     for (int t = R + tid; t < R2; t += nt) key[t] = ~0ull;
     __syncthreads();
     if (c.dbg_phase <= 5) return;
-    block4_sort_u64(key, R2);
+    block4_sort<uint64_t>(key, R2);
     if (c.dbg_phase <= 6) return;
     // voxels = groups of sorted runs with equal id; sum members in (run start, position) order.
     // Sorted run t = u * 256 + tid sits in slot u of a lane, so a wave's voxel heads of one slot are

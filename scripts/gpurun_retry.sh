@@ -6,7 +6,7 @@ to=$1; shift
 for attempt in 1 2 3 4 5 6; do
   out=$(/usr/local/graft/bin/gpurun --timeout "$to" -- "$@" 2>&1); rc=$?
   echo "$out" | tail -4
-  if echo "$out" | grep -qE "status=transient|backing off|no box|slot free"; then
+  if echo "$out" | grep -qE "status=transient|backing off|no box|slot free|busy"; then
     sleep 60; continue
   fi
   exit $rc
