@@ -92,41 +92,83 @@ constexpr int kAdjWords = kAdjCap / 32;
 // ---- wave / block primitives (wave64) ------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// Lane exchanges as VALU ops (ds_bpermute, what __shfl_* compile to, queues in the LDS pipe):
+// DPP row / quad permutations and gfx950's v_permlane16/32_swap.
+template <int J>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v) {  // v of lane (lane ^ J), J < 64
+  const int l = threadIdx.x & 63;
+  if constexpr (J == 1) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+  } else if constexpr (J == 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+  } else if constexpr (J == 4) {  // row_ror:n: lane i reads lane (i - n) mod 16 of its row
+    const uint32_t a = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xf, 0xf, false);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x12C, 0xf, 0xf, false);
+    return (l & 4) ? a : b;
+  } else if constexpr (J == 8) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false);
+  } else if constexpr (J == 16) {  // odd 16-lane rows of the first operand <-> even rows of the second
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (l & 16) ? r[0] : r[1];
+  } else {  // upper 32 lanes of the first operand <-> lower 32 of the second
+    static_assert(J == 32, "lane_xor: J < 64");
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (l & 32) ? r[0] : r[1];
+  }
+}
+template <int J>
+__device__ __forceinline__ uint64_t lane_xor(uint64_t v) {
+  return ((uint64_t)lane_xor<J>((uint32_t)(v >> 32)) << 32) | lane_xor<J>((uint32_t)v);
+}
+template <int J, class T>
+__device__ __forceinline__ T lane_xor_t(T v) {  // any 4- or 8-byte type
+  if constexpr (sizeof(T) == 4) return __builtin_bit_cast(T, lane_xor<J>(__builtin_bit_cast(uint32_t, v)));
+  else return __builtin_bit_cast(T, lane_xor<J>(__builtin_bit_cast(uint64_t, v)));
+}
+
+// inclusive scan (32-bit integers): DPP row_shr within 16-lane rows, then row_bcast:15 / :31
 template <class T>
 __device__ __forceinline__ T wave_incl_scan_add(T x) {
-  const int l = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    T y = __shfl_up(x, d, 64);
-    if (l >= d) x += y;
-  }
-  return x;
+  static_assert(sizeof(T) == 4, "wave_incl_scan_add: 32-bit integers");
+  const int l = lane_id(), rl = l & 15;
+  int v = (int)x, t;
+  t = __builtin_amdgcn_mov_dpp(v, 0x111, 0xf, 0xf, false); if (rl >= 1) v += t;   // row_shr:1
+  t = __builtin_amdgcn_mov_dpp(v, 0x112, 0xf, 0xf, false); if (rl >= 2) v += t;   // row_shr:2
+  t = __builtin_amdgcn_mov_dpp(v, 0x114, 0xf, 0xf, false); if (rl >= 4) v += t;   // row_shr:4
+  t = __builtin_amdgcn_mov_dpp(v, 0x118, 0xf, 0xf, false); if (rl >= 8) v += t;   // row_shr:8
+  t = __builtin_amdgcn_mov_dpp(v, 0x142, 0xf, 0xf, false); if ((l & 31) >= 16) v += t;  // row_bcast:15
+  t = __builtin_amdgcn_mov_dpp(v, 0x143, 0xf, 0xf, false); if (l >= 32) v += t;   // row_bcast:31
+  return (T)v;
 }
 
 template <class T>
 __device__ __forceinline__ T wave_reduce_add(T x) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  x += lane_xor_t<32>(x); x += lane_xor_t<16>(x); x += lane_xor_t<8>(x);
+  x += lane_xor_t<4>(x); x += lane_xor_t<2>(x); x += lane_xor_t<1>(x);
   return x;
 }
 
 template <class T>
 __device__ __forceinline__ T wave_reduce_min(T x) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    T y = __shfl_xor(x, d, 64);
-    x = y < x ? y : x;
-  }
+  T y;
+  y = lane_xor_t<32>(x); x = y < x ? y : x;
+  y = lane_xor_t<16>(x); x = y < x ? y : x;
+  y = lane_xor_t<8>(x); x = y < x ? y : x;
+  y = lane_xor_t<4>(x); x = y < x ? y : x;
+  y = lane_xor_t<2>(x); x = y < x ? y : x;
+  y = lane_xor_t<1>(x); x = y < x ? y : x;
   return x;
 }
 
 template <class T>
 __device__ __forceinline__ T wave_reduce_max(T x) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    T y = __shfl_xor(x, d, 64);
-    x = y > x ? y : x;
-  }
+  T y;
+  y = lane_xor_t<32>(x); x = y > x ? y : x;
+  y = lane_xor_t<16>(x); x = y > x ? y : x;
+  y = lane_xor_t<8>(x); x = y > x ? y : x;
+  y = lane_xor_t<4>(x); x = y > x ? y : x;
+  y = lane_xor_t<2>(x); x = y > x ? y : x;
+  y = lane_xor_t<1>(x); x = y > x ? y : x;
   return x;
 }
 

@@ -202,32 +202,6 @@ constexpr int kWin = kRingMax + 16;
 // between a lane's own registers. Only the stages that pair different waves' quarters read the LDS
 // (each wave computes its own positions' results from the values it needs), so a sort costs five
 // barriers. The full bitonic network's compare-exchanges (padding ~0 keys stay at the end).
-template <int J>
-__device__ __forceinline__ uint32_t lane_xor(uint32_t v) {  // v of lane (lane ^ J), J < 64
-  const int l = threadIdx.x & 63;
-  if constexpr (J == 1) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
-  } else if constexpr (J == 2) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
-  } else if constexpr (J == 4) {  // row_ror:n: lane i reads lane (i - n) mod 16 of its row
-    const uint32_t a = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xf, 0xf, false);
-    const uint32_t b = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x12C, 0xf, 0xf, false);
-    return (l & 4) ? a : b;
-  } else if constexpr (J == 8) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false);
-  } else if constexpr (J == 16) {  // odd 16-lane rows of the first operand <-> even rows of the second
-    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    return (l & 16) ? r[0] : r[1];
-  } else {  // upper 32 lanes of the first operand <-> lower 32 of the second
-    static_assert(J == 32, "lane_xor: J < 64");
-    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    return (l & 32) ? r[0] : r[1];
-  }
-}
-template <int J>
-__device__ __forceinline__ uint64_t lane_xor(uint64_t v) {
-  return ((uint64_t)lane_xor<J>((uint32_t)(v >> 32)) << 32) | lane_xor<J>((uint32_t)v);
-}
 // One compare-exchange of a key with its partner's value o: the min when this position takes the
 // min (lower index of an ascending pair or upper of a descending one), else the max. Equal keys
 // are interchangeable. One compare, the mask flip and a select per 32-bit word.
@@ -352,9 +326,10 @@ __global__ __launch_bounds__(64) void k_debug_exact_sort(const float* vals, int 
 // each chunk of 64 candidates reads `picked` once; the first still-alive candidate is selected,
 // candidates inside its suppression interval die, repeat. Steps per chunk = picks in the chunk.
 // Returns the number selected; writes labels, picked and the output list in selection order.
+// wflag[w]: bits 0-2 forward reach, 3-5 backward reach, 6 ground, 7 picked (k_select_ring).
 template <class Order>
-__device__ __forceinline__ int greedy_wave(Order order, int nc, int ws, uint8_t* wpick, const uint8_t* wreach,
-                                           int8_t* wlab, int8_t lab, int* outp) {
+__device__ __forceinline__ int greedy_wave(Order order, int nc, int ws, uint8_t* wflag, int8_t* wlab, int8_t lab,
+                                           int* outp) {
   const int l = lane_id();
   const unsigned long long lt = (1ull << l) - 1ull;
   int nsel = 0;
@@ -363,14 +338,14 @@ __device__ __forceinline__ int greedy_wave(Order order, int nc, int ws, uint8_t*
     const bool valid = t < nc;
     const int ind = valid ? order(t) : 0;
     const int w = valid ? ind - ws : 0;
-    bool alive = valid && wpick[w] == 0;
-    const int r = valid ? wreach[w] : 0;
-    const int lo = w - (r >> 4), hi = w + (r & 15);
+    const int r = valid ? wflag[w] : 0x80;
+    bool alive = valid && (r & 0x80) == 0;
+    const int lo = w - ((r >> 3) & 7), hi = w + (r & 7);
     unsigned long long sel = 0ull;
     unsigned long long m = __ballot(alive);
     while (m) {
       const int s = __ffsll((long long)m) - 1;
-      const int slo = __shfl(lo, s, 64), shi = __shfl(hi, s, 64);
+      const int slo = __builtin_amdgcn_readlane(lo, s), shi = __builtin_amdgcn_readlane(hi, s);  // s is uniform
       sel |= 1ull << s;
       if (l > s && w >= slo && w <= shi) alive = false;
       if (l == s) alive = false;
@@ -379,7 +354,8 @@ __device__ __forceinline__ int greedy_wave(Order order, int nc, int ws, uint8_t*
     if ((sel >> l) & 1ull) {
       wlab[w] = lab;
       outp[nsel + __popcll(sel & lt)] = ind;
-      for (int q = lo; q <= hi; ++q) wpick[q] = 1;
+      // other bits of the bytes are static during the passes: concurrent read-or-writes agree
+      for (int q = lo; q <= hi; ++q) wflag[q] = (uint8_t)(wflag[q] | 0x80);
     }
     nsel += __popcll(sel);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -388,17 +364,16 @@ __device__ __forceinline__ int greedy_wave(Order order, int nc, int ws, uint8_t*
   return nsel;
 }
 
-__global__ __launch_bounds__(256, 4) void k_select_ring(DevCfg c, DevBufs d) {
-  // LDS 36 KB -> 4 workgroups per CU. The window arrays are dead once the less-flat candidates are
-  // compacted, so the VoxelGrid's voxel ids reuse their bytes; the greedy passes read the visiting
-  // order straight from the sorted keys.
+__global__ __launch_bounds__(256, 5) void k_select_ring(DevCfg c, DevBufs d) {
+  // LDS < 32 KB -> 5 workgroups per CU. The window keeps two bytes per position: a flag byte
+  // (suppression reach forward | backward << 3 (FA:1186-1205), ground << 6, picked << 7) and the
+  // label; the VoxelGrid's voxel ids use key[] (dead after the greedy passes); the greedy passes read
+  // the visiting order straight from the sorted keys.
   __shared__ uint64_t key[kRingMax];
-  __shared__ uint32_t win_raw[6 * kWin / 4];
-  uint8_t* wpick = reinterpret_cast<uint8_t*>(win_raw);
-  uint8_t* wgnd = wpick + kWin;
-  int8_t* wlab = reinterpret_cast<int8_t*>(wpick + 2 * kWin);
-  uint8_t* wreach = wpick + 3 * kWin;  // suppression reach: fwd | bwd << 4 (FA:1186-1205)
-  uint16_t* wcol = reinterpret_cast<uint16_t*>(wpick + 4 * kWin);
+  __shared__ uint32_t win_raw[2 * kWin / 4];
+  uint8_t* wflag = reinterpret_cast<uint8_t*>(win_raw);
+  int8_t* wlab = reinterpret_cast<int8_t*>(wflag + kWin);
+  __shared__ uint16_t cfirst[kWin / 64 + 1];  // column of the first position of every 64
   __shared__ uint16_t cpos[kRingMax];
   __shared__ uint16_t rstart[kRingMax + 1];
   __shared__ int tmp[8];
@@ -424,13 +399,15 @@ __global__ __launch_bounds__(256, 4) void k_select_ring(DevCfg c, DevBufs d) {
   // in one round trip: kPer positions per lane, all loads in flight together (blockDim.x == 256)
   constexpr int kPer = (kWin + 255) / 256;
   float cvr[kPer];
+  uint32_t cl[kPer];
+  uint32_t pkm = 0, gdm = 0;  // picked / ground bit per slot
   {
     uint8_t pk[kPer], gd[kPer];
     int8_t lb[kPer];
-    uint32_t cl[kPer];
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int t = tid + u * 256, pos = ws + t;
+      cl[u] = 0;
       if (t < wn) {
         pk[u] = d.picked[base + pos];
         gd[u] = d.seg_ground[base + pos];
@@ -443,10 +420,10 @@ __global__ __launch_bounds__(256, 4) void k_select_ring(DevCfg c, DevBufs d) {
     for (int u = 0; u < kPer; ++u) {
       const int t = tid + u * 256;
       if (t < wn) {
-        wpick[t] = pk[u];
-        wgnd[t] = gd[u];
         wlab[t] = lb[u];
-        wcol[t] = (uint16_t)cl[u];
+        pkm |= (pk[u] != 0 ? 1u : 0u) << u;
+        gdm |= (gd[u] != 0 ? 1u : 0u) << u;
+        if ((t & 63) == 0) cfirst[t >> 6] = (uint16_t)cl[u];
       }
     }
   }
@@ -464,13 +441,18 @@ __global__ __launch_bounds__(256, 4) void k_select_ring(DevCfg c, DevBufs d) {
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int t = tid + u * 256;
-      const bool stop = t + 1 >= wn || abs((int)wcol[t + 1] - (int)wcol[t]) > 10;
+      const int dn = __shfl_down((int)cl[u], 1, 64);
+      const int nx = l < 63 ? dn : (t + 1 < wn ? (int)cfirst[(t + 1) >> 6] : 0);
+      const bool stop = t + 1 >= wn || abs(nx - (int)cl[u]) > 10;
       const uint64_t m = __ballot(t < wn && stop);
       if (l == 0 && (t >> 6) <= (wn >> 6)) gbits[t >> 6] = m;
     }
     __syncthreads();
     const int nw = (wn >> 6) + 1;
-    for (int t = tid; t < wn; t += nt) {
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int t = tid + u * 256;
+      if (t >= wn) break;
       const int k = t >> 6, sh = t & 63;
       uint64_t fw = gbits[k] >> sh;
       if (sh && k + 1 < nw) fw |= gbits[k + 1] << (64 - sh);
@@ -482,7 +464,7 @@ __global__ __launch_bounds__(256, 4) void k_select_ring(DevCfg c, DevBufs d) {
         if (s2 < 63 && kq > 0) bw |= gbits[kq - 1] >> (s2 + 1);
         bk = min(min(5, t), bw ? (int)__clzll((long long)bw) : 64);
       }
-      wreach[t] = (uint8_t)(f | (bk << 4));
+      wflag[t] = (uint8_t)(f | (bk << 3) | (((gdm >> u) & 1u) << 6) | (((pkm >> u) & 1u) << 7));
     }
   }
   __syncthreads();
@@ -544,11 +526,11 @@ __global__ __launch_bounds__(256, 4) void k_select_ring(DevCfg c, DevBufs d) {
   };
   auto edge_elig = [&](int ind) {
     const int w = ind - ws;
-    return w >= 0 && w < wn && wpick[w] == 0 && curv_of(ind) > c.edge_thr && wgnd[w] == 0;
+    return w >= 0 && w < wn && (wflag[w] & 0xC0) == 0 && curv_of(ind) > c.edge_thr;
   };
   auto flat_elig = [&](int ind) {
     const int w = ind - ws;
-    return w >= 0 && w < wn && wpick[w] == 0 && curv_of(ind) < c.surf_thr && wgnd[w] == 1;
+    return w >= 0 && w < wn && (wflag[w] & 0xC0) == 0x40 && curv_of(ind) < c.surf_thr;
   };
   // wave-aggregated append of the statically eligible keys of the fast path
   auto append = [&](bool edge) {
@@ -560,11 +542,12 @@ __global__ __launch_bounds__(256, 4) void k_select_ring(DevCfg c, DevBufs d) {
       const float v = p == 4 ? 0.0f : cvr[u];          // the sort value
       const float ve = p == 4 ? ph_curv : cvr[u];     // cloudCurvature[ind]
       const int w = in ? ind - ws : 0;
-      const bool e = in && wpick[w] == 0 && (edge ? (ve > c.edge_thr && wgnd[w] == 0) : (ve < c.surf_thr && wgnd[w] == 1));
+      const int fg = in ? (wflag[w] & 0xC0) : 0x80;  // picked | ground
+      const bool e = in && (edge ? (fg == 0 && ve > c.edge_thr) : (fg == 0x40 && ve < c.surf_thr));
       const unsigned long long m = __ballot(e);
       int wb = 0;
       if (lane_id() == 0 && m) wb = atomicAdd(&s_cnt, (int)__popcll(m));
-      wb = __shfl(wb, 0, 64);
+      wb = __builtin_amdgcn_readlane(wb, 0);
       if (e) key[wb + __popcll(m & ((1ull << lane_id()) - 1ull))] = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)ind;
     }
   };
@@ -578,7 +561,7 @@ __global__ __launch_bounds__(256, 4) void k_select_ring(DevCfg c, DevBufs d) {
   if (tid == 0) s_exact = 0;
   __syncthreads();
   // ---- edges: eligible entries visited in descending sorted order, the unsorted ep first ----
-  const bool epE = curv[ep] > c.edge_thr && wgnd[ep - ws] == 0;
+  const bool epE = curv[ep] > c.edge_thr && (wflag[ep - ws] & 0x40) == 0;
   const int e0 = epE ? 1 : 0;
   append(true);
   __syncthreads();
@@ -595,23 +578,23 @@ __global__ __launch_bounds__(256, 4) void k_select_ring(DevCfg c, DevBufs d) {
     if (tid < 64) {
       const int cnt = compact_sorted(true, edge_elig);
       auto order = [&](int t) { return t < e0 ? ep : (int)(uint32_t)key[cpos[t - e0]]; };
-      const int sel = greedy_wave(order, cnt + e0, ws, wpick, wreach, wlab, (int8_t)1, d.edge_tmp + base + sp);
+      const int sel = greedy_wave(order, cnt + e0, ws, wflag, wlab, (int8_t)1, d.edge_tmp + base + sp);
       if (tid == 0) { rc[i] = sel; s_cnt = 0; }
     }
   } else if (tid < 64) {
     auto order = [&](int t) { return t < e0 ? ep : (int)(uint32_t)key[n2 - 1 - (t - e0)]; };
-    const int cnt = greedy_wave(order, nE + e0, ws, wpick, wreach, wlab, (int8_t)1, d.edge_tmp + base + sp);
+    const int cnt = greedy_wave(order, nE + e0, ws, wflag, wlab, (int8_t)1, d.edge_tmp + base + sp);
     if (tid == 0) { rc[i] = cnt; s_cnt = 0; }
   }
   __syncthreads();
   if (c.dbg_phase <= 2) return;
   // ---- flats: eligible entries in ascending sorted order, the unsorted ep last ----
-  const bool epF = curv[ep] < c.surf_thr && wgnd[ep - ws] == 1;
+  const bool epF = curv[ep] < c.surf_thr && (wflag[ep - ws] & 0x40) != 0;
   if (s_exact) {
     if (tid < 64) {
       const int cnt = compact_sorted(false, flat_elig);
       auto order = [&](int t) { return t < cnt ? (int)(uint32_t)key[cpos[t]] : ep; };
-      const int sel = greedy_wave(order, cnt + (epF ? 1 : 0), ws, wpick, wreach, wlab, (int8_t)-1, d.flat_tmp + base + sp);
+      const int sel = greedy_wave(order, cnt + (epF ? 1 : 0), ws, wflag, wlab, (int8_t)-1, d.flat_tmp + base + sp);
       if (tid == 0) rc[H + i] = sel;
     }
   } else {
@@ -627,19 +610,19 @@ __global__ __launch_bounds__(256, 4) void k_select_ring(DevCfg c, DevBufs d) {
       if (tid < 64) {
         const int cnt = compact_sorted(false, flat_elig);
         auto order = [&](int t) { return t < cnt ? (int)(uint32_t)key[cpos[t]] : ep; };
-        const int sel = greedy_wave(order, cnt + (epF ? 1 : 0), ws, wpick, wreach, wlab, (int8_t)-1, d.flat_tmp + base + sp);
+        const int sel = greedy_wave(order, cnt + (epF ? 1 : 0), ws, wflag, wlab, (int8_t)-1, d.flat_tmp + base + sp);
         if (tid == 0) rc[H + i] = sel;
       }
     } else if (tid < 64) {
       auto order = [&](int t) { return t < nF ? (int)(uint32_t)key[t] : ep; };
-      const int cnt = greedy_wave(order, nF + (epF ? 1 : 0), ws, wpick, wreach, wlab, (int8_t)-1, d.flat_tmp + base + sp);
+      const int cnt = greedy_wave(order, nF + (epF ? 1 : 0), ws, wflag, wlab, (int8_t)-1, d.flat_tmp + base + sp);
       if (tid == 0) rc[H + i] = cnt;
     }
   }
   __syncthreads();
   if (c.dbg_phase <= 3) return;
   for (int t = tid; t < wn; t += nt) {
-    d.picked[base + ws + t] = wpick[t];
+    d.picked[base + ws + t] = (uint8_t)(wflag[t] >> 7);
     d.clabel[base + ws + t] = wlab[t];
   }
   // ---- less-flat candidates k in [sp, ep] with cloudLabel[k] <= 0 (FA:1262-1266) ----
@@ -698,16 +681,21 @@ __global__ __launch_bounds__(256, 4) void k_select_ring(DevCfg c, DevBufs d) {
   }
   const int mul1 = div[0], mul2 = div[0] * div[1];
   // voxel id of every candidate, in ring order (points of one voxel are mostly consecutive)
-  uint32_t* vk = win_raw;  // the window arrays are dead (barrier after the compaction above)
+  // (in key[]: dead after the greedy passes; every key[] write below comes after the barriers that
+  // end the vk[] reads, and a lane's own ids stay in vkr)
+  uint32_t* vk = reinterpret_cast<uint32_t*>(key);
+  uint32_t vkr[kLp];
 #pragma unroll
   for (int u = 0; u < kLp; ++u) {
     const int t = tid + u * 256;
+    vkr[u] = 0u;
     if (t >= L) continue;
     const float4 p = lpr[u];
     const int i0 = (int)(floorf(p.x * inv) - (float)minb[0]);
     const int i1 = (int)(floorf(p.y * inv) - (float)minb[1]);
     const int i2 = (int)(floorf(p.z * inv) - (float)minb[2]);
-    vk[t] = (uint32_t)(i0 + i1 * mul1 + i2 * mul2);
+    vkr[u] = (uint32_t)(i0 + i1 * mul1 + i2 * mul2);
+    vk[t] = vkr[u];
   }
   __syncthreads();
   __shared__ int scnt[kLp * 4 + 1];
@@ -718,10 +706,14 @@ __global__ __launch_bounds__(256, 4) void k_select_ring(DevCfg c, DevBufs d) {
     // LLSR_VOXEL_ORDER_PCL (llsr_set_voxel_order): std::sort(index_vector) by voxel id alone (PCL
     // 1.10 voxel_grid.hpp): equal ids keep the order libstdc++'s introsort leaves them in, and each
     // centroid sums its points in that order.
-    for (int t = tid; t < L; t += nt) key[t] = ((uint64_t)vk[t] << 32) | (uint32_t)t;
+#pragma unroll
+    for (int u = 0; u < kLp; ++u) {
+      const int t = tid + u * 256;
+      if (t < L) key[t] = ((uint64_t)vkr[u] << 32) | (uint32_t)t;
+    }
     __syncthreads();
     if (c.dbg_phase <= 5) return;
-    // Lp = rstart, Rp = the (dead) voxel-id words
+    // Lp = rstart, Rp = the (dead) window bytes
     // (dbg_phase 100: diagnostic re-launch without the depth limit, to time the heap-sort fallback)
     if (tid < 64)
       exact_introsort(key, L, rstart, reinterpret_cast<uint16_t*>(win_raw), stk, VoxLess{}, c.dbg_phase == 100 ? 1000 : -1);
@@ -781,7 +773,7 @@ __global__ __launch_bounds__(256, 4) void k_select_ring(DevCfg c, DevBufs d) {
 #pragma unroll
     for (int u = 0; u < kLp; ++u) {
       const int t = u * 256 + tid;
-      mR[u] = __ballot(t < L && (t == 0 || vk[t] != vk[t - 1]));
+      mR[u] = __ballot(t < L && (t == 0 || vkr[u] != vk[t - 1]));
       if (ln == 0) scnt[u * 4 + wv] = (int)__popcll(mR[u]);
     }
     slot_scan();
@@ -792,7 +784,7 @@ __global__ __launch_bounds__(256, 4) void k_select_ring(DevCfg c, DevBufs d) {
       const int t = u * 256 + tid;
       const int ro = scnt[u * 4 + wv] + (int)__popcll(mR[u] & ltm);
       rstart[ro] = (uint16_t)t;
-      key[ro] = ((uint64_t)vk[t] << 32) | (uint32_t)ro;
+      key[ro] = ((uint64_t)vkr[u] << 32) | (uint32_t)ro;
     }
     if (tid == 0) rstart[R] = (uint16_t)L;
     const int R2 = max(pow2_ceil(R), 64);
@@ -1080,7 +1072,7 @@ __device__ __forceinline__ void dbscan_merge(const DevCfg& c, const DevBufs& d, 
         word &= word - 1u;
         nb[pos++] = 32 * w + q;
       }
-      deg += __shfl(ex + cnt, 63, 64);
+      deg += __builtin_amdgcn_readlane(ex + cnt, 63);
     }
     i_in = __ballot(i_in) != 0ull;
     sync_();

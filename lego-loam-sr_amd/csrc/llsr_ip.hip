@@ -1060,8 +1060,8 @@ __global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
       unsigned long long pend = __ballot(root >= 0);
       while (pend) {
         const int leader = __ffsll((long long)pend) - 1;
-        const int lr = __shfl(root, leader, 64);
-        const int lrow = __shfl(row, leader, 64);
+        const int lr = __builtin_amdgcn_readlane(root, leader);  // leader is uniform
+        const int lrow = __builtin_amdgcn_readlane(row, leader);
         const unsigned long long grp = __ballot(root == lr) & pend;
         const unsigned long long same = __ballot(root == lr && cell != lr && row == lrow) & pend;
         if (l == leader) {
