@@ -166,6 +166,8 @@ int32_t llsr_process_scan(llsr_handle* h, const float* xyzi, int32_t n, llsr_sca
  * filled d_xyzi on the default stream must pass that stream (or synchronise) itself. Returns after
  * enqueue. Batches of one handle are ordered even across streams (each waits for the previous
  * one's completion event), because they share the slot buffers and the FA carry-over state.
+ * d_xyzi and d_offsets must stay valid and unchanged until the batch has completed: the kernels
+ * read them while they run.
  * Results stay in the handle until the next call. */
 int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const int64_t* d_offsets,
                            int32_t B, void* hip_stream);

@@ -271,7 +271,6 @@ static size_t layout(DevBufs& d, char* p0, int B, int H, int HW) {
   d.cell_pt = carve<int>(p, n);
   d.range = carve<float>(p, n);
   d.full = carve<float4>(p, n);
-  d.vis = carve<float>(p, n);
   d.ground = carve<int8_t>(p, n);
   d.label = carve<int>(p, n);
   d.near_pts = carve<float4>(p, n);

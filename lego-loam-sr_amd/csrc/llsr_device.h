@@ -48,8 +48,8 @@ struct DevBufs {
   float* orient;        // [B][4]
   int* cell_pt;         // [B][HW] raw point index or -1
   float* range;         // [B][HW]
-  float4* full;         // [B][HW] x,y,z, row + col/1e4
-  float* vis;           // [B][HW] raw intensity of the kept point
+  float4* full;         // [B][HW] the kept raw point (x, y, z, raw intensity); NaN, NaN, NaN, 0 where
+                        // empty. fullCloud's intensity row + col / 1e4 is derived (cell_intensity).
   int8_t* ground;       // [B][HW]
   int* label;           // [B][HW]
   float4* near_pts;     // [B][HW] near-ground cloud (w = cell index)
@@ -88,6 +88,12 @@ struct DevBufs {
 // DBSCAN adjacency capacity per scan (edge candidates); larger M falls back to on-the-fly rows.
 constexpr int kAdjCap = 2048;
 constexpr int kAdjWords = kAdjCap / 32;
+
+// fullCloud's intensity of cell (row i, col j): (float)(i + j / 10000.0) (IP:341); the double
+// division is a multiply by 1e-4 where both give the same float (tests/test_oracle.py)
+__device__ __forceinline__ float cell_intensity(int H, int W, int i, int j) {
+  return (float)((double)(float)i + (H <= 256 && W <= 8192 ? (double)(float)j * 1e-4 : (double)(float)j / 10000.0));
+}
 
 // ---- wave / block primitives (wave64) ------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }

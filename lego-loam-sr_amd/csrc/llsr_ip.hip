@@ -36,21 +36,27 @@ __device__ __forceinline__ int project_cell(const DevCfg& c, float4 p, float* ra
 // Certified fast path for project_cell. The cell depends on asinf/atan2f only through a truncated
 // (row) and a rounded (column) quotient, both monotone in the angle, so an approximation with a
 // known error bound decides the cell exactly unless the quotient lies within that bound of a
-// decision boundary; only then (and for |z/r| >= 0.5, zero / non-finite operands) the lane takes
-// the exact libm path. Row: asinf_ below 0.5 IS the fdlibm odd polynomial (same ops as asinf_),
-// its quotient by res_Y becomes a multiply by the reciprocal (|err| <= 2^-22 |q|; margin
-// 1e-5 |q| + 1e-6 around every non-zero integer, trunc maps (-1, 1) to 0). Column: atan2 from a
-// hardware reciprocal (<= 1 ulp) and a degree-15 odd minimax polynomial (3.7e-8 on [0, 1]) plus
-// the octant fix-ups: |ha - atan2f_| < 1e-6 rad (measured < 6e-7, tests/test_libm.py); the double
-// quotient (ha - pi/2) / res_X becomes a float multiply (|err| <= 2^-22 |q| + 3e-7 / res_X), and
-// the margin 4e-6 / res_X + 2.4e-7 |q| around every half-integer covers both with 2-4x to spare.
+// decision boundary; only then (and for |z/r| >= 0.5, zero / non-finite operands, a range within
+// 1 % of the 0.1 m cut) the lane takes the exact libm path.
+// Row: s = z / r from the hardware reciprocal square root (<= 1 ulp) and a multiply: within
+// 2.5 * 2^-23 |s| of the reference's correctly rounded sqrt and divide, so the angle within
+// 3.5e-7 |s| <= 1.75e-7 (|s| < 0.5, asin' <= 1.155); asinf_ below 0.5 IS the fdlibm odd polynomial
+// (same ops as asinf_); the quotient by res_Y is a multiply by the reciprocal (|err| <= 2^-22 |q|).
+// Margin around every non-zero integer: 1e-5 |q| + 1e-6 + 4e-7 / res_Y (trunc maps (-1, 1) to 0).
+// Column: atan2 from a hardware reciprocal (<= 1 ulp) and a degree-15 odd minimax polynomial (3.7e-8
+// on [0, 1]) plus the octant fix-ups: |ha - atan2f_| < 1e-6 rad (measured < 6e-7, tests/test_libm.py);
+// the double quotient (ha - pi/2) / res_X becomes a float multiply (|err| <= 2^-22 |q| + 3e-7 /
+// res_X), and the margin 4e-6 / res_X + 2.4e-7 |q| around every half-integer covers both with 2-4x
+// to spare. round(q) and the W / 2 offset are integer arithmetic for even W.
 // Bit-exact by construction; tests/test_gpu_projection_edges.py puts points on the boundaries.
+// Returns the row (>= 0) and *colp, or -1 (no cell); *ok = false: undecided, use project_cell.
 __device__ __forceinline__ int project_cell_fast(const DevCfg& c, float4 p, float invResY, float invResX,
-                                                 bool* ok) {
-  const float range = sqrt_(p.x * p.x + p.y * p.y + p.z * p.z);
-  const float s = p.z / range;
+                                                 bool* ok, int* colp) {
+  const float r2 = p.x * p.x + p.y * p.y + p.z * p.z;  // the reference's sqrt argument, same ops
+  const float s = p.z * __builtin_amdgcn_rsqf(r2);
   const uint32_t is = fbits(s) & 0x7fffffffu;
-  bool good = is < 0x3f000000u;  // |s| < 0.5 (false for NaN)
+  // |s| < 0.5 (false for NaN); range = fl(sqrt(r2)) vs 0.1 decided away from r2 in [0.0099, 0.0101]
+  bool good = is < 0x3f000000u && (r2 < 0.0099f || r2 > 0.0101f);
   const float p0 = 1.666675248e-1f, p1 = 7.495297643e-2f, p2 = 4.547037598e-2f,
               p3 = 2.417951451e-2f, p4 = 4.216630880e-2f;
   const float t2 = s * s;
@@ -58,7 +64,7 @@ __device__ __forceinline__ int project_cell_fast(const DevCfg& c, float4 p, floa
   const float va = is < 0x32000000u ? s : s + s * w;
   const float qr = (va + c.ip_angBottom) * invResY;
   const float rr = __builtin_rintf(qr);
-  good = good && (rr == 0.0f || fabsf(qr - rr) > 1e-5f * fabsf(qr) + 1e-6f);
+  good = good && (rr == 0.0f || fabsf(qr - rr) > 1e-5f * fabsf(qr) + 1e-6f + 4e-7f * invResY);
   const int row = (int)__builtin_truncf(qr);
   const float a = p.x, b = p.y;
   const float ax = fabsf(a), bx = fabsf(b);
@@ -85,22 +91,28 @@ __device__ __forceinline__ int project_cell_fast(const DevCfg& c, float4 p, floa
   const float fl = __builtin_floorf(qc);
   good = fabsf(qc - fl - 0.5f) > 4e-6f * invResX + 2.4e-7f * fabsf(qc);
   *ok = good;
-  int col = trunc_i32(-(double)(fl + 1.0f) + c.W * 0.5);  // round(qc) = fl + (qc - fl > 0.5)
-  if (qc - fl < 0.5f) col = trunc_i32(-(double)fl + c.W * 0.5);
+  const float rq = qc - fl < 0.5f ? fl : fl + 1.0f;  // round(qc) away from the half-integers
+  int col;
+  if ((c.W & 1) == 0) col = (c.W >> 1) - (int)rq;   // -round + W * 0.5, exact in integers
+  else col = trunc_i32(-(double)rq + c.W * 0.5);
   if (col >= c.W) col -= c.W;
-  if (col < 0 || col >= c.W || (double)range < 0.1) return -1;
-  return col + row * c.W;
+  if (col < 0 || col >= c.W || r2 < 0.0099f) return -1;  // (double)fl(sqrt(r2)) < 0.1
+  *colp = col;
+  return row;
 }
 
-// project_cell's result through the certified fast path, the exact libm path where it cannot decide
-__device__ __forceinline__ int project_cell_any(const DevCfg& c, float4 p, float invResY, float invResX) {
+// project_cell's (row, col) through the certified fast path, the exact libm path where it cannot
+// decide; returns the row or -1
+__device__ __forceinline__ int project_cell_any(const DevCfg& c, float4 p, float invResY, float invResX, int* colp) {
   bool ok;
-  int cell = project_cell_fast(c, p, invResY, invResX, &ok);
+  int row = project_cell_fast(c, p, invResY, invResX, &ok, colp);
   if (!ok) {
     float r;
-    cell = project_cell(c, p, &r);
+    const int cell = project_cell(c, p, &r);
+    row = cell < 0 ? -1 : cell / c.W;
+    if (cell >= 0) *colp = cell - row * c.W;
   }
-  return cell;
+  return row;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -128,11 +140,9 @@ __global__ __launch_bounds__(256) void k_project(DevCfg c, const float4* __restr
     ++npts;
     first = min(first, (int)i);
     last = max(last, (int)i);
-    const int cell = project_cell_any(c, p, 1.0f / c.ip_resY, 1.0f / c.ip_resX);
-    if (cell >= 0) {
-      const int row = cell / c.W, col = cell - row * c.W;
-      atomicMax(&d.ccl_a[(size_t)b * c.HW + (size_t)col * c.H + row], (int)i);
-    }
+    int col;
+    const int row = project_cell_any(c, p, 1.0f / c.ip_resY, 1.0f / c.ip_resX, &col);
+    if (row >= 0) atomicMax(&d.ccl_a[(size_t)b * c.HW + (size_t)col * c.H + row], (int)i);
   }
   __shared__ int red[3][4];
   npts = wave_reduce_add(npts);
@@ -193,20 +203,17 @@ __global__ __launch_bounds__(64) void k_gather_column(DevCfg c, const float4* __
     const int pi = colw[i];
     d.cell_pt[base + cell] = pi;
     float4 f;
-    float rng, vis;
+    float rng;
     if (pi >= 0) {
       const float4 p = pts[o0 + pi];
       rng = sqrt_(p.x * p.x + p.y * p.y + p.z * p.z);
-      f = make_float4(p.x, p.y, p.z, (float)((double)(float)i + (c.H <= 256 && c.W <= 8192 ? (double)(float)j * 1e-4 : (double)(float)j / 10000.0)));
-      vis = p.w;
+      f = make_float4(p.x, p.y, p.z, cell_intensity(c.H, c.W, i, j));
     } else {
       rng = FLT_MAX;
       f = make_float4(qnan, qnan, qnan, 0.0f);
-      vis = 0.0f;
     }
     d.range[base + cell] = rng;
-    d.full[base + cell] = f;
-    d.vis[base + cell] = vis;
+    d.full[base + cell] = pi >= 0 ? pts[o0 + pi] : make_float4(qnan, qnan, qnan, 0.0f);
     int8_t g;
     if (f.w == 0.0f) {
       g = -1;  // IP:535: NaN cells (and a real point at row 0, col 0) have intensity 0
@@ -235,11 +242,12 @@ __global__ __launch_bounds__(64) void k_gather_column(DevCfg c, const float4* __
 
 // ---------------------------------------------------------------------------------------------
 // K1+K2 fused for range images that fit LDS (H <= 16, H*W <= 32000, e.g. VLP-16): one workgroup per scan.
-// Pass 1 projects every raw point (coalesced reads) and resolves IP:337-347's serial "last writer
-// wins" with an LDS atomicMax of the raw index per cell; pass 2 re-reads the points and only each
-// cell's winner writes range / full_cloud / raw intensity; empty cells get the resetParameters
-// values (IP:170-179); pass 3 runs the per-column ground test + Filter (IP:524-629) on the cell
-// arrays. No global atomics, no gather of scattered input points.
+// The claim pass projects every raw point once (coalesced reads) and resolves IP:337-347's serial
+// "last writer wins" with an LDS atomicMax of the raw index per cell, each cell's winner writing its
+// range and its raw point (x, y, z, raw intensity: fullCloud with the intensity row + col / 1e4
+// derived where needed, cell_intensity); a sweep of the final winner table writes the cell ->
+// point map and the resetParameters values of empty cells (IP:170-179); the per-column ground test
+// + Filter (IP:524-629) reads the kept points back. No global atomics.
 // ---------------------------------------------------------------------------------------------
 // groundRemovalOurs' per-column test (IP:524-629) as a step over one column's state, so a lane can
 // carry two columns at once: their serial 16-row chains interleave (ILP) instead of running in two
@@ -275,9 +283,10 @@ __device__ __forceinline__ int8_t ground_step(const DevCfg& c, GndState& st, flo
   return g;
 }
 
-// columns j0 and j1 (j1 >= W: none), their cells loaded 8 rows at a time ahead of the tests
-__device__ __forceinline__ void ground_columns2(const DevCfg& c, const float4* __restrict__ full, int8_t* ground,
-                                                int j0, int j1) {
+// columns j0 and j1 (j1 >= W: none), their cells loaded 8 rows at a time ahead of the tests;
+// cellf(cell) = (x, y, z, w) with w == 0 exactly for the cells groundRemoval skips (IP:535)
+template <class CellF>
+__device__ __forceinline__ void ground_columns2(const DevCfg& c, CellF cellf, int8_t* ground, int j0, int j1) {
   GndState s0, s1;
   const bool has1 = j1 < c.W;
   constexpr int kR = 8;
@@ -286,8 +295,8 @@ __device__ __forceinline__ void ground_columns2(const DevCfg& c, const float4* _
 #pragma unroll
     for (int u = 0; u < kR; ++u) {
       const bool in = i0 + u < c.H;
-      f0[u] = in ? full[j0 + (i0 + u) * c.W] : make_float4(0.f, 0.f, 0.f, 0.f);
-      f1[u] = in && has1 ? full[j1 + (i0 + u) * c.W] : make_float4(0.f, 0.f, 0.f, 0.f);
+      f0[u] = in ? cellf(j0 + (i0 + u) * c.W) : make_float4(0.f, 0.f, 0.f, 0.f);
+      f1[u] = in && has1 ? cellf(j1 + (i0 + u) * c.W) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int u = 0; u < kR; ++u) {
@@ -319,45 +328,37 @@ __global__ __launch_bounds__(1024) void k_project_fused(DevCfg c, const float4* 
   const float invResY = 1.0f / c.ip_resY, invResX = 1.0f / c.ip_resX;
   const float qnan = __builtin_nanf("");
   const int W = c.W;
-  // (float)(row + (double)col / 1e4) == (float)(row + col * 1e-4) for every row < 256, col < 8192
-  // (tests/test_oracle.py checks all of them), so the double division becomes a multiply there.
-  const bool mulInt = c.H <= 256 && W <= 8192;
   // Chunks of nt raw points in DESCENDING index order. "Last writer wins" (IP:337-347) makes a
   // cell's point the largest raw index mapped to it, so once a chunk has raised the LDS winner table
   // (atomicMax) a cell holding an index of THIS chunk is final: no later-processed (lower-index)
-  // point can take it. Its winner emits the cell's range / full cloud / intensity / point index from
-  // registers, so the raw points are read from HBM exactly once. A firing-ordered stream (Velodyne:
+  // point can take it. Its winner emits the cell's range and point from registers, so the claim
+  // pass reads the raw points from HBM exactly once. A firing-ordered stream (Velodyne:
   // the rings of one azimuth are consecutive) puts a chunk's cells in a band of ~nt / H columns:
   // winners inside the 64-column band starting at the chunk's smallest column go through an LDS
   // tile written out row by row (full lines); any other winner (wrap-around, unordered input)
   // writes its cell directly.
-  // Chunks of kU * nt points (kU per lane, loads of the next chunk issued before this chunk's
-  // barriers); the tile holds the band's full cloud and intensity, and "won in this chunk" is read
-  // back from the winner table (index within the chunk's range).
+  // Chunks of kU * nt points (kU per lane, the loads of the next two chunks in flight during this
+  // chunk's barriers); the tile holds the band's points, and "won in this chunk" is read back from
+  // the winner table (index within the chunk's range).
   constexpr int kU = 2, kTC = 128, kTP = kTC + 1;  // padded rows
   __shared__ float4 tfull[16 * kTP];
-  __shared__ float tvis[16 * kTP];
   __shared__ int s_cmin[2];
   if (tid < 2) s_cmin[tid] = INT_MAX;
   const int C = kU * nt;
   const int nch = (n + C - 1) / C;
-  float4 pn[kU];
-  auto load = [&](int ch) {
+  // two chunks of loads in flight (buffers A / B alternate, so no register copy waits on a load
+  // that is still outstanding)
+  float4 pa[kU], pb[kU];
+  auto load = [&](float4 (&buf)[kU], int ch) {
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int i = ch * C + u * nt + tid;
-      pn[u] = (ch >= 0 && i < n) ? pts[o0 + i] : make_float4(qnan, 0.f, 0.f, 0.f);
+      buf[u] = (ch >= 0 && i < n) ? pts[o0 + i] : make_float4(qnan, 0.f, 0.f, 0.f);
     }
   };
-  load(nch - 1);
-  __syncthreads();
-  for (int ch = nch - 1; ch >= 0; --ch) {
+  auto chunk = [&](int ch, const float4 (&pp)[kU]) {
     const int par = ch & 1;
     const int lo = ch * C, hi = lo + C;  // this chunk's raw index range
-    float4 pp[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) pp[u] = pn[u];
-    load(ch - 1);  // in flight during this chunk
     if (tid == 0) s_cmin[par ^ 1] = INT_MAX;  // the next chunk's
     int cell[kU], row[kU], col[kU];
     int cm = INT_MAX;
@@ -371,12 +372,14 @@ __global__ __launch_bounds__(1024) void k_project_fused(DevCfg c, const float4* 
       ++nfin;
       first = i < first ? i : first;
       last = i > last ? i : last;
-      cell[u] = project_cell_any(c, pp[u], invResY, invResX);
-      if (cell[u] >= 0) {
+      int cc;
+      const int rw = project_cell_any(c, pp[u], invResY, invResX, &cc);
+      if (rw >= 0) {
+        cell[u] = cc + rw * W;
         atomicMax(&cidx[cell[u]], i);
-        row[u] = cell[u] / W;
-        col[u] = cell[u] - row[u] * W;
-        cm = col[u] < cm ? col[u] : cm;
+        row[u] = rw;
+        col[u] = cc;
+        cm = cc < cm ? cc : cm;
       }
     }
     cm = wave_reduce_min(cm);
@@ -388,18 +391,11 @@ __global__ __launch_bounds__(1024) void k_project_fused(DevCfg c, const float4* 
       const int i = lo + u * nt + tid;
       if (cell[u] < 0 || cidx[cell[u]] != i) continue;
       const float4 p = pp[u];
-      const double dc = mulInt ? (double)(float)col[u] * 1e-4 : (double)(float)col[u] / 10000.0;
-      const float4 f = make_float4(p.x, p.y, p.z, (float)((double)(float)row[u] + dc));
       if (col[u] - c0 < kTC) {
-        const int t = row[u] * kTP + (col[u] - c0);
-        tfull[t] = f;
-        tvis[t] = p.w;
+        tfull[row[u] * kTP + (col[u] - c0)] = p;
       } else {
-        const size_t q = base + cell[u];
-        d.cell_pt[q] = i;
-        d.range[q] = sqrt_(p.x * p.x + p.y * p.y + p.z * p.z);
-        d.full[q] = f;
-        d.vis[q] = p.w;
+        d.range[base + cell[u]] = sqrt_(p.x * p.x + p.y * p.y + p.z * p.z);
+        d.full[base + cell[u]] = p;
       }
     }
     __syncthreads();
@@ -409,16 +405,28 @@ __global__ __launch_bounds__(1024) void k_project_fused(DevCfg c, const float4* 
         if (tcol >= W) continue;
         const int wpi = cidx[trow * W + tcol];
         if (wpi < lo || wpi >= hi) continue;
-        const int tt = trow * kTP + ck;
+        const float4 f = tfull[trow * kTP + ck];
         const size_t q = base + (size_t)trow * W + tcol;
-        const float4 f = tfull[tt];
-        d.cell_pt[q] = wpi;
         d.range[q] = sqrt_(f.x * f.x + f.y * f.y + f.z * f.z);
         d.full[q] = f;
-        d.vis[q] = tvis[tt];
       }
     }
     __syncthreads();
+  };
+  load(pa, nch - 1);
+  load(pb, nch - 2);
+  __syncthreads();
+  for (int ch = nch - 1; ch >= 0; ch -= 2) {
+    float4 pp[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) pp[u] = pa[u];
+    load(pa, ch - 2);
+    chunk(ch, pp);
+    if (ch == 0) break;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) pp[u] = pb[u];
+    load(pb, ch - 3);
+    chunk(ch - 1, pp);
   }
   nfin = block_reduce_add(nfin, tmp);
   first = block_reduce_min(first, tmp);
@@ -430,17 +438,25 @@ __global__ __launch_bounds__(1024) void k_project_fused(DevCfg c, const float4* 
     cnt[C_LAST] = last;
   }
   if (c.dbg_phase <= 0) return;
-  // cells no point reached keep the resetParameters values (IP:170-179)
+  // the cell -> point map from the final winner table; cells no point reached keep the
+  // resetParameters range (IP:170-179)
   for (int q = tid; q < HW; q += nt) {
-    if (cidx[q] >= 0) continue;
-    d.cell_pt[base + q] = -1;
-    d.range[base + q] = FLT_MAX;
-    d.full[base + q] = make_float4(qnan, qnan, qnan, 0.0f);
-    d.vis[base + q] = 0.0f;
+    const int w = cidx[q];
+    d.cell_pt[base + q] = w;
+    if (w < 0) {
+      d.range[base + q] = FLT_MAX;
+      d.full[base + q] = make_float4(qnan, qnan, qnan, 0.0f);
+    }
   }
   __syncthreads();
   if (c.dbg_phase <= 1) return;
-  for (int j = tid; j < c.W; j += 2 * nt) ground_columns2(c, d.full + base, d.ground + base, j, j + nt);
+  // the column ground test on the winners' points (w == 0: empty, or the point of cell (0, 0))
+  const float4* full = d.full + base;
+  auto cellf = [&](int q) {
+    const float4 p = full[q];
+    return make_float4(p.x, p.y, p.z, (cidx[q] < 0 || q == 0) ? 0.0f : 1.0f);
+  };
+  for (int j = tid; j < c.W; j += 2 * nt) ground_columns2(c, cellf, d.ground + base, j, j + nt);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -830,8 +846,7 @@ __global__ __launch_bounds__(1024) void k_ground_elev_ransac(DevCfg c, DevBufs d
       if ((double)ransac_dist(cf, q) < 0.5) {
         ++ninl;
         const int cell = (int)q.w;
-        const float4 p = full[cell];
-        const float depth = sqrt_(p.x * p.x + p.y * p.y);
+        const float depth = sqrt_(q.x * q.x + q.y * q.y);  // the near cloud holds the cell's x, y, z
         if ((double)depth <= 5) g[cell] = 1;
       }
     }
@@ -1184,9 +1199,12 @@ __global__ __launch_bounds__(1024) void k_segment(DevCfg c, const float4* __rest
 #pragma unroll
     for (int u = 0; u < kC; ++u) {
       if (kk[u] == 0) continue;
-      const size_t q = base + t0 + u * nt + tid;
-      f[u] = d.full[q];
-      vs[u] = d.vis[q];
+      const int cell = t0 + u * nt + tid;
+      const size_t q = base + cell;
+      const float4 p = d.full[q];
+      const int ci = cell / W;
+      f[u] = make_float4(p.x, p.y, p.z, cell_intensity(H, W, ci, cell - ci * W));
+      vs[u] = p.w;
       rg[u] = kk[u] == 1 ? d.range[q] : 0.0f;
     }
     if (t0 + kC * nt < HW) load_kind(t0 + kC * nt);
