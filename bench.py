@@ -462,7 +462,7 @@ def odometry_leg(dev, lidar: str, B: int, seqs: int, frames: int, steps: int, wa
     lm_ms = st["lm_ms"] / max(1, st["batches"])
     N = float(cnt[:, 0].sum())
     proj_ms = kt["k_project"] + kt["k_gather_column"]
-    bpc_proj = 20 * N + (24 + 4 + 1) * float(H * W * B)
+    bpc_proj = 20 * N + (24 + 1) * float(H * W * B)
     def roof(kname, nbytes, ms, note):
         a = nbytes / (ms * 1e-3) / 1e9
         return {"bound": "hbm", "kernel": kname, "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -482,8 +482,8 @@ def odometry_leg(dev, lidar: str, B: int, seqs: int, frames: int, steps: int, wa
                                 "bytes per launch"),
                          "traffic": lm_traffic("k_s2s_lm", B, "odometry " + lidar)},
            "roofline_projection": roof("k_project" if not hdl else "k_project+k_gather_column", bpc_proj, proj_ms,
-                                       "SURVEY 8(d) B_pc projection part 20 N + 24 HW (+ 5 HW raw intensity "
-                                       "and ground) over the projection kernels"),
+                                       "SURVEY 8(d) B_pc projection part 20 N + 24 HW (+ 1 HW ground) "
+                                       "over the projection kernels"),
            "kernels_ms_per_step": {**{k: round(v, 4) for k, v in kt.items()},
                                    "s2s_grid_build": round(st["grid_ms"] / max(1, st["batches"]), 4),
                                    "k_s2s_lm": round(lm_ms, 4)},
@@ -888,9 +888,10 @@ def main():
         per["k_gather_column"] = 0.0
     # SURVEY.md 8(d) B_pc: 20 N + 24 HW for the projection (each input point read once and its index
     # scattered; range, XYZI and cell->point index written per cell) + 29 S for the curvature; the
-    # fused kernel's other outputs (raw intensity 4 B, ground byte 1 B per cell) are credited too.
+    # fused kernel's other output (the ground byte per cell) is credited too; the per-cell XYZI keeps
+    # the raw intensity in w (fullCloud's row + col / 1e4 is derived where needed).
     # Re-reads (the winners' points gathered again) are not algorithmic: they show up in `traffic`.
-    bpc_proj = 20 * csum["N"] + (24 + 4 + 1) * HWB
+    bpc_proj = 20 * csum["N"] + (24 + 1) * HWB
     bpc_curv = 29 * csum["S"]
     dom = max((k for k in ktimes if k != "init"), key=lambda k: ktimes[k])
     total_scans = B * args.steps * world
@@ -930,8 +931,8 @@ def main():
 
     proj_ms = ktimes["k_project"] + (0.0 if fused else ktimes["k_gather_column"])
     tp = traffic_of("k_project")
-    roof_proj = roofline("k_project", bpc_proj, proj_ms, note="B_pc projection part: 20 N + 24 HW (+ 5 HW "
-                         "raw intensity and ground outputs); traffic = PMC bytes incl. the winners' re-read")
+    roof_proj = roofline("k_project", bpc_proj, proj_ms, note="B_pc projection part: 20 N + 24 HW (+ 1 HW "
+                         "ground output); traffic = PMC bytes incl. the ground pass's read of the kept points")
     tc = traffic_of("k_fa_points")
     roof_pc = roofline("k_project+k_fa_points", bpc_proj + bpc_curv, proj_ms + ktimes["k_fa_points"],
                        traffic=(tp + tc) if (tp is not None and tc is not None) else None,
