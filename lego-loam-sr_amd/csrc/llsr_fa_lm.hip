@@ -22,6 +22,7 @@
 
 #include <climits>
 #include <cstdint>
+#include <type_traits>
 
 #include "llsr_device.h"
 #include "llsr_eigen.h"
@@ -417,8 +418,11 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
     int* idx = a.idx + (size_t)p * capq * 3;
     float4* grows = a.rows + (size_t)p * capq;
     uint8_t* gvalid = a.valid + (size_t)p * capq;
-    for (int phase = 0; phase < 2; ++phase) {  // 0: surf (FA:2508-2516), 1: corner (FA:2519-2527)
-      const bool surf = phase == 0;
+    // the two phases as two instantiations of one body (0: surf, FA:2508-2516; 1: corner,
+    // FA:2519-2527), so each keeps only its own Jacobian constants live (the kernel's VGPR peak)
+    auto run_phase = [&](auto tag) {
+      constexpr bool surf = decltype(tag)::value;
+      const int phase = surf ? 0 : 1;
       const float4* qry = surf ? a.flat + f0 : a.sharp + ms0;
       const int Q = surf ? F : Ms;
       // the rows of this phase: LDS when they fit (phase B re-reads them serially every iteration)
@@ -433,9 +437,9 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
         float tl[6];
         for (int k = 0; k < 6; ++k) tl[k] = t[k];
         // the Jacobian constants depend only on transformCur: once per iteration, not per query
-        JacSurf js;
-        JacCorner jc;
-        if (surf) js = JacSurf(tl);
+        [[maybe_unused]] JacSurf js;
+        [[maybe_unused]] JacCorner jc;
+        if constexpr (surf) js = JacSurf(tl);
         else jc = JacCorner(tl);
         const bool knn = it % 5 == 0;
         // the ring-constrained tripod search around a found nearest neighbour (FA:1588-1647 /
@@ -538,7 +542,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
           const int* ix = idx + 3 * q;
           float4 row = make_float4(0.f, 0.f, 0.f, 0.f);  // no correspondence: adds exact zeros
           bool valid = false;
-          if (surf) {
+          if constexpr (surf) {
             if (ix[1] >= 0 && ix[2] >= 0) {
               const float4 t1 = sl[ix[0]], t2 = sl[ix[1]], t3 = sl[ix[2]];
               float pa = (t2.y - t1.y) * (t3.z - t1.z) - (t3.y - t1.y) * (t2.z - t1.z);
@@ -559,7 +563,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
                 valid = true;
               }
             }
-          } else if (ix[1] >= 0) {
+          } else if (ix[1] >= 0) {  // corner
             float4 t1, t2;
             if (corner_lds) { t1 = lcl[ix[0]]; t2 = lcl[ix[1]]; }
             else { t1 = clg[ix[0]]; t2 = clg[ix[1]]; }
@@ -740,7 +744,9 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
       }
       if (tid == 0) iters[phase] = it;
       __syncthreads();
-    }
+    };
+    run_phase(std::true_type{});
+    run_phase(std::false_type{});
   }
   if (tid == 0) {
     llsr_s2s_report& r = a.report[p];
