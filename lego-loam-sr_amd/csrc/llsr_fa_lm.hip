@@ -352,6 +352,55 @@ struct JacCorner {
 
 }  // namespace
 
+// Phase C of one iteration (thread 0): ColPivHouseholderQR solve, the iteration-0 degeneracy test
+// and matP, the projection, pose update, NaN reset and stop test (FA:1915-2009 / 2064-2142).
+// Not inlined: the kernel's register allocation then does not carry the solver's temporaries
+// (its peak sat here), and the call runs once per iteration on one lane.
+__device__ __noinline__ int s2s_solve_step(float* t, float* matP, const float* sums, int* isDeg, int it, bool surf) {
+  float AtA[9], AtB[3], X[3];
+  for (int k = 0; k < 9; ++k) AtA[k] = sums[k];  // lane r + 3c -> column-major (r, c)
+  for (int k = 0; k < 3; ++k) AtB[k] = sums[9 + k];
+  llsr_eigen::colpiv_qr_solve<3, 3>(AtA, AtB, X);
+  if (it == 0) {
+    float E[3], V[9], V2[9];
+    llsr_eigen::eig3(AtA, E, V);
+    for (int k = 0; k < 9; ++k) V2[k] = V[k];
+    int deg = 0;
+    for (int i = 2; i >= 0; --i) {
+      if (E[i] < 10) {
+        for (int j = 0; j < 3; ++j) V2[i + 3 * j] = 0;
+        deg = 1;
+      } else {
+        break;
+      }
+    }
+    *isDeg = deg;
+    float Vi[9];
+    llsr_eigen::inverse3(V, Vi);         // matV.inverse(): cofactors (FA:1983 / 2118)
+    llsr_eigen::prod33(Vi, V2, matP);    // matP = matV.inverse() * matV2
+  }
+  if (*isDeg) {  // matX = matP * matX2 (FA:1986-1990 / 2121-2125)
+    const float X2[3] = {X[0], X[1], X[2]};
+    llsr_eigen::prod31(matP, X2, X);
+  }
+  const float r2d = (float)(180.0 / 3.14159265358979323846);  // FA:56
+  double dR, dT;
+  if (surf) {
+    t[0] += X[0]; t[2] += X[1]; t[4] += X[2];
+    const double e0 = (double)(r2d * X[0]), e1 = (double)(r2d * X[1]), e2 = (double)(X[2] * 100);
+    dR = (double)(float)sqrt(e0 * e0 + e1 * e1);
+    dT = (double)(float)sqrt(e2 * e2);
+  } else {
+    t[1] += X[0]; t[3] += X[1]; t[5] += X[2];
+    const double e0 = (double)(r2d * X[0]), e1 = (double)(X[1] * 100), e2 = (double)(X[2] * 100);
+    dR = (double)(float)sqrt(e0 * e0);
+    dT = (double)(float)sqrt(e1 * e1 + e2 * e2);
+  }
+  for (int k = 0; k < 6; ++k)
+    if (t[k] != t[k]) t[k] = 0;
+  return (dR < 0.1 && dT < 0.1) ? 1 : 0;
+}
+
 // Diagnostic build only (make prof -> libllsr_prof.so): thread 0 accumulates the wall clock of
 // each phase and the report's transform_cur carries {A with kNN, A, B, C} in 10 ns ticks.
 #ifdef LLSR_S2S_PROF
@@ -693,50 +742,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
           const int cnt = nvalid;
           nvalid = 0;  // counted again by the next phase A (after the end-of-iteration barrier)
           n_corr[phase] = cnt;
-          if (cnt >= 10) {  // FA:2514 / 2525
-            float AtA[9], AtB[3], X[3];
-            for (int k = 0; k < 9; ++k) AtA[k] = sums[k];  // lane r + 3c -> column-major (r, c)
-            for (int k = 0; k < 3; ++k) AtB[k] = sums[9 + k];
-            llsr_eigen::colpiv_qr_solve<3, 3>(AtA, AtB, X);
-            if (it == 0) {
-              float E[3], V[9], V2[9];
-              llsr_eigen::eig3(AtA, E, V);
-              for (int k = 0; k < 9; ++k) V2[k] = V[k];
-              int deg = 0;
-              for (int i = 2; i >= 0; --i) {
-                if (E[i] < 10) {
-                  for (int j = 0; j < 3; ++j) V2[i + 3 * j] = 0;
-                  deg = 1;
-                } else {
-                  break;
-                }
-              }
-              isDeg = deg;
-              float Vi[9];
-              llsr_eigen::inverse3(V, Vi);         // matV.inverse(): cofactors (FA:1983 / 2118)
-              llsr_eigen::prod33(Vi, V2, matP);    // matP = matV.inverse() * matV2
-            }
-            if (isDeg) {  // matX = matP * matX2 (FA:1986-1990 / 2121-2125)
-              const float X2[3] = {X[0], X[1], X[2]};
-              llsr_eigen::prod31(matP, X2, X);
-            }
-            const float r2d = (float)(180.0 / 3.14159265358979323846);  // FA:56
-            double dR, dT;
-            if (surf) {
-              t[0] += X[0]; t[2] += X[1]; t[4] += X[2];
-              const double e0 = (double)(r2d * X[0]), e1 = (double)(r2d * X[1]), e2 = (double)(X[2] * 100);
-              dR = (double)(float)sqrt(e0 * e0 + e1 * e1);
-              dT = (double)(float)sqrt(e2 * e2);
-            } else {
-              t[1] += X[0]; t[3] += X[1]; t[5] += X[2];
-              const double e0 = (double)(r2d * X[0]), e1 = (double)(X[1] * 100), e2 = (double)(X[2] * 100);
-              dR = (double)(float)sqrt(e0 * e0);
-              dT = (double)(float)sqrt(e1 * e1 + e2 * e2);
-            }
-            for (int k = 0; k < 6; ++k)
-              if (t[k] != t[k]) t[k] = 0;
-            stop = (dR < 0.1 && dT < 0.1) ? 1 : 0;
-          }
+          if (cnt >= 10) stop = s2s_solve_step(t, matP, sums, &isDeg, it, surf);  // FA:2514 / 2525
         }
         __syncthreads();
         LLSR_STAMP(tC);
