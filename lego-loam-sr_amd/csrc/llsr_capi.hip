@@ -161,6 +161,10 @@ struct llsr_handle {
 
 // The fused projection keeps the winning raw index per cell in LDS (k_project_fused).
 static int fused_lds(const DevCfg& c) { return c.HW * (int)sizeof(int); }
+// k_label<true>'s dynamic LDS: the parent word and the edge-bit byte of every cell (HW <= 32000:
+// <= 160000 B)
+static int label_lds(const DevCfg& c) { return c.HW * (int)(sizeof(int) + 1); }
+
 static int label_band_lds(const DevCfg& c) { return c.lbl_band * c.W * (int)sizeof(int); }
 static bool use_fused(const llsr_handle* h) { return h->dc.ccl_lds != 0; }
 
@@ -361,7 +365,7 @@ extern "C" int32_t llsr_create(const llsr_config* cfg, int32_t hip_device, int32
   }
   if (h->dc.ccl_lds) {
     if (hipFuncSetAttribute((const void*)k_label<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            h->dc.HW * (int)sizeof(int)) != hipSuccess ||
+                            label_lds(h->dc)) != hipSuccess ||
         hipFuncSetAttribute((const void*)k_project_fused, hipFuncAttributeMaxDynamicSharedMemorySize,
                             fused_lds(h->dc)) != hipSuccess) {
       llsr_destroy(h);
@@ -517,7 +521,7 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   k_ground_elev_ransac<<<B, 1024, 0, s>>>(c, h->d);
   mark();
   if (c.ccl_lds)
-    k_label<true><<<B, 1024, c.HW * sizeof(int), s>>>(c, h->d);
+    k_label<true><<<B, 1024, label_lds(c), s>>>(c, h->d);
   else
     k_label<false><<<B, 1024, label_band_lds(c), s>>>(c, h->d);
   mark();
@@ -652,7 +656,7 @@ extern "C" float llsr_debug_phase_ms(llsr_handle* h, int32_t k, int32_t phase, i
       case 7: k_fa_points<<<B, 512, 0, s>>>(c, h->d); break;
       case 6: k_segment<<<B, 1024, 0, s>>>(c, nullptr, nullptr, h->d); break;
       case 5:
-        if (c.ccl_lds) k_label<true><<<B, 1024, c.HW * sizeof(int), s>>>(c, h->d);
+        if (c.ccl_lds) k_label<true><<<B, 1024, label_lds(c), s>>>(c, h->d);
         else k_label<false><<<B, 1024, label_band_lds(c), s>>>(c, h->d);
         break;
       case 4: k_ground_elev_ransac<<<B, 1024, 0, s>>>(c, h->d); break;

@@ -925,23 +925,58 @@ __global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
   LdsAcc P{kLds ? lds_parent : d.ccl_a + base};
 
   if constexpr (kLds) {
-    // label_mat init (IP:752-759): -1 for ground or empty, else 0 -> union-find singleton
-    for (int cell = tid; cell < HW; cell += nt) {
-      const bool l0 = !(g[cell] == 1 || rng[cell] == FLT_MAX);
-      P.st(cell, l0 ? cell : -1);
+    // label_mat init (IP:752-759): -1 for ground or empty, else 0 -> union-find singleton; and the
+    // BFS edge test of every cell with its right (wrapping, IP:884-886) and lower neighbour as two
+    // bits in LDS (ebits, after the parent words), from ranges loaded kE cells per lane at once —
+    // the union pass then reads LDS only (its global loads sat behind data-dependent branches)
+    uint8_t* ebits = reinterpret_cast<uint8_t*>(lds_parent + HW);
+    constexpr int kE = 4;
+    for (int t0 = 0; t0 < HW; t0 += kE * nt) {
+      float r[kE], rr[kE], rd[kE];
+      int8_t gv[kE];
+#pragma unroll
+      for (int u = 0; u < kE; ++u) {
+        const int cell = t0 + u * nt + tid;
+        if (cell >= HW) continue;
+        const int i = cell / W, j = cell - i * W;
+        gv[u] = g[cell];
+        r[u] = rng[cell];
+        rr[u] = rng[(j + 1 < W) ? cell + 1 : cell + 1 - W];
+        rd[u] = i + 1 < H ? rng[cell + W] : FLT_MAX;
+      }
+      // A wave holds 64 consecutive cells of slot u: the right edges between neighbours of one row
+      // inside the wave are resolved here, each cell pointing straight at the first cell of its
+      // linked run (the run's smallest index, so the union-find invariant "root = smallest cell"
+      // holds); only the wave's last right edge, the row wrap and the down edges are left for the
+      // union pass.
+      const int ln = lane_id();
+#pragma unroll
+      for (int u = 0; u < kE; ++u) {
+        const int cell = t0 + u * nt + tid;
+        const bool in = cell < HW;
+        const int i = in ? cell / W : 0, j = in ? cell - i * W : 0;
+        const bool l0 = in && !(gv[u] == 1 || r[u] == FLT_MAX);
+        const bool er = in && seg_edge(c, r[u], rr[u], true);
+        const bool ed = in && i + 1 < H && seg_edge(c, r[u], rd[u], false);
+        const bool l0n = __shfl_down(l0 ? 1 : 0, 1, 64) != 0;  // the next lane's cell (j + 1 if j + 1 < W)
+        const bool link = er && l0 && l0n && ln < 63 && j + 1 < W;  // resolved in the wave
+        const unsigned long long lk = __ballot(link);
+        const unsigned long long heads = ~(lk << 1);                 // lane 0 always starts a run
+        const int head = 63 - __clzll((long long)(heads & ((2ull << ln) - 1ull)));
+        if (!in) continue;
+        P.st(cell, l0 ? cell - (ln - head) : -1);
+        ebits[cell] = (uint8_t)((er && !link ? 1 : 0) | (ed ? 2 : 0));
+      }
     }
     __syncthreads();
     if (c.dbg_phase <= 0) return;
     for (int cell = tid; cell < HW; cell += nt) {
-      if (P.ld(cell) < 0) continue;
+      const int e = ebits[cell];
+      if (e == 0 || P.ld(cell) < 0) continue;
       const int i = cell / W, j = cell - i * W;
-      const float r = rng[cell];
       const int right = (j + 1 < W) ? cell + 1 : cell + 1 - W;  // wrap (IP:884-886)
-      if (P.ld(right) >= 0 && seg_edge(c, r, rng[right], true)) uf_unite(P, cell, right);
-      if (i + 1 < H) {
-        const int down = cell + W;
-        if (P.ld(down) >= 0 && seg_edge(c, r, rng[down], false)) uf_unite(P, cell, down);
-      }
+      if ((e & 1) && P.ld(right) >= 0) uf_unite(P, cell, right);
+      if ((e & 2) && P.ld(cell + W) >= 0) uf_unite(P, cell, cell + W);
     }
     __syncthreads();
   } else {
