@@ -435,7 +435,8 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
   __shared__ uint8_t lvalid[kLdsRows];
   __shared__ uint16_t lvix[kLdsRows];  // phase B: the rows holding a correspondence, in order
   __shared__ float4 lcl[kLdsCorner];
-  __shared__ int fbq[kFbMax], nfb, nvalid;
+  __shared__ int fbq[kFbMax], nfb, nvalid, nrow;
+  __shared__ float bpart[5][12];  // phase B: per-depth-block AtA partial sums
   __shared__ float red_d[kMulti][kThreads / 64];
   __shared__ int red_i[kMulti][kThreads / 64];
   const CellGrid& gc = a.grids.g[0];
@@ -649,51 +650,84 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
         // block of kc rows (llsr_eigen::gemm_kc) is summed from zero and added to the result; below
         // N + 6 < 20 it is the lazy coefficient product, and matAt * matB always is (a sum that
         // starts from the first product). Rows without a correspondence are skipped.
-        if (Q <= kLdsRows && tid < 64) {
+        if (Q <= kLdsRows) {
           // rows in LDS: wave 0 lists the rows holding a correspondence (ballot compaction, order
-          // kept), then lanes 0..11 run their sums over that list with no per-row test
-          int N = 0;
-          for (int q0 = 0; q0 < Q; q0 += 64) {
-            const int q = q0 + tid;
-            const bool v = q < Q && lvalid[q] != 0;
-            const unsigned long long m = __ballot(v);
-            if (v) lvix[N + __popcll(m & ((1ull << tid) - 1ull))] = (uint16_t)q;
-            N += __popcll(m);
-          }
-          wave_sync_lds();
-          if (tid < 12) {
-            const int ra = tid < 9 ? tid % 3 : tid - 9, rb = tid < 9 ? tid / 3 : 3;
-            const float* rf = reinterpret_cast<const float*>(lrows);
-            const bool lazy = tid >= 9 || N + 6 < 20;
-            const int kc = lazy ? N : llsr_eigen::gemm_kc(N, 3, 3);
-            float tot = 0.0f, c = 0.0f;
-            for (int b0 = 0; b0 < N; b0 += kc) {
-              const int b1 = N - b0 < kc ? N : b0 + kc;
-              int i = b0;
-              if (lazy) {  // the coefficient product: starts from the first product
-                const int q = lvix[0];
-                c = rf[4 * q + ra] * rf[4 * q + rb];
-                i = 1;
-              } else {     // a GEMM depth block: summed from zero
-                c = 0.0f;
-              }
-              for (; i + 16 <= b1; i += 16) {
-                int qv[16];
-                float pv[16];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) qv[u] = 4 * lvix[i + u];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) pv[u] = rf[qv[u] + ra] * rf[qv[u] + rb];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) c = c + pv[u];
-              }
-              for (; i < b1; ++i) {
-                const int q = 4 * lvix[i];
-                c = c + rf[q + ra] * rf[q + rb];
-              }
-              if (!lazy) tot = tot + 1.0f * c;
+          // kept), the block moves them to the front of lrows in that order (stable, in place: a
+          // row only moves down, every read before the first write), then the sums read contiguous
+          // rows. Each GEMM depth block of AtA is its own lane (12 entries x blocks <= 64 lanes of
+          // wave 0), summed from zero; lanes 0..8 then add the blocks in order. AtB (lanes 9..11)
+          // and the lazy product are single chains over all rows.
+          if (tid < 64) {
+            int N = 0;
+            for (int q0 = 0; q0 < Q; q0 += 64) {
+              const int q = q0 + tid;
+              const bool v = q < Q && lvalid[q] != 0;
+              const unsigned long long m = __ballot(v);
+              if (v) lvix[N + __popcll(m & ((1ull << tid) - 1ull))] = (uint16_t)q;
+              N += __popcll(m);
             }
-            sums[tid] = lazy ? c : tot;
+            if (tid == 0) nrow = N;
+          }
+          __syncthreads();
+          const int N = nrow;
+          constexpr int kMv = (kLdsRows + kThreads - 1) / kThreads;
+          float4 mv[kMv];
+#pragma unroll
+          for (int u = 0; u < kMv; ++u) {
+            const int i = tid + u * kThreads;
+            if (i < N) mv[u] = lrows[lvix[i]];
+          }
+          __syncthreads();
+#pragma unroll
+          for (int u = 0; u < kMv; ++u) {
+            const int i = tid + u * kThreads;
+            if (i < N) lrows[i] = mv[u];
+          }
+          __syncthreads();
+          const float* rf = reinterpret_cast<const float*>(lrows);
+          const bool lazyAll = N + 6 < 20;
+          const int kc = lazyAll ? N : llsr_eigen::gemm_kc(N, 3, 3);
+          const int nblk = lazyAll || N == 0 ? 1 : (N + kc - 1) / kc;
+          if (tid < 64) {
+            // lane = entry (0..11) + 12 * block; AtB entries and the lazy product use block 0 only
+            const int e = tid % 12, blk = tid / 12;
+            const bool lazy = e >= 9 || lazyAll;
+            const bool act = blk < (lazy ? 1 : nblk) && 12 * nblk <= 64;
+            const int ra = e < 9 ? e % 3 : e - 9, rb = e < 9 ? e / 3 : 3;
+            float c = 0.0f;
+            if (act) {
+              const int b0 = lazy ? 0 : blk * kc, b1 = lazy ? N : min(N, b0 + kc);
+              int i = b0;
+              if (lazy && N > 0) { c = rf[ra] * rf[rb]; i = 1; }  // the coefficient product
+              for (; i + 8 <= b1; i += 8) {
+                float pv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) pv[u] = rf[4 * (i + u) + ra] * rf[4 * (i + u) + rb];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) c = c + pv[u];
+              }
+              for (; i < b1; ++i) c = c + rf[4 * i + ra] * rf[4 * i + rb];
+              if (!lazy) bpart[blk][e] = c;
+            }
+            wave_sync_lds();
+            if (tid < 12) {
+              if (lazy) {
+                sums[tid] = c;
+              } else if (12 * nblk <= 64) {
+                float tot = 0.0f;
+                for (int x = 0; x < nblk; ++x) tot = tot + 1.0f * bpart[x][tid];
+                sums[tid] = tot;
+              } else {  // more depth blocks than wave 0 has lanes for: one lane per entry
+                float tot = 0.0f;
+                for (int b0 = 0; b0 < N; b0 += kc) {
+                  const int b1 = min(N, b0 + kc);
+                  float cb = 0.0f;
+                  for (int i = b0; i < b1; ++i) cb = cb + rf[4 * i + ra] * rf[4 * i + rb];
+                  tot = tot + 1.0f * cb;
+                }
+                sums[tid] = tot;
+              }
+            }
           }
         } else if (Q > kLdsRows && tid < 12) {
           const int ra = tid < 9 ? tid % 3 : tid - 9, rb = tid < 9 ? tid / 3 : 3;
