@@ -1136,7 +1136,8 @@ extern "C" int32_t llsr_scan2scan_reserve(llsr_handle* h, int32_t P, int32_t ms,
   const size_t Tc = (size_t)1 << lc, Ts = (size_t)1 << ls;
   const size_t capq = (size_t)(ms > f ? ms : f) + 1;
   const size_t bytes = sizeof(CellSlot) * P * (Tc + Ts) + (sizeof(float4) + sizeof(int2)) * P * ((size_t)nc + ns) +
-                       sizeof(int) * 2 * P + (3 * sizeof(int) + sizeof(float4) + 1) * P * capq + 64 + 13 * 256;
+                       sizeof(int) * 2 * P + (3 * sizeof(int) + sizeof(float4) + 1) * P * capq +
+                       sizeof(float4) * 2 * P * (((size_t)ns + 7) / 8) + 64 + 14 * 256;
   if (hipMalloc(&m.pool, bytes) != hipSuccess) {
     m.pool = nullptr;
     m.P = 0;
@@ -1161,6 +1162,7 @@ extern "C" int32_t llsr_scan2scan_reserve(llsr_handle* h, int32_t P, int32_t ms,
   a.rows = carve<float4>(q, (size_t)P * capq);
   a.valid = carve<uint8_t>(q, (size_t)P * capq);
   a.error = carve<int>(q, 1);
+  a.sbox = carve<float4>(q, 2 * (size_t)P * (((size_t)ns + 7) / 8));
   a.cap_sharp = ms;
   a.cap_flat = f;
   if (!m.host_flag && hipHostMalloc((void**)&m.host_flag, sizeof(int)) != hipSuccess) {
@@ -1203,6 +1205,10 @@ extern "C" int32_t llsr_scan2scan_batch(llsr_handle* h, const llsr_s2s_batch* b,
   if (h->s2s_rec) HIP_OK(h, hipStreamWaitEvent(s, h->s2s_done, 0));  // shared buffers: after the last batch
   if (h->profiling) HIP_OK(h, hipEventRecord(m.p0, s));
   grid_build(a.grids, s);
+  {
+    const int nb = (m.ns + 7) / 8;
+    if (nb > 0) k_s2s_boxes<<<dim3((nb + 255) / 256, P), 256, 0, s>>>(a);
+  }
   if (h->profiling) HIP_OK(h, hipEventRecord(m.p1, s));
   // the small-LDS instantiation (4 workgroups per CU instead of 2) when every problem's queries
   // and corner-last cloud fit it (reserved capacities are the batch maxima)

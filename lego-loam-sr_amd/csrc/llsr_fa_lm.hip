@@ -235,9 +235,25 @@ __device__ void corner_finish(const float4* cl, int Nc, int fwd, float4 sel, flo
   i2 = b2;
 }
 
-// findCorrespondingSurfFeatures search (FA:1724-1809)
-__device__ void surf_finish(const float4* sl, int Ns, int fwd, float4 sel, float dist_sqr, int nn, float nd,
-                            int& i1, int& i2, int& i3) {
+// Squared-distance lower bound of q to a block's box, summed in sqdis' order: every point of the
+// block has fl(sqdis) >= this value (each rounded gap and square is monotone in its exact value),
+// so a block whose bound is >= the current minimum cannot change a strict '<' minimum. NaN
+// coordinates give NaN bounds, which never skip.
+__device__ __forceinline__ float box_lb(const float4& lo, const float4& hi, float4 q) {
+  const float gx = q.x < lo.x ? lo.x - q.x : (q.x > hi.x ? q.x - hi.x : 0.0f);
+  const float gy = q.y < lo.y ? lo.y - q.y : (q.y > hi.y ? q.y - hi.y : 0.0f);
+  const float gz = q.z < lo.z ? lo.z - q.z : (q.z > hi.z ? q.z - hi.z : 0.0f);
+  return gx * gx + gy * gy + gz * gz;
+}
+
+// findCorrespondingSurfFeatures search (FA:1724-1809): the up-walk visits nn+1 .. end-1 until a
+// ring above cs + 2.5, the down-walk nn-1 .. 0 until a ring below cs - 2.5, each point updating the
+// nearest same-ring (m2) or other-ring (m3) candidate with strict '<'. Whole 8-point blocks
+// (aligned to the box array) that contain no walk stop and whose box cannot beat the minimum they
+// would be tested against are skipped: the visits that remain are the walk's, in its order, so
+// the result is the serial loop's.
+__device__ void surf_finish(const float4* sl, const float4* box, int Ns, int fwd, float4 sel, float dist_sqr,
+                            int nn, float nd, int& i1, int& i2, int& i3) {
   i1 = -1;
   i2 = -1;
   i3 = -1;
@@ -247,22 +263,60 @@ __device__ void surf_finish(const float4* sl, int Ns, int fwd, float4 sel, float
   float m2 = dist_sqr, m3 = dist_sqr;
   int b2 = -1, b3 = -1;
   const int end = fwd < Ns ? fwd : Ns;
-  scan_up(sl, nn + 1, end, cs, [&](int j, float4 c, int rj) {
+  // the minimum a block of rings [rlo, rhi] is tested against: the up-walk tests rings <= cs
+  // against m2, the down-walk rings >= cs; the rest against m3
+  auto bound_up = [&](float rlo, float rhi) { return rhi <= (float)cs ? m2 : rlo > (float)cs ? m3 : fmaxf(m2, m3); };
+  auto bound_dn = [&](float rlo, float rhi) { return rlo >= (float)cs ? m2 : rhi < (float)cs ? m3 : fmaxf(m2, m3); };
+  // up-walk: single points up to the next block boundary, then blocks
+  int j = nn + 1;
+  bool stop = false;
+  auto up_visit = [&](int jj, float4 c) {
+    const int rj = trunc_i32(c.w);
+    if ((double)rj > (double)cs + 2.5) { stop = true; return; }
     const float d = sqdis(c, sel);
     if (rj <= cs) {
-      if (d < m2) { m2 = d; b2 = j; }
+      if (d < m2) { m2 = d; b2 = jj; }
     } else {
-      if (d < m3) { m3 = d; b3 = j; }
+      if (d < m3) { m3 = d; b3 = jj; }
     }
-  });
-  scan_down(sl, nn - 1, cs, [&](int j, float4 c, int rj) {
+  };
+  for (; j < end && (j & 7) && !stop; ++j) up_visit(j, sl[j]);
+  for (; j < end && !stop; j += kScan) {
+    if (j + kScan <= end) {
+      const float4 lo = box[2 * (j >> 3)], hi = box[2 * (j >> 3) + 1];
+      if ((double)(int)hi.w <= (double)cs + 2.5 && box_lb(lo, hi, sel) >= bound_up(lo.w, hi.w)) continue;
+    }
+    float4 c[kScan];
+#pragma unroll
+    for (int u = 0; u < kScan; ++u) c[u] = j + u < end ? sl[j + u] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < kScan; ++u)
+      if (!stop && j + u < end) up_visit(j + u, c[u]);
+  }
+  // down-walk: single points down to a block's last index, then blocks [j - 7, j]
+  j = nn - 1;
+  stop = false;
+  auto down_visit = [&](int jj, float4 c) {
+    const int rj = trunc_i32(c.w);
+    if ((double)rj < (double)cs - 2.5) { stop = true; return; }
     const float d = sqdis(c, sel);
     if (rj >= cs) {
-      if (d < m2) { m2 = d; b2 = j; }
+      if (d < m2) { m2 = d; b2 = jj; }
     } else {
-      if (d < m3) { m3 = d; b3 = j; }
+      if (d < m3) { m3 = d; b3 = jj; }
     }
-  });
+  };
+  for (; j >= 0 && (j & 7) != 7 && !stop; --j) down_visit(j, sl[j]);
+  for (; j >= 0 && !stop; j -= kScan) {
+    const float4 lo = box[2 * (j >> 3)], hi = box[2 * (j >> 3) + 1];  // block [j - 7, j]
+    if ((double)(int)lo.w >= (double)cs - 2.5 && box_lb(lo, hi, sel) >= bound_dn(lo.w, hi.w)) continue;
+    float4 c[kScan];
+#pragma unroll
+    for (int u = 0; u < kScan; ++u) c[u] = sl[j - u];
+#pragma unroll
+    for (int u = 0; u < kScan; ++u)
+      if (!stop) down_visit(j - u, c[u]);
+  }
   i2 = b2;
   i3 = b3;
 }
@@ -401,6 +455,28 @@ __device__ __noinline__ int s2s_solve_step(float* t, float* matP, const float* s
   return (dR < 0.1 && dT < 0.1) ? 1 : 0;
 }
 
+// k_s2s_boxes: per 8-point block of laserCloudSurfLast (index order), the box of its points and
+// the range of their rings (trunc of the intensity, as the walks read it).
+__global__ void k_s2s_boxes(S2SArgs a) {
+  const CellGrid& g = a.grids.g[1];
+  const int p = blockIdx.y;
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = g.count(p);
+  if (8 * k >= n) return;
+  const float4* pts = g.src + g.off[p];
+  float4 lo = make_float4(INFINITY, INFINITY, INFINITY, INFINITY);
+  float4 hi = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+  for (int j = 8 * k; j < 8 * k + 8 && j < n; ++j) {
+    const float4 c = pts[j];
+    const float r = (float)trunc_i32(c.w);
+    lo = make_float4(fminf(lo.x, c.x), fminf(lo.y, c.y), fminf(lo.z, c.z), fminf(lo.w, r));
+    hi = make_float4(fmaxf(hi.x, c.x), fmaxf(hi.y, c.y), fmaxf(hi.z, c.z), fmaxf(hi.w, r));
+  }
+  float4* b = a.sbox + ((size_t)p * ((g.cap + 7) / 8) + k) * 2;
+  b[0] = lo;
+  b[1] = hi;
+}
+
 // Diagnostic build only (make prof -> libllsr_prof.so): thread 0 accumulates the wall clock of
 // each phase and the report's transform_cur carries {A with kNN, A, B, C} in 10 ns ticks.
 #ifdef LLSR_S2S_PROF
@@ -464,6 +540,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
     if (corner_lds)  // visible to every thread after the barrier at the top of the first phase
       for (int k = tid; k < Nc; k += kThreads) lcl[k] = clg[k];
     const float4* sl = gs.src + gs.off[p];
+    const float4* sbox = a.sbox + (size_t)p * ((gs.cap + 7) / 8) * 2;
     const int capq = a.cap_sharp > a.cap_flat ? a.cap_sharp : a.cap_flat;
     int* idx = a.idx + (size_t)p * capq * 3;
     float4* grows = a.rows + (size_t)p * capq;
@@ -505,7 +582,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
         auto finish = [&](int q, float4 sel, int nn, float nd) {
           int i1, i2, i3 = -1;
           if (surf) {
-            surf_finish(sl, Ns, F, sel, a.dist_sqr, nn, nd, i1, i2, i3);
+            surf_finish(sl, sbox, Ns, F, sel, a.dist_sqr, nn, nd, i1, i2, i3);
           } else if (corner_lds) {  // LDS-typed accesses (a generic pointer would issue flat loads)
             corner_finish(lcl, Nc, Ms, sel, a.dist_sqr, nn, nd, i1, i2);
           } else {

@@ -21,7 +21,13 @@ struct S2SArgs {
   float4* rows;                // [P][max(cap_sharp, cap_flat)] Jacobian row (3) + b (0 without a correspondence)
   uint8_t* valid;              // [P][max(cap_sharp, cap_flat)] 1: the row holds a correspondence
   int* error;                  // capacity violations
+  float4* sbox;                // [P][ceil(cap / 8)][2] bounding boxes of 8-point blocks of laserCloudSurfLast
+                               // in index order: (min x, y, z, min ring), (max x, y, z, max ring)
 };
+
+// bounding boxes of the surf-last cloud's 8-point blocks (the tripod walks skip a block whose box
+// cannot hold a nearer point); grid (ceil(ceil(cap / 8) / 256), P), block 256
+__global__ void k_s2s_boxes(S2SArgs a);
 
 // threads per scan-to-scan workgroup (one workgroup per problem)
 constexpr int kS2SThreads = 512;  // measured: 256 -> 512 HDL-64E LM 39.3 -> 32.6 ms, VLP-16 9.1 -> 8.4 ms; 1024 slower on VLP-16
