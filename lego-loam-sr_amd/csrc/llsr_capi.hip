@@ -1137,7 +1137,7 @@ extern "C" int32_t llsr_scan2scan_reserve(llsr_handle* h, int32_t P, int32_t ms,
   const size_t capq = (size_t)(ms > f ? ms : f) + 1;
   const size_t bytes = sizeof(CellSlot) * P * (Tc + Ts) + (sizeof(float4) + sizeof(int2)) * P * ((size_t)nc + ns) +
                        sizeof(int) * 2 * P + (3 * sizeof(int) + sizeof(float4) + 1) * P * capq +
-                       sizeof(float4) * 2 * P * (((size_t)ns + 7) / 8) + 64 + 14 * 256;
+                       sizeof(float4) * 2 * P * (((size_t)ns + 7) / 8 + ((size_t)ns + 63) / 64) + 64 + 15 * 256;
   if (hipMalloc(&m.pool, bytes) != hipSuccess) {
     m.pool = nullptr;
     m.P = 0;
@@ -1163,6 +1163,8 @@ extern "C" int32_t llsr_scan2scan_reserve(llsr_handle* h, int32_t P, int32_t ms,
   a.valid = carve<uint8_t>(q, (size_t)P * capq);
   a.error = carve<int>(q, 1);
   a.sbox = carve<float4>(q, 2 * (size_t)P * (((size_t)ns + 7) / 8));
+  a.sbox2 = carve<float4>(q, 2 * (size_t)P * (((size_t)ns + 63) / 64));
+
   a.cap_sharp = ms;
   a.cap_flat = f;
   if (!m.host_flag && hipHostMalloc((void**)&m.host_flag, sizeof(int)) != hipSuccess) {

@@ -85,11 +85,22 @@ __device__ bool nn1_shells(const CellGrid& g, int p, float4 q, float dist_sqr, i
   bd = INFINITY;
   bi = INT_MAX;
   const int cx = cell_coord(q.x), cy = cell_coord(q.y), cz = cell_coord(q.z);
+  // squared gap of q to the cell slab at offset dd along one axis, rounded as l2 rounds: a point
+  // of that slab has |fl(q - p)| >= this gap (rounding is monotone and symmetric)
+  auto gap2 = [](float v, int c, int dd) {
+    const float g = dd < 0 ? v - (float)(c + dd + 1) : dd > 0 ? (float)(c + dd) - v : 0.0f;
+    return g * g;
+  };
   for (int h = 0; h <= kMaxShell; ++h) {
     for (int dx = -h; dx <= h; ++dx)
       for (int dy = -h; dy <= h; ++dy) {
         const int step = (h == 0 || dx == -h || dx == h || dy == -h || dy == h) ? 1 : 2 * h;
+        const float lxy = gap2(q.x, cx, dx) + gap2(q.y, cy, dy);
         for (int dz = -h; dz <= h; dz += step) {
+          // a cell whose every point is farther than bd cannot change the (d, index) minimum, and
+          // one with none nearer than dist_sqr cannot give a correspondence (finish rejects nd >= it)
+          const float lb = lxy + gap2(q.z, cz, dz);
+          if (lb > bd || lb >= dist_sqr) continue;
           const int s = grid_find(tab, g.log2T, cell_key(cx + dx, cy + dy, cz + dz));
           if (s < 0) continue;
           const int st = tab[s].start, n = tab[s].count;
@@ -249,11 +260,11 @@ __device__ __forceinline__ float box_lb(const float4& lo, const float4& hi, floa
 // findCorrespondingSurfFeatures search (FA:1724-1809): the up-walk visits nn+1 .. end-1 until a
 // ring above cs + 2.5, the down-walk nn-1 .. 0 until a ring below cs - 2.5, each point updating the
 // nearest same-ring (m2) or other-ring (m3) candidate with strict '<'. Whole 8-point blocks
-// (aligned to the box array) that contain no walk stop and whose box cannot beat the minimum they
-// would be tested against are skipped: the visits that remain are the walk's, in its order, so
-// the result is the serial loop's.
-__device__ void surf_finish(const float4* sl, const float4* box, int Ns, int fwd, float4 sel, float dist_sqr,
-                            int nn, float nd, int& i1, int& i2, int& i3) {
+// (aligned to the box array) and whole 64-point superblocks that contain no walk stop and whose
+// box cannot beat the minimum they would be tested against are skipped: the visits that remain
+// are the walk's, in its order, so the result is the serial loop's.
+__device__ void surf_finish(const float4* sl, const float4* box, const float4* box2, int Ns, int fwd, float4 sel,
+                            float dist_sqr, int nn, float nd, int& i1, int& i2, int& i3) {
   i1 = -1;
   i2 = -1;
   i3 = -1;
@@ -282,6 +293,13 @@ __device__ void surf_finish(const float4* sl, const float4* box, int Ns, int fwd
   };
   for (; j < end && (j & 7) && !stop; ++j) up_visit(j, sl[j]);
   for (; j < end && !stop; j += kScan) {
+    if ((j & 63) == 0 && j + 64 <= end) {  // a whole superblock
+      const float4 lo = box2[2 * (j >> 6)], hi = box2[2 * (j >> 6) + 1];
+      if ((double)(int)hi.w <= (double)cs + 2.5 && box_lb(lo, hi, sel) >= bound_up(lo.w, hi.w)) {
+        j += 64 - kScan;
+        continue;
+      }
+    }
     if (j + kScan <= end) {
       const float4 lo = box[2 * (j >> 3)], hi = box[2 * (j >> 3) + 1];
       if ((double)(int)hi.w <= (double)cs + 2.5 && box_lb(lo, hi, sel) >= bound_up(lo.w, hi.w)) continue;
@@ -308,6 +326,13 @@ __device__ void surf_finish(const float4* sl, const float4* box, int Ns, int fwd
   };
   for (; j >= 0 && (j & 7) != 7 && !stop; --j) down_visit(j, sl[j]);
   for (; j >= 0 && !stop; j -= kScan) {
+    if ((j & 63) == 63) {  // superblock [j - 63, j]
+      const float4 lo = box2[2 * (j >> 6)], hi = box2[2 * (j >> 6) + 1];
+      if ((double)(int)lo.w >= (double)cs - 2.5 && box_lb(lo, hi, sel) >= bound_dn(lo.w, hi.w)) {
+        j -= 64 - kScan;
+        continue;
+      }
+    }
     const float4 lo = box[2 * (j >> 3)], hi = box[2 * (j >> 3) + 1];  // block [j - 7, j]
     if ((double)(int)lo.w >= (double)cs - 2.5 && box_lb(lo, hi, sel) >= bound_dn(lo.w, hi.w)) continue;
     float4 c[kScan];
@@ -456,13 +481,14 @@ __device__ __noinline__ int s2s_solve_step(float* t, float* matP, const float* s
 }
 
 // k_s2s_boxes: per 8-point block of laserCloudSurfLast (index order), the box of its points and
-// the range of their rings (trunc of the intensity, as the walks read it).
+// the range of their rings (trunc of the intensity, as the walks read it); lanes 8m .. 8m + 7 then
+// combine their blocks into the box of 64-point superblock m. NaN coordinates stay out of the
+// boxes (fminf / fmaxf): their distances are NaN, which never update a minimum.
 __global__ void k_s2s_boxes(S2SArgs a) {
   const CellGrid& g = a.grids.g[1];
   const int p = blockIdx.y;
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   const int n = g.count(p);
-  if (8 * k >= n) return;
   const float4* pts = g.src + g.off[p];
   float4 lo = make_float4(INFINITY, INFINITY, INFINITY, INFINITY);
   float4 hi = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
@@ -472,9 +498,23 @@ __global__ void k_s2s_boxes(S2SArgs a) {
     lo = make_float4(fminf(lo.x, c.x), fminf(lo.y, c.y), fminf(lo.z, c.z), fminf(lo.w, r));
     hi = make_float4(fmaxf(hi.x, c.x), fmaxf(hi.y, c.y), fmaxf(hi.z, c.z), fmaxf(hi.w, r));
   }
-  float4* b = a.sbox + ((size_t)p * ((g.cap + 7) / 8) + k) * 2;
-  b[0] = lo;
-  b[1] = hi;
+  if (8 * k < n) {
+    float4* b = a.sbox + ((size_t)p * ((g.cap + 7) / 8) + k) * 2;
+    b[0] = lo;
+    b[1] = hi;
+  }
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) {
+    lo = make_float4(fminf(lo.x, __shfl_xor(lo.x, o, 64)), fminf(lo.y, __shfl_xor(lo.y, o, 64)),
+                     fminf(lo.z, __shfl_xor(lo.z, o, 64)), fminf(lo.w, __shfl_xor(lo.w, o, 64)));
+    hi = make_float4(fmaxf(hi.x, __shfl_xor(hi.x, o, 64)), fmaxf(hi.y, __shfl_xor(hi.y, o, 64)),
+                     fmaxf(hi.z, __shfl_xor(hi.z, o, 64)), fmaxf(hi.w, __shfl_xor(hi.w, o, 64)));
+  }
+  if ((k & 7) == 0 && 8 * k < n) {
+    float4* b = a.sbox2 + ((size_t)p * ((g.cap + 63) / 64) + (k >> 3)) * 2;
+    b[0] = lo;
+    b[1] = hi;
+  }
 }
 
 // Diagnostic build only (make prof -> libllsr_prof.so): thread 0 accumulates the wall clock of
@@ -501,7 +541,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
   const int p = blockIdx.x;
   const int tid = threadIdx.x;
 #ifdef LLSR_S2S_PROF
-  unsigned long long tprev = wall_clock64(), tAks = 0, tAkc = 0, tA = 0, tB = 0, tC = 0, tF = 0;
+  unsigned long long tprev = wall_clock64(), tAks = 0, tAkc = 0, tA = 0, tB = 0, tC = 0, tF = 0, tW = 0;
 #endif
   __shared__ float t[6];
   __shared__ float matP[9];
@@ -541,6 +581,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
       for (int k = tid; k < Nc; k += kThreads) lcl[k] = clg[k];
     const float4* sl = gs.src + gs.off[p];
     const float4* sbox = a.sbox + (size_t)p * ((gs.cap + 7) / 8) * 2;
+    const float4* sbox2 = a.sbox2 + (size_t)p * ((gs.cap + 63) / 64) * 2;
     const int capq = a.cap_sharp > a.cap_flat ? a.cap_sharp : a.cap_flat;
     int* idx = a.idx + (size_t)p * capq * 3;
     float4* grows = a.rows + (size_t)p * capq;
@@ -582,7 +623,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
         auto finish = [&](int q, float4 sel, int nn, float nd) {
           int i1, i2, i3 = -1;
           if (surf) {
-            surf_finish(sl, sbox, Ns, F, sel, a.dist_sqr, nn, nd, i1, i2, i3);
+            surf_finish(sl, sbox, sbox2, Ns, F, sel, a.dist_sqr, nn, nd, i1, i2, i3);
           } else if (corner_lds) {  // LDS-typed accesses (a generic pointer would issue flat loads)
             corner_finish(lcl, Nc, Ms, sel, a.dist_sqr, nn, nd, i1, i2);
           } else {
@@ -655,12 +696,15 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
           }
           if (tid == 0) nfb = 0;
           __syncthreads();
-          LLSR_STAMP(tF);
+          if (surf) LLSR_STAMP(tAks);
+          else LLSR_STAMP(tAkc);
           for (int q = tid; q < Q; q += kThreads) {
             const int* ix = idx + 3 * q;
             finish(q, to_start(tl, qry[q]), ix[0], __int_as_float(ix[1]));
           }
           __syncthreads();
+          if (surf) LLSR_STAMP(tW);
+          else LLSR_STAMP(tF);
         }
         int nval = 0;
         for (int q = tid; q < Q; q += kThreads) {
@@ -881,6 +925,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
 #ifdef LLSR_S2S_PROF
     r.transform_cur[0] = (float)tAks; r.transform_cur[1] = (float)tAkc; r.transform_cur[2] = (float)tA;
     r.transform_cur[3] = (float)tB; r.transform_cur[4] = (float)tC; r.transform_cur[5] = (float)tF;
+    r.ms = (float)tW;
 #endif
     a.degen[p] = isDeg;
   }

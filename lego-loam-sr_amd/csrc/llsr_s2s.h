@@ -23,6 +23,7 @@ struct S2SArgs {
   int* error;                  // capacity violations
   float4* sbox;                // [P][ceil(cap / 8)][2] bounding boxes of 8-point blocks of laserCloudSurfLast
                                // in index order: (min x, y, z, min ring), (max x, y, z, max ring)
+  float4* sbox2;               // [P][ceil(cap / 64)][2] the same for 64-point superblocks
 };
 
 // bounding boxes of the surf-last cloud's 8-point blocks (the tripod walks skip a block whose box

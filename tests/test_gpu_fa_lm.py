@@ -137,3 +137,31 @@ def test_scan2scan_degenerate_bit_exact(require_gpu):
     pipe.close()
     assert n_deg >= 4
     assert not errs, "\n".join(errs)
+
+
+@pytest.mark.parametrize("variant", ["twins", "shuffled", "rings_swapped"])
+def test_scan2scan_surf_cloud_order(require_gpu, variant):
+    """The surf tripod search reads the last cloud's order (FA:1737-1803 walk it by index): the
+    device answers from the cell grid when that cloud's rings are sorted (k_s2s_boxes certifies
+    it), else walks. Twins (every point repeated in place: every distance ties, sorted) pin the
+    tie rule; a shuffled cloud and one with two ring blocks swapped take the walks."""
+    cfg, pairs = _pairs("vlp16", [31, 32, 33])
+    pipe = Pipeline(cfg)
+    errs = []
+    rng = np.random.default_rng(7)
+    for k, (sharp, flat, cl, sl) in enumerate(pairs):
+        if variant == "twins":
+            sl = np.repeat(sl, 2, axis=0)
+        elif variant == "shuffled":
+            sl = sl[rng.permutation(len(sl))]
+        else:
+            ring = np.trunc(sl[:, 3]).astype(np.int64)
+            a, b = ring == 3, ring == 9
+            sl = np.concatenate([sl[ring < 3], sl[b], sl[(ring > 3) & (ring < 9)], sl[a], sl[ring > 9]])
+        sl = np.ascontiguousarray(sl)
+        t = np.full(6, 0.002, np.float32)
+        g = pipe.scan2scan(sharp, flat, cl, sl, t, 0)
+        o = oracle_py.scan2scan(cfg, sharp, flat, cl, sl, t, 0)
+        errs += [f"pair {k}: {e}" for e in _same(g, o)]
+    pipe.close()
+    assert not errs, "\n".join(errs)
