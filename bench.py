@@ -140,7 +140,7 @@ def cpu_stage_times(budget_s: float, frames: int = 40) -> dict:
     ip = fa = mo = 0.0
     n, spent = 0, 0.0
     for k in range(frames):
-        scan = synth.make_scan(1 + k, "vlp16")
+        scan = synth.make_scan(1 + k, "vlp16", motion=True)
         t1 = time.perf_counter()
         om.process(scan)
         tot = time.perf_counter() - t1
@@ -408,7 +408,8 @@ def odometry_leg(dev, lidar: str, B: int, seqs: int, frames: int, steps: int, wa
     cfg.mode = _abi.LLSR_MODE_LM_APPLIED
     H, W = cfg.num_vertical_scans, cfg.num_horizontal_scans
     rank = dist.get_rank() if dist else 0
-    seq_scans = [[synth.make_scan(1 + 64 * (q + 4 * rank) + k, lidar) for k in range(frames)] for q in range(seqs)]
+    seq_scans = [[synth.make_scan(1 + 64 * (q + 4 * rank) + k, lidar, motion=True) for k in range(frames)]
+                 for q in range(seqs)]
     batches = []
     for k in range(frames):
         scans = [seq_scans[b % seqs][k] for b in range(B)]
@@ -457,6 +458,7 @@ def odometry_leg(dev, lidar: str, B: int, seqs: int, frames: int, steps: int, wa
     reps = [pipe.odometry_fetch(b)["lm"] for b in range(0, B, max(1, B // 64))]
     q_mean = float(np.mean(cnt[:, 4] + cnt[:, 5] + 160))
     it_mean = float(np.mean([r["surf_iterations"] + r["corner_iterations"] for r in reps]))
+    surf_it = [r["surf_iterations"] for r in reps if not r["skipped"]]
     last_mean = float(np.mean(cnt[:, 3] + cnt[:, 6] + 160))  # M + L + shadow: the next frame's last clouds
     lm_bytes = B * 16.0 * (q_mean + last_mean)
     lm_ms = st["lm_ms"] / max(1, st["batches"])
@@ -487,7 +489,9 @@ def odometry_leg(dev, lidar: str, B: int, seqs: int, frames: int, steps: int, wa
            "kernels_ms_per_step": {**{k: round(v, 4) for k, v in kt.items()},
                                    "s2s_grid_build": round(st["grid_ms"] / max(1, st["batches"]), 4),
                                    "k_s2s_lm": round(lm_ms, 4)},
-           "lm_iterations_mean": it_mean, "lm_queries_mean": q_mean}
+           "lm_iterations_mean": it_mean, "lm_queries_mean": q_mean,
+           "surf_iterations_mean": round(float(np.mean(surf_it)), 2) if surf_it else None,
+           "surf_iterations_max": int(max(surf_it)) if surf_it else None}
     if check:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle_py
@@ -527,7 +531,7 @@ def _mapping_cpu_worker(args):
     om = oracle_py.OracleMapping(cfg, mo_mode)
     n, t = 0, 0.0
     for k in range(frames):
-        scan = synth.make_scan(seed0 + k, "vlp16")
+        scan = synth.make_scan(seed0 + k, "vlp16", motion=True)
         t1 = time.perf_counter()
         om.process(scan)
         if k >= skip:
@@ -566,7 +570,7 @@ def mapping_leg(dev, B: int, seqs: int, warmup: int, steps: int, dist, check: bo
     rank = dist.get_rank() if dist else 0
     frames = warmup + steps
     seeds = [1 + 64 * (q + 4 * rank) for q in range(seqs)]
-    seq_scans = [[synth.make_scan(s0 + k, "vlp16") for k in range(frames)] for s0 in seeds]
+    seq_scans = [[synth.make_scan(s0 + k, "vlp16", motion=True) for k in range(frames)] for s0 in seeds]
     batches = []
     for k in range(frames):
         scans = [seq_scans[b % seqs][k] for b in range(B)]

@@ -18,7 +18,14 @@
 extern "C" {
 #endif
 
-#define LLSR_ABI_VERSION 1
+/* Bumped on every change of a struct layout or entry-point signature. Version 2: llsr_map_config
+ * gained enable_loop_closure and surrounding_keyframe_search_num (5 floats -> 5 floats + 2 int32),
+ * so a caller built against version 1 would pass a struct the library reads past. A consumer checks
+ * llsr_abi_version() == LLSR_ABI_VERSION once after loading the library. */
+#define LLSR_ABI_VERSION 2
+
+/* LLSR_ABI_VERSION as compiled into the loaded library. */
+int32_t llsr_abi_version(void);
 
 #define LLSR_OK 0
 #define LLSR_EINVAL (-22)
@@ -139,6 +146,9 @@ typedef struct llsr_sizes {
 } llsr_sizes;
 
 typedef struct llsr_handle llsr_handle;
+/* The configuration a handle was created with (e.g. iterCountThres for a host loop that drives
+ * the llsr_scan2map_shard_* steps itself). */
+int32_t llsr_get_config(const llsr_handle* h, llsr_config* cfg);
 
 /* Create a handle on HIP device `hip_device` able to process batches of up to `max_batch`
  * scans of up to `max_points` raw points each. Fails with LLSR_ENODEV when no device or the

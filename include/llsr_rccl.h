@@ -21,7 +21,7 @@ extern "C" {
 /* One split-correspondence scan-to-map batch on this rank (the handle must have been reserved as
  * for llsr_scan2map_batch; every rank passes the same batch):
  *   llsr_scan2map_shard_begin
- *   up to iterCountThres times:
+ *   up to iterCountThres times (the handle's, llsr_get_config):
  *     llsr_scan2map_shard_partial(h, rank, world, d_ne)
  *     ncclAllReduce(d_ne, d_ne, P * LLSR_NE_WORDS, ncclInt64, ncclSum, comm, hip_stream)
  *     llsr_scan2map_shard_step(h, d_ne, n_active or NULL)   host check every `poll` iterations
@@ -30,7 +30,7 @@ extern "C" {
  * kernels and the collective share (required: NULL is LLSR_EINVAL, since RCCL would read it as the
  * legacy default stream, which is not ordered with the handle's own stream). d_ne: device int64
  * [P][LLSR_NE_WORDS] exchange buffer, or NULL to allocate one for the call. *iterations (may be
- * NULL) = LM iterations run. The poses and reports land in batch->pose / batch->report,
+ * NULL) = LM iterations run (<= iterCountThres). The poses and reports land in batch->pose / batch->report,
  * bit-identical for every world size. LLSR_EIO when a collective fails (ncclGetLastError has the
  * text); the other codes as the llsr_scan2map_shard_* calls return them. */
 int32_t llsr_scan2map_rccl(llsr_handle* h, const llsr_s2m_batch* batch, void* nccl_comm, int32_t rank,

@@ -180,6 +180,8 @@ static int32_t fail(llsr_handle* h, int32_t code, const std::string& msg) {
       return fail(h, LLSR_EIO, std::string(#expr ": ") + hipGetErrorString(e_));         \
   } while (0)
 
+extern "C" int32_t llsr_abi_version(void) { return LLSR_ABI_VERSION; }
+
 extern "C" int32_t llsr_config_default(llsr_config* c, int32_t lidar) {
   if (!c) return LLSR_EINVAL;
   std::memset(c, 0, sizeof *c);
@@ -427,6 +429,12 @@ static hipError_t sync_handle_streams(llsr_handle* h) {
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+extern "C" int32_t llsr_get_config(const llsr_handle* h, llsr_config* cfg) {
+  if (!h || !cfg) return LLSR_EINVAL;
+  *cfg = h->cfg;
+  return LLSR_OK;
 }
 
 extern "C" const char* llsr_last_error(const llsr_handle* h) { return h ? h->err.c_str() : "null handle"; }

@@ -813,7 +813,9 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
             // lane = entry (0..11) + 12 * block; AtB entries and the lazy product use block 0 only
             const int e = tid % 12, blk = tid / 12;
             const bool lazy = e >= 9 || lazyAll;
-            const bool act = blk < (lazy ? 1 : nblk) && 12 * nblk <= 64;
+            // the lazy lanes (AtB, or everything when lazyAll) always sum on block 0: their result
+            // is read below whatever nblk is; the GEMM-blocked lanes only when the blocks fit
+            const bool act = lazy ? blk == 0 : (blk < nblk && 12 * nblk <= 64);
             const int ra = e < 9 ? e % 3 : e - 9, rb = e < 9 ? e / 3 : 3;
             float c = 0.0f;
             if (act) {

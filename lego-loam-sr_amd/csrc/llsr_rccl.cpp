@@ -37,24 +37,29 @@ extern "C" int32_t llsr_scan2map_rccl(llsr_handle* h, const llsr_s2m_batch* batc
     d_ne = own.p;
   }
   if (poll < 1) poll = 1;
+  llsr_config cfg;
+  if (llsr_get_config(h, &cfg) != LLSR_OK) return LLSR_EINVAL;
+  const int iter_max = cfg.iterCountThres;  // the loop bound of MO:1578
+  if (iter_max < 1) return LLSR_EINVAL;
   ncclComm_t comm = static_cast<ncclComm_t>(nccl_comm);
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
   int32_t rc = llsr_scan2map_shard_begin(h, batch, hip_stream);
   if (rc != LLSR_OK) return rc;
-  // iterCountThres bounds the loop; the device marks a problem done at that count too, so the
-  // n_active poll below ends the loop no later than the reference's
+  // at most iterCountThres rounds (MO:1578); the host reads the active count every `poll` rounds
+  // and on the last one, so a converged batch stops within poll - 1 rounds and never runs past
+  // the bound when poll does not divide it (the device also marks every problem done there)
   int it = 0;
-  for (;;) {
+  while (it < iter_max) {
     rc = llsr_scan2map_shard_partial(h, rank, world, d_ne, hip_stream);
     if (rc != LLSR_OK) return rc;
     const ncclResult_t nr = ncclAllReduce(d_ne, d_ne, words, ncclInt64, ncclSum, comm, s);
     if (nr != ncclSuccess) return LLSR_EIO;
     ++it;
     int32_t active = -1;
-    rc = llsr_scan2map_shard_step(h, d_ne, (it % poll == 0) ? &active : nullptr, hip_stream);
+    const bool check = it % poll == 0 || it == iter_max;
+    rc = llsr_scan2map_shard_step(h, d_ne, check ? &active : nullptr, hip_stream);
     if (rc != LLSR_OK) return rc;
     if (active == 0) break;
-    if (it >= 1000000) return LLSR_EIO;  // unreachable: every problem stops at iterCountThres
   }
   rc = llsr_scan2map_shard_end(h, hip_stream);
   if (rc != LLSR_OK) return rc;

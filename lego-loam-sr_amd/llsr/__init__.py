@@ -30,7 +30,7 @@ LIB_PATH = os.environ.get("LLSR_LIB") or os.path.join(_PKG, "libllsr.so")  # ove
 _LIB = None
 
 EXPORTS = [
-    "llsr_config_default", "llsr_create", "llsr_destroy", "llsr_last_error", "llsr_query_sizes",
+    "llsr_abi_version", "llsr_config_default", "llsr_get_config", "llsr_create", "llsr_destroy", "llsr_last_error", "llsr_query_sizes",
     "llsr_reset_state", "llsr_process_scan", "llsr_process_batch", "llsr_fetch_scan",
     "llsr_batch_counts", "llsr_kernel_times_ms", "llsr_kernel_name", "llsr_set_profiling",
     "llsr_scan2map_reserve", "llsr_scan2map_batch", "llsr_scan2map", "llsr_scan2map_stats",
@@ -59,6 +59,11 @@ def lib():
             raise LlsrError(f"{LIB_PATH} missing: build it with `make -C lego-loam-sr_amd` "
                             "(there is no CPU fallback for the HIP path)")
         L = C.CDLL(LIB_PATH)
+        L.llsr_abi_version.restype = C.c_int32
+        L.llsr_abi_version.argtypes = []
+        if L.llsr_abi_version() != _abi.ABI_VERSION:
+            raise LlsrError(f"{LIB_PATH} has ABI version {L.llsr_abi_version()}, the bindings expect "
+                            f"{_abi.ABI_VERSION}: rebuild with `make -C lego-loam-sr_amd`")
         L.llsr_config_default.argtypes = [C.POINTER(Config), C.c_int32]
         L.llsr_create.argtypes = [C.POINTER(Config), C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]
         L.llsr_destroy.argtypes = [C.c_void_p]

@@ -5,6 +5,7 @@ import ctypes as C
 
 import numpy as np
 
+ABI_VERSION = 2  # LLSR_ABI_VERSION of include/llsr.h these bindings mirror (checked at load)
 LLSR_OK = 0
 LLSR_LIDAR_VLP16 = 0
 LLSR_LIDAR_HDL64E = 2

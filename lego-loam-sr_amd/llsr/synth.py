@@ -121,13 +121,41 @@ class _Scene:
         return t
 
 
+def sensor_attitude(seed: int) -> np.ndarray:
+    """The moving sensor's (dz, roll, pitch, yaw) for frame `seed` of its drive (radians / m).
+
+    A vehicle on an uneven road: each DoF is a sum of two sinusoids over the frame index
+    k = seed % 64 with phases drawn from the drive (scene) seed, amplitudes bounded by 5 cm in z,
+    2 deg in roll and pitch and 3 deg in yaw. Consecutive frames differ by up to ~1.5 deg in roll /
+    pitch and a few cm in z, which is what the scan-to-scan surf step solves for (pitch, roll and
+    the vertical translation, featureAssociation.cpp:2001-2003): without it that step converges
+    at its first iteration."""
+    k = float(seed % 64)
+    ph = np.random.default_rng(7700001 + seed // 64).uniform(0.0, 2.0 * np.pi, (4, 2))
+    amp = np.array([0.05, np.deg2rad(2.0), np.deg2rad(2.0), np.deg2rad(3.0)])
+    freq = np.array([[0.9, 2.3], [0.7, 1.9], [0.8, 2.1], [0.4, 1.3]])
+    return amp * (0.6 * np.sin(freq[:, 0] * k + ph[:, 0]) + 0.4 * np.sin(freq[:, 1] * k + ph[:, 1]))
+
+
+def _rot_zyx(roll: float, pitch: float, yaw: float) -> np.ndarray:
+    cr, sr, cp, sp, cy, sy = np.cos(roll), np.sin(roll), np.cos(pitch), np.sin(pitch), np.cos(yaw), np.sin(yaw)
+    rz = np.array([[cy, -sy, 0.0], [sy, cy, 0.0], [0.0, 0.0, 1.0]])
+    ry = np.array([[cp, 0.0, sp], [0.0, 1.0, 0.0], [-sp, 0.0, cp]])
+    rx = np.array([[1.0, 0.0, 0.0], [0.0, cr, -sr], [0.0, sr, cr]])
+    return rz @ ry @ rx
+
+
 def make_scan(seed: int, lidar: str = VLP16, dropout: float = 0.02, noise: float = 0.01,
               max_range: float = 100.0, origin_xy: tuple[float, float] | None = None,
-              scene_id: int | None = None, ground_ramp: tuple[float, float] | None = None) -> np.ndarray:
+              scene_id: int | None = None, ground_ramp: tuple[float, float] | None = None,
+              motion: bool = False) -> np.ndarray:
     """One raw scan as float32 [N, 4] (x, y, z, intensity), N = rings * columns (NaNs kept).
 
     The sensor sits at (0.5 * (seed % 64), U(-0.5, 0.5), 0) of scene `seed // 64`; scan-to-map
-    fixtures override both (`origin_xy`, `scene_id`) to place keyframes along one street."""
+    fixtures override both (`origin_xy`, `scene_id`) to place keyframes along one street. With
+    `motion` the sensor also carries the drive's 6-DoF attitude (`sensor_attitude`): the rays are
+    cast in the world from the tilted, yawed sensor and the points are returned in the sensor's own
+    frame, so every beam still points at its range-image bin centre."""
     rng = np.random.default_rng(seed)
     scene_id = seed // 64 if scene_id is None else scene_id  # scenes shared by 64 scans
     scene = _Scene(np.random.default_rng(1000003 + scene_id), ground_ramp)
@@ -146,7 +174,12 @@ def make_scan(seed: int, lidar: str = VLP16, dropout: float = 0.02, noise: float
     origin = np.array([0.5 * (seed % 64), rng.uniform(-0.5, 0.5), 0.0])
     if origin_xy is not None:
         origin[:2] = origin_xy
-    t = scene.cast(origin, d, max_range)
+    if motion:
+        dz, roll, pitch, yaw = sensor_attitude(seed)
+        origin[2] += dz
+        t = scene.cast(origin, d @ _rot_zyx(roll, pitch, yaw).T, max_range)
+    else:
+        t = scene.cast(origin, d, max_range)
     r = t + rng.normal(0.0, noise, size=t.shape)
     drop = rng.random(t.shape) < dropout
     r[drop | ~np.isfinite(t)] = np.nan
@@ -180,14 +213,15 @@ def make_symmetric_scan(seed: int, lidar: str = VLP16, quadrants: int = 4) -> np
     return np.concatenate(out, axis=0)
 
 
-def make_batch(n_scans: int, lidar: str = VLP16, distinct: int | None = None, seed0: int = 1):
+def make_batch(n_scans: int, lidar: str = VLP16, distinct: int | None = None, seed0: int = 1,
+               motion: bool = False):
     """B raw scans packed as (float32 [sum N, 4], int64 offsets [B+1]).
 
     `distinct` scans are ray-cast (seeds seed0..) and tiled to fill the batch — the device work
     per scan is identical whether or not two slots carry the same cloud.
     """
     distinct = n_scans if distinct is None else max(1, min(distinct, n_scans))
-    base = [make_scan(seed0 + k, lidar) for k in range(distinct)]
+    base = [make_scan(seed0 + k, lidar, motion=motion) for k in range(distinct)]
     scans = [base[k % distinct] for k in range(n_scans)]
     offsets = np.zeros(n_scans + 1, dtype=np.int64)
     offsets[1:] = np.cumsum([s.shape[0] for s in scans])

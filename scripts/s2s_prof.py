@@ -23,7 +23,7 @@ B = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
 cfg = default_config(lidar, 2048 if lidar == "hdl64e" else None)
 cfg.mode = _abi.LLSR_MODE_LM_APPLIED
 # the bench's odometry leg: 2 sequences x 4 frames replayed in a loop (every 4th batch jumps back)
-seqs = [[synth.make_scan(1 + 64 * q + k, lidar) for k in range(4)] for q in range(2)]
+seqs = [[synth.make_scan(1 + 64 * q + k, lidar, motion=True) for k in range(4)] for q in range(2)]
 pipe = Pipeline(cfg, max_batch=B, max_points=cfg.num_vertical_scans * cfg.num_horizontal_scans)
 batches = []
 for k in range(4):

@@ -38,6 +38,34 @@ def fa_degenerate_pairs(n=6):
     return cfg, out
 
 
+# flat-query offsets k of fa_degenerate_surf_pairs whose surf step is degenerate at iteration 0
+# (every AtA eigenvalue below 10), and offsets with fewer than 10 surf correspondences (every surf
+# iteration skipped); found by the oracle, re-checked by tests/test_degenerate.py
+FA_DEGENERATE_SURF_CASES = (8, 10, 17)
+FA_SURF_SKIP_CASES = (0, 4)
+
+
+def fa_degenerate_surf_pairs():
+    """(cfg, [(sharp, flat, corner_last, surf_last, t0, is_degenerate_in)]): frames 1 -> 2 of the
+    moving drive shrunk 10x with 12 flat queries (offset k) and 5 sharp ones (the corner step
+    never reaches 10 correspondences, so it skips every iteration and the flag it leaves is the
+    surf step's), each with isDegenerate carried in as 0 and as 1."""
+    cfg = default_config("vlp16")
+    ora = oracle_py.Oracle(cfg)
+    prev = ora.process(synth.make_scan(1, "vlp16", motion=True))
+    cur = ora.process(synth.make_scan(2, "vlp16", motion=True))
+    sharp, flat, cl, sl = oracle_py.fa_lm_inputs(prev, cur)
+    n = len(flat) - 160  # the scan's own flat points (the shadow points are appended)
+    t0 = np.array([0.01, 0.0, -0.01, 0.0, 0.02, 0.0], np.float32)
+    out = []
+    for k in FA_DEGENERATE_SURF_CASES + FA_SURF_SKIP_CASES:
+        idx = (np.arange(12) * 11 + 5 * k) % n
+        for deg_in in (0, 1):
+            out.append((_scaled(sharp[:5], 0.1), _scaled(flat[idx], 0.1), _scaled(cl, 0.1), _scaled(sl, 0.1),
+                        t0, deg_in))
+    return cfg, out
+
+
 # (query, offset) pairs of the fixture whose shrunk 10 + 50 query problem is degenerate
 # (found by the oracle; tests/test_degenerate.py re-checks that every one of them is)
 MO_DEGENERATE_CASES = ((0, 0), (0, 12), (1, 16), (1, 20), (2, 4), (2, 8), (3, 12), (3, 28))

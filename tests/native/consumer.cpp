@@ -179,6 +179,10 @@ int main(int argc, char** argv) {
     fprintf(stderr, "usage: %s ipfa|s2s|s2m|mapping in.bin out.bin\n", argv[0]);
     return 2;
   }
+  if (llsr_abi_version() != LLSR_ABI_VERSION) {  // built against another header
+    fprintf(stderr, "libllsr ABI %d, header %d\n", (int)llsr_abi_version(), LLSR_ABI_VERSION);
+    return 5;
+  }
   const std::string mode = argv[1];
   FILE* in = fopen(argv[2], "rb");
   FILE* out = fopen(argv[3], "wb");

@@ -15,7 +15,8 @@ int main(void) {
   float pose[6] = {0, 0, 0, 0, 0, 0};
   float tc[6] = {0, 0, 0, 0, 0, 0};
   int32_t deg = 0;
-  int32_t rc = llsr_config_default(&cfg, LLSR_LIDAR_VLP16);
+  int32_t rc = llsr_abi_version() == LLSR_ABI_VERSION ? LLSR_OK : LLSR_EINVAL;
+  if (rc == LLSR_OK) rc = llsr_config_default(&cfg, LLSR_LIDAR_VLP16);
   if (rc == LLSR_OK) rc = llsr_create(&cfg, 0, 1, 30000, &h);
   if (rc != LLSR_OK) {
     printf("llsr_create: %d\n", (int)rc);

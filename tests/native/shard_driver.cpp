@@ -153,6 +153,7 @@ int main(int argc, char** argv) {
     std::ofstream out(argv[2], std::ios::binary);
     out.write(reinterpret_cast<const char*>(rep.data()), P * sizeof(llsr_lm_report));
     out.write(reinterpret_cast<const char*>(&us), sizeof us);
+    out.write(reinterpret_cast<const char*>(&it), sizeof it);
     CHECK(out.good(), "write OUT");
   }
   std::printf("rank %d of %d: %d problems, %d LM iterations, allreduce %.2f us\n", rank, world, P, it, us);

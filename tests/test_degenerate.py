@@ -38,3 +38,38 @@ def test_mo_degenerate_freezes_pose():
             np.testing.assert_array_equal(o["pose"], pr[4])
         for pr in _scenes.mo_degenerate_problems(regular=True)[len(_scenes.MO_DEGENERATE_CASES):]:
             assert oracle_py.scan2map(cfg, *pr)["degenerate"] == 0
+
+
+def test_fa_surf_phase_degenerate():
+    """The surf step's degenerate scenes (_scenes.fa_degenerate_surf_pairs): a degenerate iteration
+    0 leaves the pose and stops the step; a step with fewer than 10 correspondences skips every
+    iteration and passes the carried-in flag through (the corner step skips too)."""
+    cfg, cases = _scenes.fa_degenerate_surf_pairs()
+    n_deg = n_skip = 0
+    for sharp, flat, cl, sl, t0, deg_in in cases:
+        o = oracle_py.scan2scan(cfg, sharp, flat, cl, sl, t0, deg_in)
+        assert o["corner_iterations"] == 100 and o["n_corner_corr"] < 10
+        np.testing.assert_array_equal(o["transform_cur"], t0)  # nothing moves in either case
+        if o["n_surf_corr"] >= 10:
+            assert o["degenerate"] == 1 and o["surf_iterations"] == 0
+            n_deg += 1
+        else:
+            assert o["surf_iterations"] == 100 and o["degenerate"] == deg_in
+            n_skip += 1
+    assert n_deg == 2 * len(_scenes.FA_DEGENERATE_SURF_CASES)
+    assert n_skip == 2 * len(_scenes.FA_SURF_SKIP_CASES)
+
+
+def test_moving_drive_iterates_surf_step():
+    """synth.sensor_attitude makes consecutive frames differ in z / roll / pitch, so the surf step
+    runs past its first iteration (on a level drive it converges at iteration 0)."""
+    from llsr import synth
+    cfg = default_config("vlp16")
+    its = {}
+    for motion in (False, True):
+        ora = oracle_py.Oracle(cfg)
+        prev = ora.process(synth.make_scan(2, "vlp16", motion=motion))
+        cur = ora.process(synth.make_scan(3, "vlp16", motion=motion))
+        its[motion] = oracle_py.scan2scan(cfg, *oracle_py.fa_lm_inputs(prev, cur), np.zeros(6, np.float32))
+    assert its[False]["surf_iterations"] <= 1
+    assert its[True]["surf_iterations"] >= 6

@@ -16,13 +16,15 @@ from llsr import Pipeline, _abi, default_config, shadow_points, synth
 pytestmark = pytest.mark.gpu
 
 
-def _pairs(lidar, seeds, horizontal=None):
+def _pairs(lidar, seeds, horizontal=None, motion=True):
+    """Consecutive frames of a moving sensor (synth.sensor_attitude: z, roll, pitch and yaw change
+    from frame to frame, so the surf step iterates, FA:1846-2010)."""
     cfg = default_config(lidar, horizontal)
     ora = oracle_py.Oracle(cfg)
-    prev = ora.process(synth.make_scan(seeds[0], lidar))
+    prev = ora.process(synth.make_scan(seeds[0], lidar, motion=motion))
     out = []
     for s in seeds[1:]:
-        cur = ora.process(synth.make_scan(s, lidar))
+        cur = ora.process(synth.make_scan(s, lidar, motion=motion))
         out.append(oracle_py.fa_lm_inputs(prev, cur))
         prev = cur
     return cfg, out
@@ -43,25 +45,32 @@ def test_shadow_points_match_oracle(require_gpu):
     np.testing.assert_array_equal(shadow_points(), oracle_py.shadow_points())
 
 
-@pytest.mark.parametrize("lidar,seeds,horizontal", [("vlp16", [1, 2, 3, 4, 5, 70], None),
-                                                    ("hdl64e", [5, 6, 7], 2048)])
+@pytest.mark.parametrize("lidar,seeds,horizontal", [("vlp16", [1, 2, 3, 4, 5, 6, 7, 70], None),
+                                                    ("hdl64e", [5, 6, 7, 8], 2048)])
 def test_scan2scan_bit_exact(require_gpu, lidar, seeds, horizontal):
+    """Every surf iteration past the first is covered: the kNN refresh every 5th iteration and the
+    parked indices in between (FA:1707-1803), the iterCount >= 5 weighting (FA:1825-1830) and the
+    surf update of pitch / roll / vertical translation (FA:2001-2003) — at least one pair per lidar
+    runs the surf step for >= 6 iterations (asserted on the oracle's count)."""
     cfg, pairs = _pairs(lidar, seeds, horizontal)
     pipe = Pipeline(cfg)
-    errs = []
+    errs, surf_its = [], []
     t = np.zeros(6, np.float32)
     for k, (sharp, flat, cl, sl) in enumerate(pairs):
         g = pipe.scan2scan(sharp, flat, cl, sl, t, 0)
         o = oracle_py.scan2scan(cfg, sharp, flat, cl, sl, t, 0)
+        surf_its.append(o["surf_iterations"])
         errs += [f"pair {k}: {e}" for e in _same(g, o)]
         t = o["transform_cur"] * np.float32(0.5)  # a non-zero initial guess for the next pair
     pipe.close()
     assert not errs, "\n".join(errs)
+    assert max(surf_its) >= 6, f"no pair iterates the surf step: {surf_its}"
 
 
 def test_scan2scan_batch_and_skip(require_gpu):
     import torch
     cfg, pairs = _pairs("vlp16", [11, 12, 13, 14, 15])
+    assert max(oracle_py.scan2scan(cfg, *pr, np.zeros(6, np.float32), 0)["surf_iterations"] for pr in pairs) >= 6
     # problem 4: a last corner cloud below the FA:2506 guard -> skipped, transform untouched
     pairs.append((pairs[0][0], pairs[0][1], pairs[0][2][:9], pairs[0][3]))
     P = len(pairs)
@@ -139,12 +148,40 @@ def test_scan2scan_degenerate_bit_exact(require_gpu):
     assert not errs, "\n".join(errs)
 
 
+def test_scan2scan_degenerate_surf_bit_exact(require_gpu):
+    """The surf step's degenerate branch (FA:1959-1996): shrunk scenes with 12 flat queries whose
+    iteration-0 AtA has every eigenvalue below 10 (matP = matV.inverse() * 0, the pose stays, the
+    step stops: surf_iterations 0 with the flag set), and scenes with fewer than 10 surf
+    correspondences, where every surf iteration is skipped (FA:2516) and a carried-in isDegenerate
+    survives into the corner step (5 sharp points: skipped too, so the flag reported is the surf
+    step's). matP at iteration >= 1 after a degenerate iteration 0 is unreachable: a degenerate
+    iteration 0 gives matX = 0, so deltaR = deltaT = 0 and the loop breaks (FA:2007-2009), and a
+    skipped iteration 0 leaves the pose, hence the correspondence set, unchanged."""
+    import _scenes
+    cfg, cases = _scenes.fa_degenerate_surf_pairs()
+    pipe = Pipeline(cfg)
+    errs, n_deg, n_skip = [], 0, 0
+    for k, (sharp, flat, cl, sl, t0, deg_in) in enumerate(cases):
+        g = pipe.scan2scan(sharp, flat, cl, sl, t0, deg_in)
+        o = oracle_py.scan2scan(cfg, sharp, flat, cl, sl, t0, deg_in)
+        n_deg += o["degenerate"] and o["surf_iterations"] == 0 and o["n_surf_corr"] >= 10
+        n_skip += o["surf_iterations"] == 100
+        errs += [f"case {k}: {e}" for e in _same(g, o)]
+        if g["is_degenerate"] != o["is_degenerate"]:
+            errs.append(f"case {k}: is_degenerate {g['is_degenerate']} vs {o['is_degenerate']}")
+    pipe.close()
+    assert n_deg >= 3 and n_skip >= 2, (n_deg, n_skip)
+    assert not errs, "\n".join(errs)
+
+
 @pytest.mark.parametrize("variant", ["twins", "shuffled", "rings_swapped"])
 def test_scan2scan_surf_cloud_order(require_gpu, variant):
     """The surf tripod search reads the last cloud's order (FA:1737-1803 walk it by index): the
-    device answers from the cell grid when that cloud's rings are sorted (k_s2s_boxes certifies
-    it), else walks. Twins (every point repeated in place: every distance ties, sorted) pin the
-    tie rule; a shuffled cloud and one with two ring blocks swapped take the walks."""
+    device walks the cloud from the kNN hit in both directions, skipping 8-point blocks and
+    64-point superblocks whose bounding boxes (k_s2s_boxes) cannot beat the current minimum and
+    hold no ring stop. Twins (every point repeated in place: every distance ties) pin the tie
+    rule; a shuffled cloud and one with two ring blocks swapped break the ring order the stops
+    and boxes see."""
     cfg, pairs = _pairs("vlp16", [31, 32, 33])
     pipe = Pipeline(cfg)
     errs = []

@@ -1,7 +1,7 @@
 """GPU parity of the mapping chain (llsr_mapping_*: IP -> FA -> odometry -> MapOptimization::run,
 MO:1854-1896) against the oracle's sequence restatement (oracle_py.OracleMapping).
 
-B independent VLP-16 drives advance one scan per call; after every call each slot's MapOptimization
+B independent moving drives (synth.sensor_attitude) advance one scan per call; after every call each slot's MapOptimization
 state is compared with the oracle's: frame / keyframe counts, whether scan-to-map ran (MO:1573),
 the query and local-map sizes, the LM report, transformSum / TobeMapped / BefMapped / AftMapped,
 and at the end the key poses (cloudKeyPoses6D).
@@ -44,10 +44,10 @@ def _drive(mode, seeds, frames, iters=None, pcl=False, lidar="vlp16", search_num
         pipe.set_voxel_order(_abi.LLSR_VOXEL_ORDER_PCL)
     oras = [oracle_py.OracleMapping(cfg, mode, pcl_voxel_order=pcl, loop_closure=lc, search_num=search_num)
             for _ in seeds]
-    errs = []
+    errs, surf_its = [], []
     queue_full = False
     for k in range(frames):
-        scans = [synth.make_scan(s0 + k, lidar) for s0 in seeds]
+        scans = [synth.make_scan(s0 + k, lidar, motion=True) for s0 in seeds]
         off = np.zeros(len(scans) + 1, np.int64)
         off[1:] = np.cumsum([len(s) for s in scans])
         d_pts = torch.from_numpy(np.concatenate(scans)).cuda()
@@ -60,6 +60,8 @@ def _drive(mode, seeds, frames, iters=None, pcl=False, lidar="vlp16", search_num
             tag = f"mode {mode} slot {b} frame {k}"
             if g["frames"] != o["frames"]:
                 errs.append(f"{tag}: frames {g['frames']} vs {o['frames']}")
+            if o["odo"]["lm"] is not None:
+                surf_its.append(o["odo"]["lm"]["surf_iterations"])
             if g["mo_frames"] != ora.mo_frames or g["keyframes"] != len(ora.keyposes):
                 errs.append(f"{tag}: MapOptimization frames / keyframes {g['mo_frames']} / {g['keyframes']} vs "
                             f"{ora.mo_frames} / {len(ora.keyposes)}")
@@ -93,6 +95,7 @@ def _drive(mode, seeds, frames, iters=None, pcl=False, lidar="vlp16", search_num
         elif not np.array_equal(kg, ko):
             errs.append(f"slot {b}: keyposes max |d| {np.abs(kg - ko).max():.3g}")
     pipe.close()
+    assert max(surf_its) >= 6, f"the drives never iterate the FA surf step: {surf_its}"
     return errs, queue_full
 
 
@@ -145,7 +148,7 @@ def test_mapping_reset_repeats(require_gpu):
     for _ in range(2):
         pipe.mapping_reset()
         for k in range(4):
-            pts = synth.make_scan(9 + k, "vlp16")
+            pts = synth.make_scan(9 + k, "vlp16", motion=True)
             d_pts = torch.from_numpy(pts).cuda()
             d_off = torch.tensor([0, len(pts)], dtype=torch.int64).cuda()
             torch.cuda.synchronize()

@@ -24,9 +24,9 @@ def _sequence(lidar, horizontal, slots, frames):
     H, W = cfg.num_vertical_scans, cfg.num_horizontal_scans
     pipe = Pipeline(cfg, max_batch=len(slots), max_points=H * W)
     oras = [oracle_py.OracleOdometry(cfg) for _ in slots]
-    errs = []
+    errs, surf_its = [], []
     for k in range(frames):
-        scans = [synth.make_scan(s0 + k, lidar) for s0 in slots]
+        scans = [synth.make_scan(s0 + k, lidar, motion=True) for s0 in slots]
         off = np.zeros(len(scans) + 1, np.int64)
         off[1:] = np.cumsum([len(s) for s in scans])
         d_pts = torch.from_numpy(np.concatenate(scans)).cuda()
@@ -41,6 +41,11 @@ def _sequence(lidar, horizontal, slots, frames):
                 errs.append(f"{tag}: frames {g['frames']} vs {o['frames']}")
             if (g["lm"]["skipped"] == 1) != (o["lm"] is None):
                 errs.append(f"{tag}: skipped {g['lm']['skipped']} vs oracle lm {o['lm'] is not None}")
+            elif o["lm"] is not None:
+                surf_its.append(o["lm"]["surf_iterations"])
+                for key in ("surf_iterations", "corner_iterations", "n_surf_corr", "n_corner_corr", "degenerate"):
+                    if g["lm"][key] != o["lm"][key]:
+                        errs.append(f"{tag}: lm {key} {g['lm'][key]} vs {o['lm'][key]}")
             for key in ("transform_cur", "transform_sum"):
                 if not np.array_equal(g[key], o[key]):
                     errs.append(f"{tag}: {key} {g[key]} vs {o[key]} (max |d| {np.abs(g[key] - o[key]).max():.3g})")
@@ -51,10 +56,12 @@ def _sequence(lidar, horizontal, slots, frames):
                 elif not np.array_equal(g[key], ref):
                     errs.append(f"{tag}: {key} max |d| {np.abs(g[key] - ref).max():.3g}")
     pipe.close()
+    assert max(surf_its) >= 6, f"the drive never iterates the surf step: {surf_its}"
     return errs
 
 
 def test_odometry_vlp16_sequences(require_gpu):
+    """Three moving drives (synth.sensor_attitude), five frames each."""
     errs = _sequence("vlp16", None, [1, 65, 130], 5)
     assert not errs, "\n".join(errs)
 

@@ -54,10 +54,11 @@ def _cfg(iters):
     return cfg
 
 
-def test_cpp_driver_rccl_world1(require_gpu, tmp_path):
+@pytest.mark.parametrize("iters,poll", [(60, 3), (50, 16), (7, 4)])
+def test_cpp_driver_rccl_world1(require_gpu, tmp_path, iters, poll):
+    """poll 16 does not divide 50 (nor 4 divide 7): the driver still stops at iterCountThres."""
     assert os.path.exists(DRIVER), "build it with `make -C lego-loam-sr_amd`"
     probs = _problems()
-    iters = 60
     inp, out = tmp_path / "in.bin", tmp_path / "out.bin"
     with open(inp, "wb") as f:
         f.write(struct.pack("<i", len(probs)))
@@ -66,15 +67,17 @@ def test_cpp_driver_rccl_world1(require_gpu, tmp_path):
             for c in pr[:4]:
                 f.write(np.ascontiguousarray(c, np.float32).tobytes())
             f.write(np.ascontiguousarray(pr[4], np.float32).tobytes())
-    r = subprocess.run([DRIVER, str(inp), str(out), str(_abi.LLSR_MODE_LM_APPLIED), str(iters), "3"],
+    r = subprocess.run([DRIVER, str(inp), str(out), str(_abi.LLSR_MODE_LM_APPLIED), str(iters), str(poll)],
                        capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stdout + r.stderr
     raw = out.read_bytes()
     n = ctypes.sizeof(_abi.LmReport)
     dev = [_abi.LmReport.from_buffer_copy(raw[p * n:(p + 1) * n]).as_dict() for p in range(len(probs))]
-    us = struct.unpack("<f", raw[len(probs) * n:len(probs) * n + 4])[0]
+    us, it = struct.unpack("<fi", raw[len(probs) * n:len(probs) * n + 8])
     assert us > 0.0
     ora = oracle_py.shard_run_local(_cfg(iters), probs, 1)
+    it_ref = max(o["iterations"] for o in ora)
+    assert it_ref <= it <= min(iters, it_ref + poll - 1), (it, it_ref, iters, poll)
     errs = [f"problem {p}: {dev[p]} vs {ora[p]}" for p in range(len(probs)) if not _same(dev[p], ora[p])]
     assert not errs, "\n".join(errs)
     print(r.stdout.strip())
