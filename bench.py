@@ -109,9 +109,23 @@ def cpu_baseline_all_cores(scans: list[np.ndarray], budget_s: float) -> dict:
     wall = time.perf_counter() - t1
     n = sum(r[0] for r in res)
     busy = max(r[1] for r in res)
-    return {"value": round(n / busy, 1), "unit": "scans/s", "cores": nproc, "kind": "port", "cpu": cpu_model(),
+    v = n / busy
+    return {"value": round(v, 1), "unit": "scans/s", "cores": nproc, "kind": "port", "cpu": cpu_model(),
             "sample": f"{nproc} processes x the oracle IP+FA-feature path, {n} scans in all, slowest process "
-                      f"{busy:.1f} s busy ({wall:.1f} s wall incl. start-up)"}
+                      f"{busy:.1f} s busy ({wall:.1f} s wall incl. start-up)",
+            **host_share(v, nproc)}
+
+
+def host_share(value: float, nproc: int) -> dict:
+    """Why the all-core baselines stop at 16 processes, and the whole host's figure next to it."""
+    ncpu = os.cpu_count() or nproc
+    return {"cores_cap_reason": "16 = the host-CPU share the GPU pool grants one MI355X job (OMP_NUM_THREADS / "
+                                "MAX_JOBS are 16 there; more workers than the share would be throttled); on an "
+                                "8-GPU node that is also about one GPU's share of the host",
+            "host_cpus": ncpu,
+            "full_host_extrapolated": round(value / nproc * ncpu, 1),
+            "full_host_note": f"linear extrapolation of the per-process rate to all {ncpu} host CPUs "
+                              "(an upper bound: SMT siblings and memory bandwidth are shared)"}
 
 
 def cpu_stage_times(budget_s: float, frames: int = 40) -> dict:
@@ -163,6 +177,13 @@ def cpu_stage_times(budget_s: float, frames: int = 40) -> dict:
                       "1 thread per stage)"}
 
 
+def same_build(record: dict) -> bool:
+    """A PMC record under profiles/ counts only for the build it measured (llsr_build_id, a hash
+    of the kernel sources): bytes measured on other kernels would be stale evidence."""
+    from llsr import build_id
+    return record.get("build_id") == build_id()
+
+
 def lm_traffic(kernel: str, problems: int, leg: str | None = None):
     """PMC-measured HBM bytes per launch of an LM kernel (scripts/pmc_lm.sh, committed as
     profiles/traffic_lm_latest.json; records keyed "kernel" or "kernel@leg"), or None when it was
@@ -170,7 +191,10 @@ def lm_traffic(kernel: str, problems: int, leg: str | None = None):
     f = os.environ.get("LLSR_TRAFFIC_LM_JSON", os.path.join(REPO, "profiles", "traffic_lm_latest.json"))
     if not os.path.exists(f):
         return None
-    ks = json.load(open(f)).get("kernels", {})
+    tj = json.load(open(f))
+    if not same_build(tj):
+        return None
+    ks = tj.get("kernels", {})
     rec = ks.get(f"{kernel}@{leg}") if leg else None
     rec = rec or ks.get(kernel)
     if rec and leg and rec.get("leg_key", leg) != leg:
@@ -633,7 +657,8 @@ def mapping_leg(dev, B: int, seqs: int, warmup: int, steps: int, dist, check: bo
         out["cpu_baseline_all_cores"] = {
             "value": round(nf / busy, 2), "unit": "scans/s", "cores": nproc, "kind": "port", "cpu": cpu_model(),
             "sample": f"{nproc} processes, one drive each, frames {warmup}..{frames - 1} timed ({nf} frames, "
-                      f"slowest process {busy:.1f} s busy, {wall:.1f} s wall incl. start-up and untimed frames)"}
+                      f"slowest process {busy:.1f} s busy, {wall:.1f} s wall incl. start-up and untimed frames)",
+            **host_share(nf / busy, nproc)}
         out["speedup_vs_cpu"] = round(out["value"] / world / out["cpu_baseline"]["value"], 1)
         out["speedup_vs_cpu_all_cores"] = round(out["value"] / world / out["cpu_baseline_all_cores"]["value"], 1)
     pipe.close()
@@ -832,7 +857,7 @@ def main():
         rccl1.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1,
                                  device_id=torch.device("cuda", dev))
 
-    from llsr import Pipeline, default_config, synth
+    from llsr import Pipeline, build_id, default_config, synth
     cfg = default_config("vlp16")
     H, W = cfg.num_vertical_scans, cfg.num_horizontal_scans
     B = args.batch
@@ -917,8 +942,12 @@ def main():
     # scaled to this batch size; null when no measurement for this kernel exists.
     tfile = os.environ.get("LLSR_TRAFFIC_JSON", os.path.join(REPO, "profiles", "traffic_latest.json"))
     tjson = json.load(open(tfile)) if os.path.exists(tfile) else {}
+    if not same_build(tjson):
+        tjson = {}
 
     def traffic_of(kname):
+        if kname == "k_project" and fused:
+            kname = "k_project_fused"  # the VLP-16 launch's own name in the PMC record
         rec = tjson.get("kernels", {}).get(kname)
         return rec["hbm_bytes"] / tjson["batch"] * B if rec and tjson.get("batch") else None
 
@@ -942,6 +971,15 @@ def main():
                        traffic=(tp + tc) if (tp is not None and tc is not None) else None,
                        note="north_star's projection+curvature figure: SURVEY.md 8(d) B_pc = 20 N + 24 HW + 29 S "
                             "over the two kernels' time")
+
+    # the dominant kernel at SURVEY.md 8(d)'s own per-unit figure where it names one (feature
+    # select B_fs = 25 S); the builder's wider model (incl. the VoxelGrid gathers) rides along
+    if dom == "k_select_ring":
+        roof_dom = roofline(dom, 25 * csum["S"], note="SURVEY.md 8(d) B_fs = 25 S; builder model incl. the "
+                            f"less-flat VoxelGrid gathers: {per[dom]:.4g} B per launch")
+        roof_dom["builder_model_frac"] = roofline(dom)["frac"]
+    else:
+        roof_dom = roofline(dom)
 
     s2m = {}
     for mode_name in [m for m in args.s2m_modes.split(",") if m]:
@@ -985,6 +1023,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
+            "build_id": build_id(),
             "dtype": "fp32",
             "data": "synthetic (seeded ray-cast VLP-16 street scenes, 2% dropout, 1 cm noise)",
             "config": {"workload": "configs[1]: VLP-16 1800x16 projection + ground/cluster segmentation "
@@ -992,7 +1031,7 @@ def main():
                        "lidar": "VLP-16", "rings": H, "columns": W, "scans_per_gpu_per_step": B,
                        "distinct_clouds_per_gpu": args.distinct, "streams_per_gpu": nS,
                        "parallelism": f"scan-sharded x{world}"},
-            "roofline": roofline(dom),
+            "roofline": roof_dom,
             # north_star's kernel: the (fused) projection + range image + column ground pass
             "roofline_projection": roof_proj,
             "roofline_projection_curvature": roof_pc,

@@ -26,6 +26,9 @@ extern "C" {
 
 /* LLSR_ABI_VERSION as compiled into the loaded library. */
 int32_t llsr_abi_version(void);
+/* 16 hex digits identifying the kernel sources the library was built from (a hash of them): the
+ * performance records under profiles/ name the build they measured. */
+const char* llsr_build_id(void);
 
 #define LLSR_OK 0
 #define LLSR_EINVAL (-22)

@@ -30,7 +30,7 @@ LIB_PATH = os.environ.get("LLSR_LIB") or os.path.join(_PKG, "libllsr.so")  # ove
 _LIB = None
 
 EXPORTS = [
-    "llsr_abi_version", "llsr_config_default", "llsr_get_config", "llsr_create", "llsr_destroy", "llsr_last_error", "llsr_query_sizes",
+    "llsr_abi_version", "llsr_build_id", "llsr_config_default", "llsr_get_config", "llsr_create", "llsr_destroy", "llsr_last_error", "llsr_query_sizes",
     "llsr_reset_state", "llsr_process_scan", "llsr_process_batch", "llsr_fetch_scan",
     "llsr_batch_counts", "llsr_kernel_times_ms", "llsr_kernel_name", "llsr_set_profiling",
     "llsr_scan2map_reserve", "llsr_scan2map_batch", "llsr_scan2map", "llsr_scan2map_stats",
@@ -51,6 +51,11 @@ class LlsrError(RuntimeError):
     pass
 
 
+def build_id() -> str:
+    """The loaded library's llsr_build_id() (hash of the kernel sources it was built from)."""
+    return lib().llsr_build_id().decode()
+
+
 def lib():
     """Load libllsr.so (raises if it has not been built)."""
     global _LIB
@@ -64,6 +69,8 @@ def lib():
         if L.llsr_abi_version() != _abi.ABI_VERSION:
             raise LlsrError(f"{LIB_PATH} has ABI version {L.llsr_abi_version()}, the bindings expect "
                             f"{_abi.ABI_VERSION}: rebuild with `make -C lego-loam-sr_amd`")
+        L.llsr_build_id.restype = C.c_char_p
+        L.llsr_build_id.argtypes = []
         L.llsr_config_default.argtypes = [C.POINTER(Config), C.c_int32]
         L.llsr_create.argtypes = [C.POINTER(Config), C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]
         L.llsr_destroy.argtypes = [C.c_void_p]
@@ -134,7 +141,7 @@ def lib():
                                       C.c_void_p, C.c_void_p]
         for fn in EXPORTS:
             if fn not in ("llsr_last_error", "llsr_kernel_name", "llsr_destroy", "llsr_map_create",
-                          "llsr_map_destroy", "llsr_map_last_error"):
+                          "llsr_map_destroy", "llsr_map_last_error", "llsr_build_id"):
                 getattr(L, fn).restype = C.c_int32
         L.llsr_destroy.restype = None
         L.llsr_map_create.restype = C.c_void_p

@@ -25,6 +25,9 @@ out = {"source": f"scripts/pmc_lm.sh ({src}): rocprofv3 --pmc FETCH_SIZE / WRITE
                  "scans), leg B = HDL-64E odometry (512 scans)",
        "note": "FETCH_SIZE doubled per the gfx950 note (scripts/pmc_parse.py); bytes per launch averaged over "
                "the pass's launches", "kernels": {}}
+ids = {json.load(open(os.path.join(d, leg, "traffic.json"))).get("build_id") for leg in want}
+assert len(ids) == 1, ids
+out["build_id"] = ids.pop()
 for leg, items in want.items():
     t, sq = load(leg)
     for k, key_leg, leg_name, problems in items:

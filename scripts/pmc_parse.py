@@ -38,7 +38,7 @@ for k in sorted(set(fetch) | set(write)):
     f = (sum(fv) / len(fv) if fv else 0.0) * 1024 * 2
     w = (sum(wv) / len(wv) if wv else 0.0) * 1024
     out[k] = {"fetch_bytes_x2": f, "write_bytes": w, "hbm_bytes": f + w, "launches": max(len(fv), len(wv))}
-# the fused VLP-16 projection is reported under the bench's kernel name
-if "k_project_fused" in out:
-    out["k_project"] = out["k_project_fused"]
-print(json.dumps({"batch": batch, "kernels": out}, indent=1))
+# the build these counters measured: bench.py reports the bytes only for the same build
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "lego-loam-sr_amd"))
+import llsr  # noqa: E402
+print(json.dumps({"batch": batch, "build_id": llsr.build_id(), "kernels": out}, indent=1))
