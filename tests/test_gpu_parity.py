@@ -121,6 +121,25 @@ def test_edge_cases(require_gpu, case):
     assert not errs, f"{case}:\n  " + "\n  ".join(errs)
 
 
+def test_host_buffer_sequence_sizes(require_gpu):
+    """llsr_process_scan (the host-buffer, single-scan path) over a sequence on ONE handle with
+    max_points 40000, as the compiled consumer drives it (round 3's r03_v17 run faulted there on 3
+    VLP-16 scans in an uncommitted build): full scans, a 40000-point scan (max_points exactly, more
+    points than cells: every cell collides), a short one, an empty one and full scans again, each
+    compared with the oracle carrying the same FA state."""
+    cfg = default_config("vlp16")
+    scans = [synth.make_scan(s, "vlp16", motion=True) for s in (31, 32, 33)]
+    big = np.concatenate([scans[0], scans[1][: 40000 - len(scans[0])]], axis=0)
+    seq = scans + [big, scans[2][:3000], np.zeros((0, 4), np.float32)] + \
+        [synth.make_scan(s, "vlp16", motion=True) for s in (34, 35)]
+    pipe = Pipeline(cfg, max_points=40000)
+    ora = oracle_py.Oracle(cfg)
+    for k, pts in enumerate(seq):
+        errs = compare(pipe.process_scan(pts), ora.process(pts))
+        assert not errs, f"scan {k} ({len(pts)} points):\n  " + "\n  ".join(errs)
+    pipe.close()
+
+
 def test_golden_fixtures_pcl_order(require_gpu):
     """The device in LLSR_VOXEL_ORDER_PCL reproduces the committed golden fixtures (the reference
     statement, tests/golden/make_golden.py) bit for bit, through one handle as the fixtures were made."""
