@@ -422,8 +422,10 @@ def odometry_leg(dev, lidar: str, B: int, seqs: int, frames: int, steps: int, wa
                  check: bool, cpu_seconds: float) -> dict:
     """configs[3] (HDL-64E) / VLP-16: end-to-end odometry of B independent sequences, one scan per
     sequence per step: IP + feature stage + scan-to-scan LM + integrateTransformation + the next
-    last clouds, all on the device (llsr_odometry_batch). `seqs` distinct synthetic sequences of
-    `frames` consecutive scans (0.5 m apart) are tiled over the slots and replayed in a loop."""
+    last clouds, all on the device (llsr_odometry_batch). `seqs` distinct synthetic drives of
+    `frames` consecutive scans (0.5 m apart, the sensor moving in 6 DoF: synth.sensor_attitude) are
+    tiled over the slots; `frames` covers the warm-up, timed and profiled steps, so every measured
+    step is a real frame-to-frame transition."""
     import torch
     from llsr import Pipeline, _abi, default_config, synth
     from llsr.dist import max_over_ranks
@@ -990,7 +992,9 @@ def main():
     odo = {}
     for spec in [x for x in args.odo.split(",") if x]:
         lid, nb = spec.split(":")
-        odo[lid] = odometry_leg(dev, lid, int(nb), 2, 4, args.s2m_steps, 2, dist,
+        # frames: one continuous drive through warm-up, timed and profiled steps (no replay jump
+        # from the last frame back to the first inside the measured region)
+        odo[lid] = odometry_leg(dev, lid, int(nb), 2, 2 + args.s2m_steps + 2 + 1, args.s2m_steps, 2, dist,
                                 rank == 0 and not args.no_cpu and world == 1, min(args.cpu_seconds, 10.0))
 
     pc2 = pc2_decode_leg(dev, pts, off, args.s2m_steps * 4, dist) if args.pc2 else None

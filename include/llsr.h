@@ -188,6 +188,31 @@ int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const int64_t* d
 /* Copy slot b's results of the last batch into host buffers (synchronises the stream). */
 int32_t llsr_fetch_scan(llsr_handle* h, int32_t b, llsr_scan_out* out);
 
+/* ImageProjection's visualization topics for slot b of the last batch (publishClouds,
+ * imageProjection.cpp:933-967), built on the device from the slot's range image, kept points,
+ * ground and label images, then copied to the caller's host buffers (each may be NULL: skipped):
+ *   full_cloud / full_info_cloud  [H*W][4]  /full_cloud_projected, /full_cloud_info: per cell
+ *       x, y, z with intensity row + col / 1e4 resp. the range (IP:337-347); resetParameters'
+ *       nanPoint (NaN x, y, z, intensity 0) where no point landed (IP:170-179)
+ *   ground / nonground / unknownground_cloud  [<= H*W][4]  the full-cloud points of the cells
+ *       whose final ground_mat is 1 / 0 / 2, row-major (IP:760-769)
+ *   segmented_cloud_pure  [<= H*W][4]  cells with 0 < label != 999999, intensity = label,
+ *       row-major (IP:833-842)
+ * The n_* fields receive the four clouds' sizes. Synchronises. */
+typedef struct llsr_vis_out {
+  float* full_cloud;
+  float* full_info_cloud;
+  float* ground_cloud;
+  float* nonground_cloud;
+  float* unknownground_cloud;
+  float* segmented_cloud_pure;
+  int32_t n_ground;
+  int32_t n_nonground;
+  int32_t n_unknownground;
+  int32_t n_segmented_pure;
+} llsr_vis_out;
+int32_t llsr_fetch_vis_clouds(llsr_handle* h, int32_t b, llsr_vis_out* out);
+
 /* Device-side counters of the last batch: per slot {n_points, S, O, M, n_sharp, F, L, K}.
  * `out` must hold 8*B int32 (host). Synchronises. */
 int32_t llsr_batch_counts(llsr_handle* h, int32_t* out);

@@ -34,6 +34,7 @@ __global__ void k_select_ring(DevCfg, DevBufs);
 __global__ void k_debug_exact_sort(const float*, int, int*);
 __global__ void k_fa_concat(DevCfg, DevBufs);
 __global__ void k_dbscan_adj(DevCfg, DevBufs);
+__global__ void k_vis_clouds(DevCfg, DevBufs, int, float4*, int*);
 template <int kDbL> __global__ void k_dbscan_merge(DevCfg, DevBufs);
 
 __global__ void k_init_counts(int* counts, int B) {
@@ -64,6 +65,7 @@ struct llsr_handle {
   void* pool = nullptr;
   size_t pool_bytes = 0;
   float4* d_in = nullptr;      // single-scan staging
+  float4* d_vis = nullptr;     // llsr_fetch_vis_clouds: 6 x HW points + 4 counts (on first use)
   int64_t* d_off = nullptr;
   hipStream_t stream = nullptr;
   hipStream_t last_stream = nullptr;  // compared, never used: the caller may destroy its streams
@@ -100,6 +102,7 @@ struct llsr_handle {
   // scan-to-scan (llsr_scan2scan_*)
   struct {
     int P = 0, ms = 0, f = 0, nc = 0, ns = 0;
+    int launch_ms = 0, launch_f = 0, launch_nc = 0;  // the next launch's largest clouds (0: unknown)
     void* pool = nullptr;
     S2SArgs a{};
     int* host_flag = nullptr;
@@ -240,7 +243,8 @@ static void make_devcfg(const llsr_config& c, DevCfg& d) {
   d.gnd_cos[1] = llsr_libm::ground_cos_threshold(60.0f);
   d.gnd_cos[2] = llsr_libm::ground_cos_threshold(25.0f);
   d.ccl_lds = (d.H <= 16 && d.HW <= 32000) ? 1 : 0;
-  d.lbl_band = std::max(1, std::min(d.H, 36864 / std::max(1, d.W)));
+  // 72 KB bands: two labelling workgroups per CU (a 512-scan HDL-64E batch runs in one round)
+  d.lbl_band = std::max(1, std::min(d.H, 18432 / std::max(1, d.W)));
   d.dbg_phase = 1 << 30;
 }
 
@@ -390,6 +394,7 @@ extern "C" void llsr_destroy(llsr_handle* h) {
   for (hipEvent_t e : {h->last_done, h->s2s_done, h->mo_done})
     if (e) (void)hipEventDestroy(e);
   if (h->pool) (void)hipFree(h->pool);
+  if (h->d_vis) (void)hipFree(h->d_vis);
   if (h->mo.pool) (void)hipFree(h->mo.pool);
   if (h->s2s.pool) (void)hipFree(h->s2s.pool);
   if (h->s2s.stage) (void)hipFree(h->s2s.stage);
@@ -750,6 +755,32 @@ extern "C" int32_t llsr_fetch_scan(llsr_handle* h, int32_t b, llsr_scan_out* o) 
   HIP_OK(h, d2h(o->sharp_ind, h->d.sharp + base, o->n_sharp));
   HIP_OK(h, d2h(o->flat_ind, h->d.flat + base, o->n_flat));
   HIP_OK(h, d2h(o->less_flat_xyzi, (const float*)(h->d.lflat + base), 4 * (size_t)o->n_less_flat));
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_fetch_vis_clouds(llsr_handle* h, int32_t b, llsr_vis_out* o) {
+  if (!h || !o) return LLSR_EINVAL;
+  if (b < 0 || b >= h->last_B) return fail(h, LLSR_ERANGE, "slot outside last batch");
+  int32_t rc = sync_last(h);
+  if (rc) return rc;
+  const DevCfg& c = h->dc;
+  const size_t HW = (size_t)c.HW;
+  if (!h->d_vis) HIP_OK(h, hipMalloc(&h->d_vis, sizeof(float4) * (6 * HW + 1)));
+  int* d_cnt = reinterpret_cast<int*>(h->d_vis + 6 * HW);
+  k_vis_clouds<<<1, 1024, 0, h->stream>>>(c, h->d, b, h->d_vis, d_cnt);
+  HIP_OK(h, hipGetLastError());
+  HIP_OK(h, hipStreamSynchronize(h->stream));
+  int cnt[4];
+  HIP_OK(h, d2h(cnt, d_cnt, 4));
+  o->n_ground = cnt[0];
+  o->n_nonground = cnt[1];
+  o->n_unknownground = cnt[2];
+  o->n_segmented_pure = cnt[3];
+  float* dst[6] = {o->full_cloud, o->full_info_cloud, o->ground_cloud, o->nonground_cloud, o->unknownground_cloud,
+                   o->segmented_cloud_pure};
+  const size_t n[6] = {HW, HW, (size_t)cnt[0], (size_t)cnt[1], (size_t)cnt[2], (size_t)cnt[3]};
+  for (int k = 0; k < 6; ++k)
+    if (dst[k] && n[k]) HIP_OK(h, d2h(dst[k], (const float*)(h->d_vis + k * HW), 4 * n[k]));
   return LLSR_OK;
 }
 
@@ -1222,8 +1253,15 @@ extern "C" int32_t llsr_scan2scan_batch(llsr_handle* h, const llsr_s2s_batch* b,
   if (h->profiling) HIP_OK(h, hipEventRecord(m.p1, s));
   // the small-LDS instantiation (4 workgroups per CU instead of 2) when every problem's queries
   // and corner-last cloud fit it (reserved capacities are the batch maxima)
-  if (m.ms <= 1024 && m.f <= 1024 && m.nc <= 1024)
+  // bounds: this launch's largest clouds when the caller knows them (the odometry chain), else
+  // the reserved capacities
+  const int bq = std::max(m.launch_ms > 0 ? m.launch_ms : m.ms, m.launch_f > 0 ? m.launch_f : m.f);
+  const int bnc = m.launch_nc > 0 ? m.launch_nc : m.nc;
+  m.launch_ms = m.launch_f = m.launch_nc = 0;
+  if (bq <= 1024 && bnc <= 1024)
     k_s2s_lm<1024, 1024><<<P, kS2SThreads, 0, s>>>(a);
+  else if (bq <= 2560 && bnc <= 1536)
+    k_s2s_lm<2560, 1536><<<P, kS2SThreads, 0, s>>>(a);
   else
     k_s2s_lm<2048, 2048><<<P, kS2SThreads, 0, s>>>(a);
   HIP_OK(h, hipGetLastError());
@@ -1439,6 +1477,9 @@ extern "C" int32_t llsr_odometry_batch(llsr_handle* h, const float* d_xyzi, cons
   HIP_OK(h, hipMemcpyAsync(o.off + (4 + nxt) * nb, hns, sizeof(int64_t) * nb, hipMemcpyHostToDevice, s));
   rc = llsr_scan2scan_reserve(h, o.B, mMs > 1 ? mMs : 1, mF, mNc > 1 ? mNc : 1, mNs > 1 ? mNs : 1);
   if (rc != LLSR_OK) return rc;
+  h->s2s.launch_ms = mMs > 1 ? mMs : 1;  // the LM instantiation follows this batch, not the reserve
+  h->s2s.launch_f = mF > 1 ? mF : 1;
+  h->s2s.launch_nc = mNc > 1 ? mNc : 1;
   OdoArgs a{};
   a.B = B;
   a.HW = h->dc.HW;

@@ -37,7 +37,7 @@ struct DevCfg {
   float fa_resY, sinResX, RatioXY, RatioZ, DBFr;
   float gnd_cos[3];  // ground angle test thresholds on the cosine for D = 12.5, 60, 25 deg (llsr_libm.h)
   int ccl_lds;  // union-find parent array fits LDS (H <= 16 && HW <= 32000)
-  int lbl_band; // otherwise: rows per LDS union-find band of k_label<false> (band * W ints <= 144 KB)
+  int lbl_band; // otherwise: rows per LDS union-find band of k_label<false> (band * W ints <= 72 KB: two workgroups per CU)
   int exact_vg;   // LLSR_VOXEL_ORDER_PCL: the less-flat VoxelGrid sums in std::sort's tie order
   int dbg_phase;  // diagnostics only: kernels return at phase boundary >= dbg_phase (default: never)
 };

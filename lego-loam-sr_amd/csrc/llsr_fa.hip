@@ -916,28 +916,49 @@ __device__ __forceinline__ bool db_near_fast(const DevCfg& c, float4 pi, float4 
 }
 
 // ---------------------------------------------------------------------------------------------
-// K9b eps-neighbourhood bitmask for every (i, j) of a scan (M <= kAdjCap): one wave evaluates
-// 64 consecutive j of one row i and stores the ballot as two words. Massively parallel; this
-// takes the O(M^2) float work off DBSCAN's serial merge. grid (32, B), block 256.
+// K9b eps-neighbourhood bitmask for every (i, j) of a scan (M <= kAdjCap). A wave task is 64
+// consecutive j (one per lane) against kAdjRows consecutive rows i: the lane's point j, the two
+// hardware reciprocals of its scales and the fast path's eligibility are computed once per task,
+// then each row costs a wave-uniform load of point i, the scaled distance and a ballot stored as
+// two words. Decisions are db_near_fast's (the same reciprocals, the same float expression, the
+// exact db_near inside the band). Takes the O(M^2) float work off DBSCAN's serial merge.
+// grid (32, B), block 256.
 // ---------------------------------------------------------------------------------------------
+constexpr int kAdjRows = 16;
+
 __global__ __launch_bounds__(256) void k_dbscan_adj(DevCfg c, DevBufs d) {
   const int b = blockIdx.y;
   const size_t base = (size_t)b * c.HW;
   const int M = d.counts[b * kCnt + C_M];
   if (M > kAdjCap) return;
-  const int nch = (M + 63) / 64;
-  const int wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nch = (M + 63) / 64, ngr = (M + kAdjRows - 1) / kAdjRows;
+  const int wv = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   const int nwv = (gridDim.x * blockDim.x) >> 6;
   const int l = lane_id();
   uint32_t* adj = d.db_adj + (size_t)b * kAdjCap * kAdjWords;
-  for (int task = wv; task < M * nch; task += nwv) {
-    const int i = task / nch, ch = task - i * nch;
+  const float4* pts = d.db_pts + base;
+  const float r2 = c.DBFr * c.DBFr, lo = r2 * (1.0f - 2e-5f), hi = r2 * (1.0f + 2e-5f);
+  for (int task = wv; task < nch * ngr; task += nwv) {
+    const int ch = task % nch, i0 = (task / nch) * kAdjRows;
     const int j = ch * 64 + l;
-    bool nb = false;
-    if (j < M) nb = db_near_fast(c, d.db_pts[base + i], d.db_pts[base + j], d.db_kz[base + j]);
-    const unsigned long long m = __ballot(nb);
-    if (l == 0) adj[(size_t)i * kAdjWords + 2 * ch] = (uint32_t)m;
-    if (l == 1 && 2 * ch + 1 < kAdjWords) adj[(size_t)i * kAdjWords + 2 * ch + 1] = (uint32_t)(m >> 32);
+    const bool inj = j < M;
+    const float4 pj = inj ? pts[j] : make_float4(0.f, 0.f, 0.f, 1.f);
+    const float kz = inj ? d.db_kz[base + j] : 1.0f;
+    const float k2 = pj.w * pj.w, z2 = kz * kz;
+    const bool fast = c.DBFr > 0.0f && k2 > 1e-30f && k2 < 1e30f && z2 > 1e-30f && z2 < 1e30f;
+    const float rk = __builtin_amdgcn_rcpf(k2), rz = __builtin_amdgcn_rcpf(z2);
+    const int i1 = i0 + kAdjRows < M ? i0 + kAdjRows : M;
+    for (int i = i0; i < i1; ++i) {
+      const float4 pi = pts[i];  // wave-uniform
+      const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
+      const float s = (dx * dx + dy * dy) * rk + dz * dz * rz;
+      bool nb = fast && s < lo;
+      if (inj && !(fast && (s < lo || s > hi))) nb = db_near(c, pi, pj, kz);
+      nb = nb && inj;
+      const unsigned long long m = __ballot(nb);
+      if (l == 0) adj[(size_t)i * kAdjWords + 2 * ch] = (uint32_t)m;
+      if (l == 1 && 2 * ch + 1 < kAdjWords) adj[(size_t)i * kAdjWords + 2 * ch + 1] = (uint32_t)(m >> 32);
+    }
   }
 }
 

@@ -346,6 +346,116 @@ __device__ void surf_finish(const float4* sl, const float4* box, const float4* b
   i3 = b3;
 }
 
+__device__ __forceinline__ float readlane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// surf_finish for the queries of one wave, walked by the whole wave one query at a time (every lane
+// of the wave calls it; `act` marks a lane holding a query). A walk visits 64 points at once, lane
+// order = walk order: the first lane meeting a ring outside the band ends the walk (lanes after it
+// are not visited), and the lowest lane of the chunk's minimum is the serial loop's first strict
+// '<' minimum (an earlier chunk's equal minimum is kept). Whole 64-point superblocks are tested 64
+// at a time, one per lane, against the current minima; skipping is only ever a shortcut (a block
+// whose box cannot beat the minimum it would be tested against and that holds no stop changes
+// nothing), so the result is the serial loop's.
+__device__ void surf_finish_wave(const float4* sl, const float4* box2, int end, float4 sel, float dist_sqr, bool act,
+                                 int nn, float nd, int& i1, int& i2, int& i3) {
+  const bool walk = act && nd < dist_sqr;
+  i1 = walk ? nn : -1;
+  i2 = -1;
+  i3 = -1;
+  const int lane = lane_id();
+  uint64_t pend = __ballot(walk);
+  while (pend) {
+    const int l = __builtin_ctzll(pend);
+    pend &= pend - 1;
+    const float4 q = make_float4(readlane_f(sel.x, l), readlane_f(sel.y, l), readlane_f(sel.z, l), 0.0f);
+    const int n0 = __builtin_amdgcn_readlane(nn, l);
+    const int cs = trunc_i32(sl[n0].w);
+    float m2 = dist_sqr, m3 = dist_sqr;
+    int b2 = -1, b3 = -1;
+    // one chunk: lane -> index idx (valid when `in`); true when the walk stops in it
+    auto visit = [&](int idx, bool in, bool up) {
+      const float4 c = in ? sl[idx] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int r = trunc_i32(c.w);
+      const bool st = in && (up ? (double)r > (double)cs + 2.5 : (double)r < (double)cs - 2.5);
+      const uint64_t sm = __ballot(st);
+      const bool v = in && (sm == 0 || lane < __builtin_ctzll(sm));
+      const float d = sqdis(c, q);
+      const bool same = up ? r <= cs : r >= cs;
+      const float d2 = v && same && d < m2 ? d : INFINITY;
+      const float d3 = v && !same && d < m3 ? d : INFINITY;
+      const float x2 = wave_reduce_min(d2), x3 = wave_reduce_min(d3);
+      if (x2 < m2) {
+        m2 = x2;
+        b2 = __builtin_amdgcn_readlane(idx, __builtin_ctzll(__ballot(d2 == x2)));
+      }
+      if (x3 < m3) {
+        m3 = x3;
+        b3 = __builtin_amdgcn_readlane(idx, __builtin_ctzll(__ballot(d3 == x3)));
+      }
+      return sm != 0;
+    };
+    auto bound_up = [&](float rlo, float rhi) { return rhi <= (float)cs ? m2 : rlo > (float)cs ? m3 : fmaxf(m2, m3); };
+    auto bound_dn = [&](float rlo, float rhi) { return rlo >= (float)cs ? m2 : rhi < (float)cs ? m3 : fmaxf(m2, m3); };
+    // up-walk n0 + 1 .. end - 1: the head up to a superblock boundary, then superblocks
+    int j = n0 + 1;
+    bool stop = false;
+    const int hend = min((j + 63) & ~63, end);
+    if (j < hend) {
+      stop = visit(j + lane, j + lane < hend, true);
+      j = hend;
+    }
+    while (!stop && j < end) {
+      const int j0 = j, sb = (j0 >> 6) + lane;
+      const bool full = (sb + 1) * 64 <= end;
+      float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
+      if (full) { lo = box2[2 * sb]; hi = box2[2 * sb + 1]; }
+      const bool nostop = full && (double)(int)hi.w <= (double)cs + 2.5;
+      int f0 = 0;
+      for (;;) {
+        const bool skip = nostop && box_lb(lo, hi, q) >= bound_up(lo.w, hi.w);
+        const uint64_t need = __ballot(!skip) & (~0ull << f0);
+        if (!need) { j = j0 + 64 * 64; break; }
+        const int f = __builtin_ctzll(need), base = j0 + 64 * f;
+        if (base >= end) { j = end; break; }
+        stop = visit(base + lane, base + lane < end, true);
+        if (stop || f == 63) { j = base + 64; break; }
+        f0 = f + 1;
+      }
+    }
+    // down-walk n0 - 1 .. 0: the head down to a superblock's first index, then superblocks
+    j = n0 - 1;
+    stop = false;
+    if (j >= 0 && (j & 63) != 63) {
+      const int hlo = j & ~63;
+      stop = visit(j - lane, j - lane >= hlo, false);
+      j = hlo - 1;
+    }
+    while (!stop && j >= 0) {
+      const int j0 = j, sb = (j0 >> 6) - lane;  // superblock [64 sb, 64 sb + 63]
+      float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
+      if (sb >= 0) { lo = box2[2 * sb]; hi = box2[2 * sb + 1]; }
+      const bool nostop = sb >= 0 && (double)(int)lo.w >= (double)cs - 2.5;
+      int f0 = 0;
+      for (;;) {
+        const bool skip = nostop && box_lb(lo, hi, q) >= bound_dn(lo.w, hi.w);
+        const uint64_t need = __ballot(!skip) & (~0ull << f0);
+        if (!need) { j = j0 - 64 * 64; break; }
+        const int f = __builtin_ctzll(need), top = j0 - 64 * f;
+        if (top < 0) { j = -1; break; }
+        stop = visit(top - lane, true, false);
+        if (stop || f == 63) { j = top - 64; break; }
+        f0 = f + 1;
+      }
+    }
+    if (lane == l) {
+      i2 = b2;
+      i3 = b3;
+    }
+  }
+}
+
 // brute-force kNN-1 of J queries per thread over the LDS corner cloud (index order, strict '<')
 template <int J>
 __device__ __forceinline__ void corner_brute(const float4* cl, int Nc, const float4* qs, float* bd, int* bi) {
@@ -534,8 +644,10 @@ __global__ void k_s2s_boxes(S2SArgs a) {
 
 // kLdsRows: Jacobian rows kept in LDS (16 B each; larger phases use the HBM buffer); kLdsCorner:
 // laserCloudCornerLast kept in LDS for a brute-force kNN-1 (larger clouds use the cell grid).
-// Two instantiations (llsr_s2s.h): 2048 / 2048 (70 KB, 2 workgroups per CU) and 1024 / 1024
-// (35 KB, 4 per CU) for batches whose queries and corner clouds fit it.
+// Three instantiations (llsr_s2s.h), chosen per launch from the batch's largest clouds: 1024 / 1024
+// (39 KB, 4 workgroups per CU: VLP-16-sized scans), 2560 / 1536 (78 KB, 2 per CU: HDL-64E, whose
+// ~2.1-2.2k flat queries would otherwise sum their rows from HBM every surf iteration) and
+// 2048 / 2048 (77 KB) otherwise.
 template <int kLdsRows, int kLdsCorner>
 __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
   const int p = blockIdx.x;
@@ -551,6 +663,9 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
   __shared__ uint8_t lvalid[kLdsRows];
   __shared__ uint16_t lvix[kLdsRows];  // phase B: the rows holding a correspondence, in order
   __shared__ float4 lcl[kLdsCorner];
+  // the large instantiations (HDL-64E-sized clouds) take the whole-wave surf walks; the 1024 /
+  // 1024 one keeps the per-lane walks, faster on VLP-16 clouds
+  constexpr bool kBig = kLdsRows > 1024;
   __shared__ int fbq[kFbMax], nfb, nvalid, nrow;
   __shared__ float bpart[5][12];  // phase B: per-depth-block AtA partial sums
   __shared__ float red_d[kMulti][kThreads / 64];
@@ -577,8 +692,9 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
   if (!skipped) {
     const bool corner_lds = Nc <= kLdsCorner;
     const float4* clg = gc.src + gc.off[p];
-    if (corner_lds)  // visible to every thread after the barrier at the top of the first phase
+    if (corner_lds) {  // visible to every thread after the barrier at the top of the first phase
       for (int k = tid; k < Nc; k += kThreads) lcl[k] = clg[k];
+    }
     const float4* sl = gs.src + gs.off[p];
     const float4* sbox = a.sbox + (size_t)p * ((gs.cap + 7) / 8) * 2;
     const float4* sbox2 = a.sbox2 + (size_t)p * ((gs.cap + 63) / 64) * 2;
@@ -651,10 +767,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
               const int wq = Q - (q0 - lane_id());
               const int nj = wq > 3 * kThreads ? 4 : wq > 2 * kThreads ? 3 : wq > kThreads ? 2 : 1;
               if (nj == 1) corner_brute<1>(lcl, Nc, qs, bd, bi);
-              else if constexpr (kMulti == 2) corner_brute<2>(lcl, Nc, qs, bd, bi);
-              else if (nj == 2) corner_brute<2>(lcl, Nc, qs, bd, bi);
-              else if (nj == 3) corner_brute<3>(lcl, Nc, qs, bd, bi);
-              else corner_brute<4>(lcl, Nc, qs, bd, bi);
+              else corner_brute<2>(lcl, Nc, qs, bd, bi);
 #pragma unroll
               for (int j = 0; j < kMulti; ++j)
                 if (q0 + j * kThreads < Q) park(q0 + j * kThreads, bi[j], bd[j]);
@@ -698,9 +811,30 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
           __syncthreads();
           if (surf) LLSR_STAMP(tAks);
           else LLSR_STAMP(tAkc);
-          for (int q = tid; q < Q; q += kThreads) {
-            const int* ix = idx + 3 * q;
-            finish(q, to_start(tl, qry[q]), ix[0], __int_as_float(ix[1]));
+          if constexpr (surf && kBig) {
+            // the whole wave walks each of its lanes' queries in turn (uniform trip count): for the
+            // long HDL-64E surf clouds, whose walks leave most lanes of a per-lane walk idle
+            for (int q0 = 0; q0 < Q; q0 += kThreads) {
+              const int q = q0 + tid;
+              const bool act = q < Q;
+              int* ix = idx + 3 * (act ? q : 0);
+              int nn = -1;
+              float nd = INFINITY;
+              float4 sel = make_float4(0.f, 0.f, 0.f, 0.f);
+              if (act) {
+                nn = ix[0];
+                nd = __int_as_float(ix[1]);
+                sel = to_start(tl, qry[q]);
+              }
+              int i1, i2, i3;
+              surf_finish_wave(sl, sbox2, F < Ns ? F : Ns, sel, a.dist_sqr, act, nn, nd, i1, i2, i3);
+              if (act) { ix[0] = i1; ix[1] = i2; ix[2] = i3; }
+            }
+          } else {
+            for (int q = tid; q < Q; q += kThreads) {
+              const int* ix = idx + 3 * q;
+              finish(q, to_start(tl, qry[q]), ix[0], __int_as_float(ix[1]));
+            }
           }
           __syncthreads();
           if (surf) LLSR_STAMP(tW);
@@ -934,6 +1068,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
 }
 
 template __global__ void k_s2s_lm<2048, 2048>(S2SArgs);
+template __global__ void k_s2s_lm<2560, 1536>(S2SArgs);
 template __global__ void k_s2s_lm<1024, 1024>(S2SArgs);
 
 }  // namespace llsr

@@ -17,25 +17,47 @@ __global__ void k_grid_clear(CellGrids2 gg) {
   t.count = 0;
 }
 
+// Consecutive points of a cloud often share a cell (scan order, VoxelGrid order), so lanes of a
+// wave holding a run of equal keys insert once: the run's first lane probes / claims the slot and
+// takes the run's ranks with ONE count atomic; the others derive slot and rank from it.
 __global__ void k_grid_insert(CellGrids2 gg) {
   const CellGrid& g = gg.g[blockIdx.z];
   const int p = blockIdx.y;
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= g.count(p)) return;
-  const float4 q = g.src[g.off[p] + k];
-  const uint64_t key = cell_key(cell_coord(q.x), cell_coord(q.y), cell_coord(q.z));
-  CellSlot* tab = g.tab + ((size_t)p << g.log2T);
-  const uint32_t mask = (1u << g.log2T) - 1u;
-  uint32_t s = cell_hash(key, g.log2T);
-  for (;;) {  // a plain load first: most cells already exist (a few points per cell)
-    uint64_t kk = __hip_atomic_load((unsigned long long*)&tab[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (kk == kCellEmpty)
-      kk = atomicCAS((unsigned long long*)&tab[s].key, (unsigned long long)kCellEmpty, (unsigned long long)key);
-    if (kk == kCellEmpty || kk == key) break;
-    s = (s + 1) & mask;
+  const int n = g.count(p);
+  if ((int)(blockIdx.x * blockDim.x) >= n) return;  // block-uniform: every lane of a live wave stays
+  const bool in = k < n;
+  uint64_t key = kCellEmpty;
+  if (in) {
+    const float4 q = g.src[g.off[p] + k];
+    key = cell_key(cell_coord(q.x), cell_coord(q.y), cell_coord(q.z));
   }
-  const int rank = atomicAdd(&tab[s].count, 1);
-  g.where[(size_t)p * g.cap + k] = make_int2((int)s, rank);
+  const int l = lane_id();
+  const uint64_t prev = __shfl_up(key, 1, 64);
+  const bool head = in && (l == 0 || prev != key);
+  const unsigned long long heads = __ballot(head);
+  const unsigned long long live = __ballot(in);
+  const int start = 63 - __clzll((long long)(heads & ((2ull << l) - 1ull)));  // this lane's run head
+  int s = 0, base = 0;
+  if (head) {
+    const unsigned long long after = heads & ~((2ull << l) - 1ull);
+    const int end = after ? __ffsll((long long)after) - 1 : 64 - __clzll((long long)live);
+    CellSlot* tab = g.tab + ((size_t)p << g.log2T);
+    const uint32_t mask = (1u << g.log2T) - 1u;
+    uint32_t h = cell_hash(key, g.log2T);
+    for (;;) {  // a plain load first: most cells already exist (a few points per cell)
+      uint64_t kk = __hip_atomic_load((unsigned long long*)&tab[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (kk == kCellEmpty)
+        kk = atomicCAS((unsigned long long*)&tab[h].key, (unsigned long long)kCellEmpty, (unsigned long long)key);
+      if (kk == kCellEmpty || kk == key) break;
+      h = (h + 1) & mask;
+    }
+    s = (int)h;
+    base = atomicAdd(&tab[h].count, end - l);
+  }
+  s = __shfl(s, start, 64);
+  base = __shfl(base, start, 64);
+  if (in) g.where[(size_t)p * g.cap + k] = make_int2(s, base + (l - start));
 }
 
 __global__ __launch_bounds__(256) void k_grid_alloc(CellGrids2 gg) {

@@ -166,89 +166,6 @@ __global__ __launch_bounds__(256) void k_project(DevCfg c, const float4* __restr
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// K2 gather + ground column pass: builds range_mat/full_cloud for each cell (IP:337-347,
-// resetParameters IP:170-179) and runs groundRemovalOurs' per-column vector test and Filter
-// (IP:524-629) in the same sweep. One thread per (scan, column), rows bottom-up. The wave's 64
-// columns of k_project's column-major winner table are one contiguous run of 64 * H ints: loaded
-// coalesced into LDS (column stride H + 1 against bank conflicts), then read per column; the
-// row-major cell->point map is written here.
-// grid (ceil(W/64), B), block 64, dynamic LDS 64 * (H + 1) ints.
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_gather_column(DevCfg c, const float4* __restrict__ pts,
-                                                      const int64_t* __restrict__ off, DevBufs d) {
-  extern __shared__ int lwin[];
-  const int b = blockIdx.y;
-  const int j0 = blockIdx.x * blockDim.x;
-  const int j = j0 + threadIdx.x;
-  const int64_t o0 = off[b];
-  const size_t base = (size_t)b * c.HW;
-  {
-    const int ncol = min(64, c.W - j0);
-    const int* src = d.ccl_a + base + (size_t)j0 * c.H;  // columns j0 .. j0 + ncol - 1, row 0 first
-    for (int t = threadIdx.x; t < ncol * c.H; t += 64) {
-      const int cj = t / c.H, ci = t - cj * c.H;
-      lwin[cj * (c.H + 1) + ci] = src[t];
-    }
-  }
-  __syncthreads();
-  if (j >= c.W) return;
-  const int* colw = lwin + threadIdx.x * (c.H + 1);  // this column's winners, row 0 first
-  const float qnan = __builtin_nanf("");
-  bool haveRV = false, obs = false;
-  float RVx = 0.f, RVy = 0.f, RVz = 0.f;
-  float lx = 0.f, ly = 0.f, lz = 0.f;
-  for (int i = 0; i < c.H; ++i) {
-    const int cell = j + i * c.W;
-    const int pi = colw[i];
-    d.cell_pt[base + cell] = pi;
-    float4 f;
-    float rng;
-    if (pi >= 0) {
-      const float4 p = pts[o0 + pi];
-      rng = sqrt_(p.x * p.x + p.y * p.y + p.z * p.z);
-      f = make_float4(p.x, p.y, p.z, cell_intensity(c.H, c.W, i, j));
-    } else {
-      rng = FLT_MAX;
-      f = make_float4(qnan, qnan, qnan, 0.0f);
-    }
-    d.range[base + cell] = rng;
-    d.full[base + cell] = pi >= 0 ? pts[o0 + pi] : make_float4(qnan, qnan, qnan, 0.0f);
-    int8_t g;
-    if (f.w == 0.0f) {
-      g = -1;  // IP:535: NaN cells (and a real point at row 0, col 0) have intensity 0
-    } else if (!haveRV) {
-      const float d0 = sqrt_(f.x * f.x + f.y * f.y);
-      RVx = f.x / d0; RVy = f.y / d0; RVz = 0.0f;
-      haveRV = true;
-      lx = f.x; ly = f.y; lz = f.z;
-      g = 1;
-    } else {
-      const float TVx = f.x - lx, TVy = f.y - ly, TVz = f.z - lz;
-      // (float)(acosf(x) / deg) <= D  <=>  gnd_cos(D) <= x <= 1  (llsr_libm.h ground_cos_threshold)
-      const float x = (TVx * RVx + TVy * RVy + TVz * RVz) /
-                      (sqrt_(TVx * TVx + TVy * TVy + TVz * TVz) * sqrt_(RVx * RVx + RVy * RVy + RVz * RVz));
-      const float xs = c.use_kitti ? (i < 16 ? c.gnd_cos[1] : c.gnd_cos[2]) : c.gnd_cos[0];
-      if (x >= xs && x <= 1.0f) { RVx += TVx; RVy += TVy; RVz += TVz; g = 1; }
-      else g = 0;
-      lx = f.x; ly = f.y; lz = f.z;
-    }
-    // Filter (IP:620-628): after the first 0 of the column every 1 becomes 2.
-    if (g == 0) obs = true;
-    else if (g == 1 && obs) g = 2;
-    d.ground[base + cell] = g;
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// K1+K2 fused for range images that fit LDS (H <= 16, H*W <= 32000, e.g. VLP-16): one workgroup per scan.
-// The claim pass projects every raw point once (coalesced reads) and resolves IP:337-347's serial
-// "last writer wins" with an LDS atomicMax of the raw index per cell, each cell's winner writing its
-// range and its raw point (x, y, z, raw intensity: fullCloud with the intensity row + col / 1e4
-// derived where needed, cell_intensity); a sweep of the final winner table writes the cell ->
-// point map and the resetParameters values of empty cells (IP:170-179); the per-column ground test
-// + Filter (IP:524-629) reads the kept points back. No global atomics.
-// ---------------------------------------------------------------------------------------------
 // groundRemovalOurs' per-column test (IP:524-629) as a step over one column's state, so a lane can
 // carry two columns at once: their serial 16-row chains interleave (ILP) instead of running in two
 // rounds of lanes.
@@ -283,6 +200,72 @@ __device__ __forceinline__ int8_t ground_step(const DevCfg& c, GndState& st, flo
   return g;
 }
 
+// ---------------------------------------------------------------------------------------------
+// K2 gather + ground column pass: builds range_mat/full_cloud for each cell (IP:337-347,
+// resetParameters IP:170-179) and runs groundRemovalOurs' per-column vector test and Filter
+// (IP:524-629) in the same sweep. One thread per (scan, column), rows bottom-up. The wave's 64
+// columns of k_project's column-major winner table are one contiguous run of 64 * H ints: loaded
+// coalesced into LDS (column stride H + 1 against bank conflicts), then read per column; the
+// row-major cell->point map is written here.
+// grid (ceil(W/64), B), block 64, dynamic LDS 64 * (H + 1) ints.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_gather_column(DevCfg c, const float4* __restrict__ pts,
+                                                      const int64_t* __restrict__ off, DevBufs d) {
+  extern __shared__ int lwin[];
+  const int b = blockIdx.y;
+  const int j0 = blockIdx.x * blockDim.x;
+  const int j = j0 + threadIdx.x;
+  const int64_t o0 = off[b];
+  const size_t base = (size_t)b * c.HW;
+  {
+    const int ncol = min(64, c.W - j0);
+    const int* src = d.ccl_a + base + (size_t)j0 * c.H;  // columns j0 .. j0 + ncol - 1, row 0 first
+    for (int t = threadIdx.x; t < ncol * c.H; t += 64) {
+      const int cj = t / c.H, ci = t - cj * c.H;
+      lwin[cj * (c.H + 1) + ci] = src[t];
+    }
+  }
+  __syncthreads();
+  if (j >= c.W) return;
+  const int* colw = lwin + threadIdx.x * (c.H + 1);  // this column's winners, row 0 first
+  const float qnan = __builtin_nanf("");
+  GndState st;
+  // rows in groups of kR: the group's winner points are gathered with all loads in flight, then
+  // the column's serial ground chain runs over them (one load latency per group, not per row)
+  constexpr int kR = 8;
+  for (int i0 = 0; i0 < c.H; i0 += kR) {
+    float4 pg[kR];
+    int wg[kR];
+#pragma unroll
+    for (int u = 0; u < kR; ++u) {
+      wg[u] = i0 + u < c.H ? colw[i0 + u] : -1;
+      pg[u] = wg[u] >= 0 ? pts[o0 + wg[u]] : make_float4(qnan, qnan, qnan, 0.0f);
+    }
+#pragma unroll
+    for (int u = 0; u < kR; ++u) {
+      const int i = i0 + u;
+      if (i >= c.H) break;
+      const int cell = j + i * c.W;
+      const float4 p = pg[u];
+      d.cell_pt[base + cell] = wg[u];
+      d.range[base + cell] = wg[u] >= 0 ? sqrt_(p.x * p.x + p.y * p.y + p.z * p.z) : FLT_MAX;
+      d.full[base + cell] = p;
+      // IP:535: NaN cells (and a real point at row 0, col 0) have intensity 0
+      const float w = wg[u] >= 0 ? cell_intensity(c.H, c.W, i, j) : 0.0f;
+      d.ground[base + cell] = ground_step(c, st, make_float4(p.x, p.y, p.z, w), i);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1+K2 fused for range images that fit LDS (H <= 16, H*W <= 32000, e.g. VLP-16): one workgroup per scan.
+// The claim pass projects every raw point once (coalesced reads) and resolves IP:337-347's serial
+// "last writer wins" with an LDS atomicMax of the raw index per cell, each cell's winner writing its
+// range and its raw point (x, y, z, raw intensity: fullCloud with the intensity row + col / 1e4
+// derived where needed, cell_intensity); a sweep of the final winner table writes the cell ->
+// point map and the resetParameters values of empty cells (IP:170-179); the per-column ground test
+// + Filter (IP:524-629) reads the kept points back. No global atomics.
+// ---------------------------------------------------------------------------------------------
 // columns j0 and j1 (j1 >= W: none), their cells loaded 8 rows at a time ahead of the tests;
 // cellf(cell) = (x, y, z, w) with w == 0 exactly for the cells groundRemoval skips (IP:535)
 template <class CellF>

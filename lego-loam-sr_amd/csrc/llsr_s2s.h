@@ -34,6 +34,6 @@ __global__ void k_s2s_boxes(S2SArgs a);
 constexpr int kS2SThreads = 512;  // measured: 256 -> 512 HDL-64E LM 39.3 -> 32.6 ms, VLP-16 9.1 -> 8.4 ms; 1024 slower on VLP-16
 
 template <int kLdsRows, int kLdsCorner>
-__global__ void k_s2s_lm(S2SArgs a);
+__global__ void k_s2s_lm(S2SArgs a);  // instantiated for <1024, 1024>, <2560, 1536>, <2048, 2048>
 
 }  // namespace llsr

@@ -31,7 +31,7 @@ _LIB = None
 
 EXPORTS = [
     "llsr_abi_version", "llsr_build_id", "llsr_config_default", "llsr_get_config", "llsr_create", "llsr_destroy", "llsr_last_error", "llsr_query_sizes",
-    "llsr_reset_state", "llsr_process_scan", "llsr_process_batch", "llsr_fetch_scan",
+    "llsr_reset_state", "llsr_process_scan", "llsr_process_batch", "llsr_fetch_scan", "llsr_fetch_vis_clouds",
     "llsr_batch_counts", "llsr_kernel_times_ms", "llsr_kernel_name", "llsr_set_profiling",
     "llsr_scan2map_reserve", "llsr_scan2map_batch", "llsr_scan2map", "llsr_scan2map_stats",
     "llsr_shadow_points", "llsr_scan2scan_reserve", "llsr_scan2scan_batch", "llsr_scan2scan_check",
@@ -81,6 +81,7 @@ def lib():
         L.llsr_process_scan.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(_abi.ScanOut)]
         L.llsr_process_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
         L.llsr_fetch_scan.argtypes = [C.c_void_p, C.c_int32, C.POINTER(_abi.ScanOut)]
+        L.llsr_fetch_vis_clouds.argtypes = [C.c_void_p, C.c_int32, C.POINTER(_abi.VisOut)]
         L.llsr_batch_counts.argtypes = [C.c_void_p, C.c_void_p]
         L.llsr_kernel_times_ms.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         L.llsr_kernel_name.restype = C.c_char_p
@@ -209,6 +210,14 @@ class Pipeline:
     def fetch(self, b: int) -> dict:
         self._check(lib().llsr_fetch_scan(self._h, b, C.byref(self.out.struct)), "llsr_fetch_scan")
         return self.out.result()
+
+    def fetch_vis_clouds(self, b: int) -> dict:
+        """publishClouds' visualization clouds of slot b (llsr_fetch_vis_clouds): {name: float32 [n, 4]}."""
+        HW = self.cfg.num_vertical_scans * self.cfg.num_horizontal_scans
+        bufs = {name: np.zeros((HW, 4), np.float32) for name, _ in _abi.VIS_CLOUDS}
+        v = _abi.VisOut(*(bufs[name].ctypes.data for name, _ in _abi.VIS_CLOUDS))
+        self._check(lib().llsr_fetch_vis_clouds(self._h, b, C.byref(v)), "llsr_fetch_vis_clouds")
+        return {name: bufs[name][: (HW if cnt is None else getattr(v, cnt))].copy() for name, cnt in _abi.VIS_CLOUDS}
 
     def batch_counts(self, B: int) -> np.ndarray:
         buf = np.zeros((B, 8), dtype=np.int32)

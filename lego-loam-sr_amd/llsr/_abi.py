@@ -80,6 +80,18 @@ def config_for(lidar: str, horizontal: int | None = None) -> Config:
 _P = C.c_void_p
 
 
+class VisOut(C.Structure):
+    """llsr_vis_out (include/llsr.h): publishClouds' visualization clouds of one slot."""
+    _fields_ = [("full_cloud", _P), ("full_info_cloud", _P), ("ground_cloud", _P), ("nonground_cloud", _P),
+                ("unknownground_cloud", _P), ("segmented_cloud_pure", _P), ("n_ground", C.c_int32),
+                ("n_nonground", C.c_int32), ("n_unknownground", C.c_int32), ("n_segmented_pure", C.c_int32)]
+
+
+VIS_CLOUDS = [("full_cloud", None), ("full_info_cloud", None), ("ground_cloud", "n_ground"),
+              ("nonground_cloud", "n_nonground"), ("unknownground_cloud", "n_unknownground"),
+              ("segmented_cloud_pure", "n_segmented_pure")]
+
+
 class ScanOut(C.Structure):
     _fields_ = [
         ("n_points", C.c_int32),

@@ -1,5 +1,5 @@
 """Phase attribution of k_s2s_lm from the diagnostic build (make -C lego-loam-sr_amd prof): runs
-the bench's odometry batches (four frames of two sequences, replayed) with LLSR_LIB=libllsr_prof.so
+the bench's odometry batches (two continuous drives, 2 warm-up + 4 measured frames) with LLSR_LIB=libllsr_prof.so
 and reports, over the slots and the four frames, the mean per-problem
 wall time of the kNN-1 search (shells / LDS scan, with the block scans for queries the shells
 left open) for surf / corner, the Jacobian rows, B (ordered sums), C (solve) and the tripod walks
@@ -22,18 +22,19 @@ lidar = sys.argv[1] if len(sys.argv) > 1 else "vlp16"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
 cfg = default_config(lidar, 2048 if lidar == "hdl64e" else None)
 cfg.mode = _abi.LLSR_MODE_LM_APPLIED
-# the bench's odometry leg: 2 sequences x 4 frames replayed in a loop (every 4th batch jumps back)
-seqs = [[synth.make_scan(1 + 64 * q + k, lidar, motion=True) for k in range(4)] for q in range(2)]
+# the bench's odometry leg: 2 continuous drives
+NF = 6  # 2 warm-up frames, then 4 measured, one continuous drive (no jump back)
+seqs = [[synth.make_scan(1 + 64 * q + k, lidar, motion=True) for k in range(NF)] for q in range(2)]
 pipe = Pipeline(cfg, max_batch=B, max_points=cfg.num_vertical_scans * cfg.num_horizontal_scans)
 batches = []
-for k in range(4):
+for k in range(NF):
     scans = [seqs[b % 2][k] for b in range(B)]
     off = np.zeros(B + 1, np.int64)
     off[1:] = np.cumsum([len(a) for a in scans])
     batches.append((torch.from_numpy(np.concatenate(scans)).cuda(), torch.from_numpy(off).cuda()))
 rows = []
 for n in range(6):  # 2 warm-up batches, then one of each frame
-    d_pts, d_off = batches[n % 4]
+    d_pts, d_off = batches[n]
     torch.cuda.synchronize()
     pipe.odometry_batch(d_pts.data_ptr(), d_off.data_ptr(), B)
     torch.cuda.synchronize()
