@@ -956,12 +956,24 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
               const int b0 = lazy ? 0 : blk * kc, b1 = lazy ? N : min(N, b0 + kc);
               int i = b0;
               if (lazy && N > 0) { c = rf[ra] * rf[rb]; i = 1; }  // the coefficient product
-              for (; i + 8 <= b1; i += 8) {
-                float pv[8];
+              // software-pipelined: the next 8 rows' LDS loads are in flight while this batch's
+              // products are added in order (the chain of adds is the only serial part)
+              if (i + 8 <= b1) {
+                float xa[8], xb[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) pv[u] = rf[4 * (i + u) + ra] * rf[4 * (i + u) + rb];
+                for (int u = 0; u < 8; ++u) { xa[u] = rf[4 * (i + u) + ra]; xb[u] = rf[4 * (i + u) + rb]; }
+                for (; i + 16 <= b1; i += 8) {
+                  float ya[8], yb[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) c = c + pv[u];
+                  for (int u = 0; u < 8; ++u) { ya[u] = rf[4 * (i + 8 + u) + ra]; yb[u] = rf[4 * (i + 8 + u) + rb]; }
+#pragma unroll
+                  for (int u = 0; u < 8; ++u) c = c + xa[u] * xb[u];
+#pragma unroll
+                  for (int u = 0; u < 8; ++u) { xa[u] = ya[u]; xb[u] = yb[u]; }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) c = c + xa[u] * xb[u];
+                i += 8;
               }
               for (; i < b1; ++i) c = c + rf[4 * i + ra] * rf[4 * i + rb];
               if (!lazy) bpart[blk][e] = c;
