@@ -1175,7 +1175,7 @@ extern "C" int32_t llsr_scan2scan_reserve(llsr_handle* h, int32_t P, int32_t ms,
   const size_t Tc = (size_t)1 << lc, Ts = (size_t)1 << ls;
   const size_t capq = (size_t)(ms > f ? ms : f) + 1;
   const size_t bytes = sizeof(CellSlot) * P * (Tc + Ts) + (sizeof(float4) + sizeof(int2)) * P * ((size_t)nc + ns) +
-                       sizeof(int) * 2 * P + (3 * sizeof(int) + sizeof(float4) + 1) * P * capq +
+                       sizeof(int) * 2 * P + (5 * sizeof(int) + sizeof(float4) + 1) * P * capq +
                        sizeof(float4) * 2 * P * (((size_t)ns + 7) / 8 + ((size_t)ns + 63) / 64) + 64 + 15 * 256;
   if (hipMalloc(&m.pool, bytes) != hipSuccess) {
     m.pool = nullptr;
@@ -1197,7 +1197,7 @@ extern "C" int32_t llsr_scan2scan_reserve(llsr_handle* h, int32_t P, int32_t ms,
   gs.cursor = carve<int>(q, (size_t)P);
   gc.cap = nc; gs.cap = ns;
   gc.log2T = lc; gs.log2T = ls;
-  a.idx = carve<int>(q, 3 * (size_t)P * capq);
+  a.idx = carve<int>(q, 5 * (size_t)P * capq);  // kIx ints per query (llsr_fa_lm.hip)
   a.rows = carve<float4>(q, (size_t)P * capq);
   a.valid = carve<uint8_t>(q, (size_t)P * capq);
   a.error = carve<int>(q, 1);

@@ -43,6 +43,7 @@ namespace {
 constexpr int kThreads = kS2SThreads;
 constexpr int kMaxShell = 2;  // grid shells searched before the exact block-wide scan (queries in sparse regions)
 constexpr int kFbMax = 256;       // queries per kNN iteration whose shells did not settle (block scan)
+constexpr int kIx = 5;            // ints per query in S2SArgs::idx
 
 // TransformToStart (FA:1389-1412)
 __device__ __forceinline__ float4 to_start(const float* t, float4 pi) {
@@ -79,11 +80,11 @@ __device__ __forceinline__ float l2(float4 q, float4 p) {
 // lower index) over growing shells of 1 m cells. Returns true once the searched shells provably
 // contain the nearest point or nothing nearer than dist_sqr can remain outside them; false when
 // kMaxShell shells do not settle it (the caller then scans the whole cloud, nn1_block).
+// (bi, bd) may start from a known point of the cloud (the previous kNN pass's answer: a real
+// candidate, so the lexicographic minimum is unchanged) — cells farther than it are not probed.
 __device__ bool nn1_shells(const CellGrid& g, int p, float4 q, float dist_sqr, int& bi, float& bd) {
   const CellSlot* tab = g.table(p);
   const float4* pts = g.cells(p);
-  bd = INFINITY;
-  bi = INT_MAX;
   const int cx = cell_coord(q.x), cy = cell_coord(q.y), cz = cell_coord(q.z);
   // squared gap of q to the cell slab at offset dd along one axis, rounded as l2 rounds: a point
   // of that slab has |fl(q - p)| >= this gap (rounding is monotone and symmetric)
@@ -263,8 +264,12 @@ __device__ __forceinline__ float box_lb(const float4& lo, const float4& hi, floa
 // (aligned to the box array) and whole 64-point superblocks that contain no walk stop and whose
 // box cannot beat the minimum they would be tested against are skipped: the visits that remain
 // are the walk's, in its order, so the result is the serial loop's.
+// w2 / w3: skip bounds from the previous kNN pass (the next float above the distance of its
+// same-ring / other-ring choice, when the nearest neighbour and hence the walk's range and classes
+// are unchanged; INFINITY otherwise): a block whose box is farther holds only points farther than a
+// point of the same class and range, so it cannot hold the argmin.
 __device__ void surf_finish(const float4* sl, const float4* box, const float4* box2, int Ns, int fwd, float4 sel,
-                            float dist_sqr, int nn, float nd, int& i1, int& i2, int& i3) {
+                            float dist_sqr, int nn, float nd, float w2, float w3, int& i1, int& i2, int& i3) {
   i1 = -1;
   i2 = -1;
   i3 = -1;
@@ -276,8 +281,14 @@ __device__ void surf_finish(const float4* sl, const float4* box, const float4* b
   const int end = fwd < Ns ? fwd : Ns;
   // the minimum a block of rings [rlo, rhi] is tested against: the up-walk tests rings <= cs
   // against m2, the down-walk rings >= cs; the rest against m3
-  auto bound_up = [&](float rlo, float rhi) { return rhi <= (float)cs ? m2 : rlo > (float)cs ? m3 : fmaxf(m2, m3); };
-  auto bound_dn = [&](float rlo, float rhi) { return rlo >= (float)cs ? m2 : rhi < (float)cs ? m3 : fmaxf(m2, m3); };
+  auto bound_up = [&](float rlo, float rhi) {
+    const float b2 = fminf(m2, w2), b3 = fminf(m3, w3);
+    return rhi <= (float)cs ? b2 : rlo > (float)cs ? b3 : fmaxf(b2, b3);
+  };
+  auto bound_dn = [&](float rlo, float rhi) {
+    const float b2 = fminf(m2, w2), b3 = fminf(m3, w3);
+    return rlo >= (float)cs ? b2 : rhi < (float)cs ? b3 : fmaxf(b2, b3);
+  };
   // up-walk: single points up to the next block boundary, then blocks
   int j = nn + 1;
   bool stop = false;
@@ -359,7 +370,7 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
 // whose box cannot beat the minimum it would be tested against and that holds no stop changes
 // nothing), so the result is the serial loop's.
 __device__ void surf_finish_wave(const float4* sl, const float4* box2, int end, float4 sel, float dist_sqr, bool act,
-                                 int nn, float nd, int& i1, int& i2, int& i3) {
+                                 int nn, float nd, float w2l, float w3l, int& i1, int& i2, int& i3) {
   const bool walk = act && nd < dist_sqr;
   i1 = walk ? nn : -1;
   i2 = -1;
@@ -396,8 +407,15 @@ __device__ void surf_finish_wave(const float4* sl, const float4* box2, int end, 
       }
       return sm != 0;
     };
-    auto bound_up = [&](float rlo, float rhi) { return rhi <= (float)cs ? m2 : rlo > (float)cs ? m3 : fmaxf(m2, m3); };
-    auto bound_dn = [&](float rlo, float rhi) { return rlo >= (float)cs ? m2 : rhi < (float)cs ? m3 : fmaxf(m2, m3); };
+    const float w2 = readlane_f(w2l, l), w3 = readlane_f(w3l, l);  // surf_finish's skip bounds
+    auto bound_up = [&](float rlo, float rhi) {
+      const float b2 = fminf(m2, w2), b3 = fminf(m3, w3);
+      return rhi <= (float)cs ? b2 : rlo > (float)cs ? b3 : fmaxf(b2, b3);
+    };
+    auto bound_dn = [&](float rlo, float rhi) {
+      const float b2 = fminf(m2, w2), b3 = fminf(m3, w3);
+      return rlo >= (float)cs ? b2 : rhi < (float)cs ? b3 : fmaxf(b2, b3);
+    };
     // up-walk n0 + 1 .. end - 1: the head up to a superblock boundary, then superblocks
     int j = n0 + 1;
     bool stop = false;
@@ -654,6 +672,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
   const int tid = threadIdx.x;
 #ifdef LLSR_S2S_PROF
   unsigned long long tprev = wall_clock64(), tAks = 0, tAkc = 0, tA = 0, tB = 0, tC = 0, tF = 0, tW = 0;
+  int nfb_total = 0;  // queries the surf / corner shells left to the block-wide scan (report.skipped)
 #endif
   __shared__ float t[6];
   __shared__ float matP[9];
@@ -699,7 +718,9 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
     const float4* sbox = a.sbox + (size_t)p * ((gs.cap + 7) / 8) * 2;
     const float4* sbox2 = a.sbox2 + (size_t)p * ((gs.cap + 63) / 64) * 2;
     const int capq = a.cap_sharp > a.cap_flat ? a.cap_sharp : a.cap_flat;
-    int* idx = a.idx + (size_t)p * capq * 3;
+    // per query: [0..2] the correspondence (i1 = nearest, i2, i3) the rows read; [3..4] the kNN
+    // pass's (nearest, d^2) until the tripod search turns them into [0..2]
+    int* idx = a.idx + (size_t)p * capq * kIx;
     float4* grows = a.rows + (size_t)p * capq;
     uint8_t* gvalid = a.valid + (size_t)p * capq;
     // the two phases as two instantiations of one body (0: surf, FA:2508-2516; 1: corner,
@@ -732,20 +753,32 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
         // searches then run from ONE call site below (one inlined copy of the walks keeps the
         // kernel at 128 VGPRs with fewer spills than three copies)
         auto park = [&](int q, int nn, float nd) {
-          int* ix = idx + 3 * q;
-          ix[0] = nn;
-          ix[1] = __float_as_int(nd);
+          int* ix = idx + kIx * q;
+          ix[3] = nn;
+          ix[4] = __float_as_int(nd);
+        };
+        // the previous kNN pass of this phase (it >= 5): its nearest neighbour seeds the shells, and
+        // when the new nearest neighbour is the same point its tripod points bound the walks
+        const bool warm = it > 0;
+        auto walk_bounds = [&](const int* ix, float4 sel, int nn, float& w2, float& w3) {
+          w2 = w3 = INFINITY;
+          if (warm && ix[0] == nn && nn >= 0) {
+            if (ix[1] >= 0) w2 = __int_as_float(__float_as_int(sqdis(sl[ix[1]], sel)) + 1);
+            if (ix[2] >= 0) w3 = __int_as_float(__float_as_int(sqdis(sl[ix[2]], sel)) + 1);
+          }
         };
         auto finish = [&](int q, float4 sel, int nn, float nd) {
           int i1, i2, i3 = -1;
           if (surf) {
-            surf_finish(sl, sbox, sbox2, Ns, F, sel, a.dist_sqr, nn, nd, i1, i2, i3);
+            float w2, w3;
+            walk_bounds(idx + kIx * q, sel, nn, w2, w3);
+            surf_finish(sl, sbox, sbox2, Ns, F, sel, a.dist_sqr, nn, nd, w2, w3, i1, i2, i3);
           } else if (corner_lds) {  // LDS-typed accesses (a generic pointer would issue flat loads)
             corner_finish(lcl, Nc, Ms, sel, a.dist_sqr, nn, nd, i1, i2);
           } else {
             corner_finish(clg, Nc, Ms, sel, a.dist_sqr, nn, nd, i1, i2);
           }
-          int* ix = idx + 3 * q;
+          int* ix = idx + kIx * q;
           ix[0] = i1; ix[1] = i2; ix[2] = i3;
         };
         if (knn) {  // kNN-1 every 5th iteration (FA:1588 / 1724)
@@ -775,8 +808,12 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
           }
           for (int q = tid; q < Q && !(!surf && corner_lds); q += kThreads) {
             const float4 sel = to_start(tl, qry[q]);
-            int nn;
-            float nd;
+            int nn = INT_MAX;
+            float nd = INFINITY;
+            if (surf && warm) {  // seed: the previous pass's nearest neighbour
+              const int pn = idx[kIx * q];
+              if (pn >= 0) { nn = pn; nd = l2(sel, sl[pn]); }
+            }
             const bool ok = nn1_shells(surf ? gs : gc, p, sel, a.dist_sqr, nn, nd);
             if (ok) {
               park(q, nn, nd);
@@ -795,6 +832,9 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
           else LLSR_STAMP(tAkc);
           // queries the shells left open: the whole block scans the cloud, kMulti queries per pass
           const int nq = nfb < kFbMax ? nfb : kFbMax;
+#ifdef LLSR_S2S_PROF
+          if (tid == 0) nfb_total += nfb;
+#endif
           for (int k0 = 0; k0 < nq; k0 += kMulti) {
             const int m = nq - k0 < kMulti ? nq - k0 : kMulti;
             float4 qs[kMulti];
@@ -817,23 +857,24 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
             for (int q0 = 0; q0 < Q; q0 += kThreads) {
               const int q = q0 + tid;
               const bool act = q < Q;
-              int* ix = idx + 3 * (act ? q : 0);
+              int* ix = idx + kIx * (act ? q : 0);
               int nn = -1;
-              float nd = INFINITY;
+              float nd = INFINITY, w2 = INFINITY, w3 = INFINITY;
               float4 sel = make_float4(0.f, 0.f, 0.f, 0.f);
               if (act) {
-                nn = ix[0];
-                nd = __int_as_float(ix[1]);
+                nn = ix[3];
+                nd = __int_as_float(ix[4]);
                 sel = to_start(tl, qry[q]);
+                walk_bounds(ix, sel, nn, w2, w3);
               }
               int i1, i2, i3;
-              surf_finish_wave(sl, sbox2, F < Ns ? F : Ns, sel, a.dist_sqr, act, nn, nd, i1, i2, i3);
+              surf_finish_wave(sl, sbox2, F < Ns ? F : Ns, sel, a.dist_sqr, act, nn, nd, w2, w3, i1, i2, i3);
               if (act) { ix[0] = i1; ix[1] = i2; ix[2] = i3; }
             }
           } else {
             for (int q = tid; q < Q; q += kThreads) {
-              const int* ix = idx + 3 * q;
-              finish(q, to_start(tl, qry[q]), ix[0], __int_as_float(ix[1]));
+              const int* ix = idx + kIx * q;
+              finish(q, to_start(tl, qry[q]), ix[3], __int_as_float(ix[4]));
             }
           }
           __syncthreads();
@@ -844,7 +885,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
         for (int q = tid; q < Q; q += kThreads) {
           const float4 pi = qry[q];
           const float4 sel = to_start(tl, pi);
-          const int* ix = idx + 3 * q;
+          const int* ix = idx + kIx * q;
           float4 row = make_float4(0.f, 0.f, 0.f, 0.f);  // no correspondence: adds exact zeros
           bool valid = false;
           if constexpr (surf) {
@@ -1074,6 +1115,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
     r.transform_cur[0] = (float)tAks; r.transform_cur[1] = (float)tAkc; r.transform_cur[2] = (float)tA;
     r.transform_cur[3] = (float)tB; r.transform_cur[4] = (float)tC; r.transform_cur[5] = (float)tF;
     r.ms = (float)tW;
+    r.skipped = nfb_total;
 #endif
     a.degen[p] = isDeg;
   }

@@ -17,7 +17,7 @@ struct S2SArgs {
   float* tcur;                 // [P][6] transformCur in/out
   int* degen;                  // [P] isDegenerate in/out
   llsr_s2s_report* report;     // [P]
-  int* idx;                    // [P][max(cap_sharp, cap_flat)][3] correspondence indices
+  int* idx;                    // [P][max(cap_sharp, cap_flat)][5] correspondence indices + kNN pass
   float4* rows;                // [P][max(cap_sharp, cap_flat)] Jacobian row (3) + b (0 without a correspondence)
   uint8_t* valid;              // [P][max(cap_sharp, cap_flat)] 1: the row holds a correspondence
   int* error;                  // capacity violations

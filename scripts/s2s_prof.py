@@ -33,6 +33,7 @@ for k in range(NF):
     off[1:] = np.cumsum([len(a) for a in scans])
     batches.append((torch.from_numpy(np.concatenate(scans)).cuda(), torch.from_numpy(off).cuda()))
 rows = []
+per = {}  # (frame, sequence) -> rows
 for n in range(6):  # 2 warm-up batches, then one of each frame
     d_pts, d_off = batches[n]
     torch.cuda.synchronize()
@@ -40,14 +41,20 @@ for n in range(6):  # 2 warm-up batches, then one of each frame
     torch.cuda.synchronize()
     if n < 2:
         continue
-    for b in range(0, B, max(1, B // 64)):
+    for b in list(range(0, B, max(1, B // 64))) + [1, 3]:
         f = pipe.odometry_fetch(b)
         t = f["lm"]["transform_cur"] / 100.0  # 100 MHz ticks -> us
         rows.append(list(t[:6]) + [f["lm"]["ms"] / 100.0, f["lm"]["surf_iterations"], f["lm"]["corner_iterations"],
-                                   f["lm"]["n_surf_corr"], f["lm"]["n_corner_corr"]])
+                                   f["lm"]["n_surf_corr"], f["lm"]["n_corner_corr"], f["lm"]["skipped"]])
+        per.setdefault((n, b % 2), []).append(rows[-1])
 r = np.array(rows)
 print(json.dumps({"lidar": lidar, "B": B,
                   "us_per_problem": dict(zip(["knn_surf", "knn_corner", "A_rows", "B_sums", "C_solve",
                                               "walks_corner", "walks_surf"], r[:, :7].mean(0).round(1).tolist())),
                   "iterations": dict(zip(["surf", "corner"], r[:, 7:9].mean(0).round(1).tolist())),
-                  "correspondences": dict(zip(["surf", "corner"], r[:, 9:].mean(0).round(1).tolist()))}))
+                  "correspondences": dict(zip(["surf", "corner"], r[:, 9:11].mean(0).round(1).tolist())),
+                  "per_frame_sequence": {f"frame {k[0]} seq {k[1]}": {
+                      "us": dict(zip(["knn_surf", "knn_corner", "A_rows", "B_sums", "C_solve", "walks_corner", "walks_surf"],
+                                     np.array(v)[:, :7].mean(0).round(1).tolist())),
+                      "iterations": np.array(v)[:, 7:9].mean(0).round(1).tolist(),
+                      "shell_fallback_queries": float(np.array(v)[:, 11].mean())} for k, v in sorted(per.items())}}))
