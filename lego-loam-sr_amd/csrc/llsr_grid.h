@@ -99,8 +99,8 @@ inline void grid_build(const CellGrids2& g, hipStream_t s) {
   const int T = 1 << (g.g[0].log2T > g.g[1].log2T ? g.g[0].log2T : g.g[1].log2T);
   const int M = g.g[0].cap > g.g[1].cap ? g.g[0].cap : g.g[1].cap;
   k_grid_clear<<<dim3((T + 255) / 256, g.P, 2), 256, 0, s>>>(g);
-  if (M > 0) k_grid_insert<<<dim3((M + 255) / 256, g.P, 2), 256, 0, s>>>(g);
-  k_grid_alloc<<<dim3((T + 255) / 256, g.P, 2), 256, 0, s>>>(g);
+  if (M > 0) k_grid_insert<<<dim3((M + 1023) / 1024, g.P, 2), 256, 0, s>>>(g);  // kInsChunk
+  k_grid_alloc<<<dim3((T + 4095) / 4096, g.P, 2), 256, 0, s>>>(g);                // 256 * kAllocPer
   if (M > 0) k_grid_scatter<<<dim3((M + 255) / 256, g.P, 2), 256, 0, s>>>(g);
 }
 
