@@ -244,7 +244,8 @@ static void make_devcfg(const llsr_config& c, DevCfg& d) {
   d.gnd_cos[2] = llsr_libm::ground_cos_threshold(25.0f);
   d.ccl_lds = (d.H <= 16 && d.HW <= 32000) ? 1 : 0;
   // 72 KB bands: two labelling workgroups per CU (a 512-scan HDL-64E batch runs in one round)
-  d.lbl_band = std::max(1, std::min(d.H, 18432 / std::max(1, d.W)));
+  // (at most 16 rows: a band root's LDS word keeps its members' rows in 16 bits)
+  d.lbl_band = std::max(1, std::min(std::min(d.H, 16), 18432 / std::max(1, d.W)));
   d.dbg_phase = 1 << 30;
 }
 

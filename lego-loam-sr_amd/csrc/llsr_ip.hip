@@ -992,11 +992,33 @@ __global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
         }
       }
       __syncthreads();
-      for (int q = tid; q < nb; q += nt) {  // read-only walks: the band is final
+      // walks (the band is final); a member's word becomes its root (a concurrent walk reading it
+      // still sees an ancestor; roots are never written here)
+      for (int q = tid; q < nb; q += nt) {
         int x = L.ld(q);
-        if (x >= 0)
+        if (x >= 0) {
           for (int px = L.ld(x); px != x; px = L.ld(x)) x = px;
+          if (x != q) L.st(q, x);
+        }
         P.st(c0 + q, x < 0 ? -1 : c0 + x);
+      }
+      __syncthreads();
+      // Band component stats in the band root's LDS word, as in the LDS path: 0x80000000 |
+      // size << 16 | rows (bit i - r0, lbl_band <= 16) of its non-root members
+      for (int q = tid; q < nb; q += nt)
+        if (L.ld(q) == q) L.st(q, (int)(0x80000000u | (1u << 16)));
+      __syncthreads();
+      for (int q = tid; q < nb; q += nt) {
+        const int x = L.ld(q);
+        if (x < 0) continue;  // not label 0, or a root (stats word)
+        atomicAdd(&lds_parent[x], 1 << 16);
+        atomicOr(&lds_parent[x], 1 << ((c0 + q) / W - r0));
+      }
+      __syncthreads();
+      // lab: -1 (not label 0), the band root's cell (member) or the band stats (band root)
+      for (int q = tid; q < nb; q += nt) {
+        const int x = L.ld(q);
+        lab[c0 + q] = x >= 0 ? c0 + x : x;
       }
       __syncthreads();
     }
@@ -1063,52 +1085,32 @@ __global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
     }
     return;
   }
-  // flatten: root per cell -> lab (temporarily), -1 for non-label-0 cells
+  // Global mode: component stats from the band components. A band root whose global root is
+  // itself is a component seed: it takes its band's stats with plain stores (lab = 0x80000000 |
+  // size, rows in ccl_b); the other band roots (components crossing a band boundary) then add
+  // theirs, their own row included, with atomics.
+  const int R = c.lbl_band;
+  unsigned long long* rowA = d.ccl_b + base;
   for (int cell = tid; cell < HW; cell += nt) {
-    const int p = P.ld(cell);
-    lab[cell] = p < 0 ? -1 : uf_find(P, cell);
+    const int v = lab[cell];
+    if (v >= -1 || uf_find(P, cell) != cell) continue;  // -1, a member, or a joined band root
+    rowA[cell] = (unsigned long long)(v & 0xffff) << ((cell / W) / R * R);
+    lab[cell] = (int)(0x80000000u | (((unsigned)v >> 16) & 0x7fffu));
   }
   __syncthreads();
-  // component stats. LDS mode packs (size << 16) | rowmask16 into one word per root;
-  // global mode keeps size in ccl_a and the 64-bit row mask in ccl_b.
-  int* stat = kLds ? lds_parent : d.ccl_a + base;
-  unsigned long long* rowm = d.ccl_b + base;
   for (int cell = tid; cell < HW; cell += nt) {
-    stat[cell] = 0;
-    if (!kLds) rowm[cell] = 0ull;
-  }
-  __syncthreads();
-  for (int cell = tid; cell < HW; cell += nt) {
-    const int root = lab[cell];
+    const int v = lab[cell];
+    if (v >= -1 || P.ld(cell) == cell) continue;  // only band roots joined to another seed
+    const int gr = uf_find(P, cell);
     const int row = cell / W;
-    if (kLds) {
-      if (root < 0) continue;
-      atomicAdd(&stat[root], 1 << 16);
-      if (cell != root) atomicOr(&stat[root], 1 << row);
-    } else {
-      // a wave holds 64 consecutive cells, mostly of one or two segments: one size atomic per
-      // distinct root of the wave (same-address global atomics serialise at L2), one row-mask
-      // atomic per (root, row) of its non-seed members
-      const int l = lane_id();
-      unsigned long long pend = __ballot(root >= 0);
-      while (pend) {
-        const int leader = __ffsll((long long)pend) - 1;
-        const int lr = __builtin_amdgcn_readlane(root, leader);  // leader is uniform
-        const int lrow = __builtin_amdgcn_readlane(row, leader);
-        const unsigned long long grp = __ballot(root == lr) & pend;
-        const unsigned long long same = __ballot(root == lr && cell != lr && row == lrow) & pend;
-        if (l == leader) {
-          atomicAdd(&stat[lr], (int)__popcll(grp));
-          if (same) atomicOr(&rowm[lr], 1ull << lrow);
-        }
-        if (((grp >> l) & 1ull) && cell != lr && row != lrow) atomicOr(&rowm[lr], 1ull << row);
-        pend &= ~grp;
-      }
-    }
+    __hip_atomic_fetch_add(&lab[gr], (int)(((unsigned)v >> 16) & 0x7fffu), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_or(&rowA[gr], ((unsigned long long)(v & 0xffff) << (row / R * R)) | (1ull << row),
+                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   __syncthreads();
   // feasibility and rank of feasible seeds in row-major order: tiles of 4 consecutive cells per
-  // lane, one block scan of the lane counts per tile
+  // lane, one block scan of the lane counts per tile; a seed's lab becomes 0x80000000 | label
   constexpr int kC = 4;
   int rank = 0;
   for (int t0 = 0; t0 < HW; t0 += kC * nt) {
@@ -1118,12 +1120,10 @@ __global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
 #pragma unroll
     for (int u = 0; u < kC; ++u) {
       const int cell = c0 + u;
-      root[u] = cell < HW && lab[cell] == cell;
+      root[u] = cell < HW && P.ld(cell) == cell;
       feas[u] = false;
       if (root[u]) {
-        int size, lines;
-        if (kLds) { size = (unsigned)stat[cell] >> 16; lines = __popc(stat[cell] & 0xffff); }
-        else { size = stat[cell]; lines = __popcll(rowm[cell]); }
+        const int size = lab[cell] & 0x7fffffff, lines = __popcll(rowA[cell]);
         feas[u] = size >= 30 || (size >= c.pointNum && lines >= c.lineNum);
       }
       nf += feas[u];
@@ -1132,13 +1132,17 @@ __global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
     int ex = rank + block_excl_scan(nf, tmp, &tot);  // barriers: all stat reads done
 #pragma unroll
     for (int u = 0; u < kC; ++u)
-      if (root[u]) stat[c0 + u] = feas[u] ? ++ex : 999999;
+      if (root[u]) lab[c0 + u] = (int)(0x80000000u | (unsigned)(feas[u] ? ++ex : 999999));
     rank += tot;
   }
   __syncthreads();
+  // every label-0 cell takes its seed's label (a seed's own word may already hold the final value:
+  // both forms read the same through the mask)
   for (int cell = tid; cell < HW; cell += nt) {
-    const int root = lab[cell];
-    if (root >= 0) lab[cell] = stat[root];
+    const int v = lab[cell];
+    if (v == -1) continue;
+    const int gr = uf_find(P, v >= 0 ? v : cell);
+    lab[cell] = __hip_atomic_load(&lab[gr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & 0x7fffffff;
   }
 }
 
