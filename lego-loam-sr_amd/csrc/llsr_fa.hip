@@ -947,18 +947,29 @@ __global__ __launch_bounds__(256) void k_dbscan_adj(DevCfg c, DevBufs d) {
     const float k2 = pj.w * pj.w, z2 = kz * kz;
     const bool fast = c.DBFr > 0.0f && k2 > 1e-30f && k2 < 1e30f && z2 > 1e-30f && z2 < 1e30f;
     const float rk = __builtin_amdgcn_rcpf(k2), rz = __builtin_amdgcn_rcpf(z2);
-    const int i1 = i0 + kAdjRows < M ? i0 + kAdjRows : M;
-    for (int i = i0; i < i1; ++i) {
-      const float4 pi = pts[i];  // wave-uniform
+    // the task's row points: one load by lanes 0 .. kAdjRows-1, broadcast per row by readlane;
+    // the rows' ballots gather in lanes 2r (low word) / 2r+1 (high word) and leave in ONE store
+    // (vector-memory instructions, not arithmetic, set this kernel's pace)
+    const float4 prow = l < kAdjRows && i0 + l < M ? pts[i0 + l] : make_float4(0.f, 0.f, 0.f, 0.f);
+    uint32_t out = 0u;
+#pragma unroll
+    for (int r = 0; r < kAdjRows; ++r) {
+      if (i0 + r >= M) break;
+      float4 pi;
+      pi.x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(prow.x), r));
+      pi.y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(prow.y), r));
+      pi.z = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(prow.z), r));
+      pi.w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(prow.w), r));
       const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
       const float s = (dx * dx + dy * dy) * rk + dz * dz * rz;
       bool nb = fast && s < lo;
       if (inj && !(fast && (s < lo || s > hi))) nb = db_near(c, pi, pj, kz);
       nb = nb && inj;
       const unsigned long long m = __ballot(nb);
-      if (l == 0) adj[(size_t)i * kAdjWords + 2 * ch] = (uint32_t)m;
-      if (l == 1 && 2 * ch + 1 < kAdjWords) adj[(size_t)i * kAdjWords + 2 * ch + 1] = (uint32_t)(m >> 32);
+      out = l == 2 * r ? (uint32_t)m : l == 2 * r + 1 ? (uint32_t)(m >> 32) : out;
     }
+    const int w = 2 * ch + (l & 1);
+    if (l < 2 * kAdjRows && i0 + (l >> 1) < M && w < kAdjWords) adj[(size_t)(i0 + (l >> 1)) * kAdjWords + w] = out;
   }
 }
 
