@@ -952,7 +952,6 @@ __global__ __launch_bounds__(256) void k_dbscan_adj(DevCfg c, DevBufs d) {
     // (vector-memory instructions, not arithmetic, set this kernel's pace)
     const float4 prow = l < kAdjRows && i0 + l < M ? pts[i0 + l] : make_float4(0.f, 0.f, 0.f, 0.f);
     uint32_t out = 0u;
-#pragma unroll
     for (int r = 0; r < kAdjRows; ++r) {
       if (i0 + r >= M) break;
       float4 pi;
