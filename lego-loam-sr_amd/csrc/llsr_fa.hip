@@ -89,58 +89,66 @@ __global__ __launch_bounds__(512) void k_fa_points(DevCfg c, DevBufs d) {
   uint8_t* picked = d.picked + base;
   int8_t* clabel = d.clabel + base;
   float* curv = d.curv + base;
+  // per tile ONE round of loads: the tile's points with their +-5 halo (kP5 per lane) and the
+  // occlusion inputs (range, column of i; the neighbours' from the adjacent lanes, the wave's edge
+  // lanes loading their one outside value), all in flight together
+  constexpr int kP5 = (kTile + 10 + 511) / 512;
+  constexpr int kQ = (kTile + 12 + 511) / 512;
+  const int ln = lane_id();
   for (int t0 = 0; t0 < S; t0 += kTile) {
-    for (int q0 = tid; q0 < kTile + 10; q0 += kP * nt) {
-      float4 pp[kP];
+    float4 pp[kP5];
+    float r1[kQ], rx[kQ];
+    uint32_t c1[kQ], cx[kQ];
 #pragma unroll
-      for (int u = 0; u < kP; ++u) {
-        const int k = t0 - 5 + q0 + u * nt;
-        pp[u] = (q0 + u * nt < kTile + 10 && k >= 0 && k < S) ? seg[k] : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+    for (int u = 0; u < kP5; ++u) {
+      const int q = tid + u * nt, k = t0 - 5 + q;
+      pp[u] = (q < kTile + 10 && k >= 0 && k < S) ? seg[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 #pragma unroll
-      for (int u = 0; u < kP; ++u) {
-        const int q = q0 + u * nt, k = t0 - 5 + q;
-        if (q >= kTile + 10) continue;
-        if (k >= 0 && k < S) {
-          const float4 lp = loam_point(c, pp[u], k, first, start, endo, diff);
-          tp[q] = lp;
-          if (q >= 5 && q < kTile + 5) loam[k] = lp;
-        } else {
-          tp[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+    for (int u = 0; u < kQ; ++u) {
+      const int q = tid + u * nt, i = t0 - 6 + q;
+      const bool in = q <= kTile + 12 && i >= 0 && i < S;  // (q = kTile + 12: the last flag's i + 1)
+      r1[u] = in ? rng[i] : 0.0f;
+      c1[u] = in ? col[i] : 0u;
+      const int ie = ln == 0 ? i - 1 : i + 1;  // lane 0: i - 1; lane 63: i + 1 (the others unused)
+      const bool ine = (ln == 0 || ln == 63) && q < kTile + 12 && ie >= 0 && ie < S;
+      rx[u] = ine ? rng[ie] : 0.0f;
+      cx[u] = ine ? col[ie] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kP5; ++u) {
+      const int q = tid + u * nt, k = t0 - 5 + q;
+      if (q >= kTile + 10) continue;
+      if (k >= 0 && k < S) {
+        const float4 lp = loam_point(c, pp[u], k, first, start, endo, diff);
+        tp[q] = lp;
+        if (q >= 5 && q < kTile + 5) loam[k] = lp;
+      } else {
+        tp[q] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
-    // occlusion flags of the tile (+ halo): every lane's ranges / columns are loaded in one batch
-    constexpr int kQ = (kTile + 12 + 511) / 512;
-    {
-      float r0[kQ], r1[kQ], r2[kQ];
-      uint32_t c1[kQ], c2[kQ];
+    // occlusion flags of the tile (+ halo)
 #pragma unroll
-      for (int u = 0; u < kQ; ++u) {
-        const int q = tid + u * nt, i = t0 - 6 + q;
-        if (q < kTile + 12 && i >= 5 && i < S - 6) {
-          r0[u] = rng[i - 1]; r1[u] = rng[i]; r2[u] = rng[i + 1];
-          c1[u] = col[i]; c2[u] = col[i + 1];
+    for (int u = 0; u < kQ; ++u) {
+      const int q = tid + u * nt, i = t0 - 6 + q;
+      const float up = __shfl_up(r1[u], 1, 64), dn = __shfl_down(r1[u], 1, 64);
+      const uint32_t cdn = (uint32_t)__shfl_down((int)c1[u], 1, 64);
+      if (q >= kTile + 12) continue;
+      uint8_t f = 0;
+      if (i >= 5 && i < S - 6) {
+        const float r0 = ln == 0 ? rx[u] : up, r2 = ln == 63 ? rx[u] : dn;
+        const uint32_t c2 = ln == 63 ? cx[u] : cdn;
+        const float d1 = r1[u], d2 = r2;
+        const int colDiff = abs((int)(c2 - c1[u]));
+        if (colDiff < 10) {
+          if ((double)(d1 - d2) > 0.3) f |= 1;
+          else if ((double)(d2 - d1) > 0.3) f |= 2;
         }
+        const float diff1 = fabs_((float)(r0 - r1[u]));
+        const float diff2 = fabs_((float)(r2 - r1[u]));
+        if ((double)diff1 > 0.02 * (double)r1[u] && (double)diff2 > 0.02 * (double)r1[u]) f |= 4;
       }
-#pragma unroll
-      for (int u = 0; u < kQ; ++u) {
-        const int q = tid + u * nt, i = t0 - 6 + q;
-        if (q >= kTile + 12) continue;
-        uint8_t f = 0;
-        if (i >= 5 && i < S - 6) {
-          const float d1 = r1[u], d2 = r2[u];
-          const int colDiff = abs((int)(c2[u] - c1[u]));
-          if (colDiff < 10) {
-            if ((double)(d1 - d2) > 0.3) f |= 1;
-            else if ((double)(d2 - d1) > 0.3) f |= 2;
-          }
-          const float diff1 = fabs_((float)(r0[u] - r1[u]));
-          const float diff2 = fabs_((float)(r2[u] - r1[u]));
-          if ((double)diff1 > 0.02 * (double)r1[u] && (double)diff2 > 0.02 * (double)r1[u]) f |= 4;
-        }
-        fl[q] = f;
-      }
+      fl[q] = f;
     }
     __syncthreads();
     for (int q0 = tid; q0 < kTile; q0 += nt) {
