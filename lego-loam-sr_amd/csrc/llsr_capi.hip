@@ -1837,6 +1837,17 @@ static int32_t mapping_mo(llsr_handle* h, int32_t B, hipStream_t s, const std::v
     sl.keyposes.insert(sl.keyposes.end(), kp, kp + 6);
     sl.mo_frames += 1;
   }
+#ifdef LLSR_S2S_PROF
+  {  // diagnostics build only: fail this call's MapOptimization part once, after its keyframes were
+     // added, when slot 0 reaches MapOptimization frame LLSR_MO_FAIL_AT (tests/test_gpu_mapping_rollback.py)
+    static bool fired = false;
+    const char* at = std::getenv("LLSR_MO_FAIL_AT");
+    if (at && !fired && step[0] && mp.slot[0].mo_frames == std::atoi(at)) {
+      fired = true;
+      return fail(h, LLSR_EIO, "injected MapOptimization failure (LLSR_MO_FAIL_AT)");
+    }
+  }
+#endif
   return LLSR_OK;
 }
 
