@@ -824,10 +824,18 @@ __global__ __launch_bounds__(256, 5) void k_select_ring(DevCfg c, DevBufs d) {
       int cntp = 0;
       for (int e = t; e < R && (uint32_t)(key[e] >> 32) == vid; ++e) {
         const int run = (int)(uint32_t)key[e];
-        for (int q = rstart[run]; q < rstart[run + 1]; ++q) {
-          const float4 p = lp[cpos[q]];
-          sx += p.x; sy += p.y; sz += p.z; si += p.w;
+        // two of the run's points in flight per step, summed in order
+        const int qe = rstart[run + 1];
+        for (int q = rstart[run]; q < qe; q += 2) {
+          const bool two = q + 1 < qe;
+          const float4 p0 = lp[cpos[q]];
+          const float4 p1 = two ? lp[cpos[q + 1]] : make_float4(0.f, 0.f, 0.f, 0.f);
+          sx += p0.x; sy += p0.y; sz += p0.z; si += p0.w;
           ++cntp;
+          if (two) {
+            sx += p1.x; sy += p1.y; sz += p1.z; si += p1.w;
+            ++cntp;
+          }
         }
       }
       const float nn = (float)cntp;
