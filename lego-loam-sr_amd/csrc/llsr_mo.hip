@@ -100,8 +100,10 @@ __device__ bool knn5(const CellSlot* __restrict__ tab, int log2T, const float4* 
     const int s = grid_find(tab, log2T, cell_key(cx + ox, cy + oy, cz + oz));
     if (s < 0) continue;
     const int st = tab[s].start, n = tab[s].count;
+    float4 pn = n > 0 ? pts[st] : make_float4(0.f, 0.f, 0.f, 0.f);
     for (int j = st; j < st + n; ++j) {
-      const float4 p = pts[j];
+      const float4 p = pn;  // the next point's load is in flight while this one is tested
+      if (j + 1 < st + n) pn = pts[j + 1];
       float d = 0.0f;
       float t = qx - p.x; d += t * t;  // nanoflann L2 accumulation order
       t = qy - p.y; d += t * t;
