@@ -31,6 +31,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "lego-loam-sr_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+VOXEL_ORDERS = {"input": 0, "pcl": 1}  # llsr.h LLSR_VOXEL_ORDER_INPUT / LLSR_VOXEL_ORDER_PCL
 
 
 def kernel_bytes(name: str, c: dict, HW: int) -> float:
@@ -101,11 +102,9 @@ def _ipfa_cpu_worker(args):
 def cpu_baseline_all_cores(scans: list[np.ndarray], budget_s: float) -> dict:
     """all-core throughput of the headline path = independent single-threaded
     pipelines, one per host core the job is granted (16 on the GPU pool), each cycling the scans."""
-    import multiprocessing as mp
     nproc = min(16, os.cpu_count() or 1)
     t1 = time.perf_counter()
-    with mp.get_context("spawn").Pool(nproc) as pool:
-        res = pool.map(_ipfa_cpu_worker, [(scans, budget_s)] * nproc)
+    res = pool_map(_ipfa_cpu_worker, [(scans, budget_s)] * nproc, nproc)
     wall = time.perf_counter() - t1
     n = sum(r[0] for r in res)
     busy = max(r[1] for r in res)
@@ -114,6 +113,19 @@ def cpu_baseline_all_cores(scans: list[np.ndarray], budget_s: float) -> dict:
             "sample": f"{nproc} processes x the oracle IP+FA-feature path, {n} scans in all, slowest process "
                       f"{busy:.1f} s busy ({wall:.1f} s wall incl. start-up)",
             **host_share(v, nproc)}
+
+
+def pool_map(fn, jobs: list, nproc: int) -> list:
+    """multiprocessing map over `nproc` spawned CPU workers, closed and joined (a `with Pool` exit
+    terminates its workers with SIGTERM, which a profiler's signal handler logs as an abort)."""
+    import multiprocessing as mp
+    pool = mp.get_context("spawn").Pool(nproc)
+    try:
+        res = pool.map(fn, jobs)
+    finally:
+        pool.close()
+        pool.join()
+    return res
 
 
 def host_share(value: float, nproc: int) -> dict:
@@ -207,6 +219,21 @@ def s2m_bytes_per_iteration(Qc: int, Qs: int, blocks: int) -> float:
     return 96.0 * (Qc + Qs) + 116.0 * blocks
 
 
+def _s2m_check_worker(args):
+    """Oracle poses of a chunk of scan-to-map problems (the parity check of every problem of a
+    step, spread over the host cores): [(problem, pose)]."""
+    fixture, mode_name, items = args
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle_py
+    from llsr import _abi, default_config
+    cfg = default_config("vlp16")
+    cfg.mode = {"lm_applied": _abi.LLSR_MODE_LM_APPLIED, "faithful": _abi.LLSR_MODE_FAITHFUL}[mode_name]
+    z = np.load(os.path.join(REPO, "tests", "golden", fixture))
+    knn = "kdtree" if oracle_py.ref_lib() is not None else "grid"
+    return [(p, oracle_py.scan2map(cfg, z[f"q{q}_corner"], z[f"q{q}_surf"], z["corner_map"], z["surf_map"], pose,
+                                   knn=knn)["pose"]) for p, q, pose in items]
+
+
 def scan2map_leg(dev, mode_name: str, P: int, steps: int, warmup: int, dist, run_cpu: bool,
                  cpu_seconds: float, fixture: str = "mo_map_vlp16.npz") -> dict:
     """Config 3: P independent scan-to-map problems per step; each problem carries its own copy of
@@ -225,7 +252,7 @@ def scan2map_leg(dev, mode_name: str, P: int, steps: int, warmup: int, dist, run
     for p in range(P):
         q = p % nq
         pose = z[f"q{q}_true"] + np.concatenate([rng.uniform(-0.05, 0.05, 3), rng.uniform(-0.2, 0.2, 3)])
-        probs.append((z[f"q{q}_corner"], z[f"q{q}_surf"], cm, sm, pose.astype(np.float32)))
+        probs.append((z[f"q{q}_corner"], z[f"q{q}_surf"], cm, sm, pose.astype(np.float32), q))
 
     def pack(k):
         arrs = [pr[k] for pr in probs]
@@ -285,6 +312,7 @@ def scan2map_leg(dev, mode_name: str, P: int, steps: int, warmup: int, dist, run
     per_launch_ms = st["iterate_ms"] / max(1, st["iteration_launches"])
     launches_per_batch = st["iteration_launches"] / max(1, st["batches"])
     achieved = lm_bytes / (st["iterate_ms"] / max(1, st["batches"]) * 1e-3) / 1e9
+    tr = lm_traffic("k_s2m_iter", P)
     out = {
         "workload": "configs[2]: scan-to-map LM (corner/surf kNN-5 correspondences + 6x6 normal "
                     f"equations + solve) against a {len(cm) + len(sm)}-point local map, mode {mode_name}",
@@ -300,7 +328,9 @@ def scan2map_leg(dev, mode_name: str, P: int, steps: int, warmup: int, dist, run
         "k_s2m_iter_launches_per_step": launches_per_batch,
         "roofline": {"bound": "hbm", "kernel": "k_s2m_iter", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": lm_traffic("k_s2m_iter", P), "algorithmic_bytes_per_step": lm_bytes,
+                     "traffic": tr, "algorithmic_bytes_per_step": lm_bytes,
+                     "traffic_per_step": tr * launches_per_batch if tr is not None else None,
+                     "traffic_over_algorithmic": round(tr * launches_per_batch / lm_bytes, 2) if tr is not None else None,
                      "algorithmic_bytes_per_launch": lm_bytes / max(1, launches_per_batch),
                      "avg_launch_ms": round(per_launch_ms, 4),
                      "note": "bytes = SURVEY 8(d) B_lm per iteration; iterate window includes the host's "
@@ -311,22 +341,20 @@ def scan2map_leg(dev, mode_name: str, P: int, steps: int, warmup: int, dist, run
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle_py
         knn = "kdtree" if oracle_py.ref_lib() is not None else "grid"
-        ncheck = min(P, nq if mode_name == "lm_applied" else 2)
-        deltas = []
+        # CPU baseline: the restatement on one core, problem after problem, for ~cpu_seconds
         t_cpu, n_cpu = 0.0, 0
-        for p in range(ncheck):
-            o = oracle_py.scan2map(cfg, *probs[p], knn=knn)
-            deltas.append(float(np.abs(poses[p] - o["pose"]).max()))
-            t_cpu += o["ms"] * 1e-3
-            n_cpu += 1
-        p = ncheck
         while t_cpu < cpu_seconds and n_cpu < 10000:
-            o = oracle_py.scan2map(cfg, *probs[p % P], knn=knn)
+            o = oracle_py.scan2map(cfg, *probs[n_cpu % P][:5], knn=knn)
             t_cpu += o["ms"] * 1e-3
             n_cpu += 1
-            p += 1
+        # parity: every problem of the step against the oracle, spread over the host cores
+        nproc = min(16, os.cpu_count() or 1, P)
+        items = [(p, probs[p][5], probs[p][4]) for p in range(P)]
+        res = pool_map(_s2m_check_worker, [(fixture, mode_name, items[k::nproc]) for k in range(nproc)], nproc)
+        deltas = [float(np.abs(poses[p] - po).max()) for chunk in res for p, po in chunk]
         out["pose_delta_max"] = max(deltas)
-        out["pose_delta_problems"] = ncheck
+        out["pose_delta_problems"] = len(deltas)
+        out["bit_exact_problems"] = int(sum(d == 0.0 for d in deltas))
         out["cpu_baseline"] = {
             "value": round(n_cpu / t_cpu, 2), "unit": "scan-to-map problems/s", "cores": 1, "kind": "port",
             "sample": f"{n_cpu} problems of this batch through the C++ MO restatement ({mode_name}, kNN = "
@@ -424,8 +452,10 @@ def odometry_leg(dev, lidar: str, B: int, seqs: int, frames: int, steps: int, wa
     sequence per step: IP + feature stage + scan-to-scan LM + integrateTransformation + the next
     last clouds, all on the device (llsr_odometry_batch). `seqs` distinct synthetic drives of
     `frames` consecutive scans (0.5 m apart, the sensor moving in 6 DoF: synth.sensor_attitude) are
-    tiled over the slots; `frames` covers the warm-up, timed and profiled steps, so every measured
-    step is a real frame-to-frame transition."""
+    tiled over the slots; `frames` covers the warm-up and timed steps, so every measured step is a
+    real frame-to-frame transition. The per-kernel times come from a replay of the SAME frames:
+    after the timed region every slot is reset and the drive runs again from frame 0, its timed
+    frames with HIP events between the kernels, so the roofline describes the timed work."""
     import torch
     from llsr import Pipeline, _abi, default_config, synth
     from llsr.dist import max_over_ranks
@@ -466,11 +496,16 @@ def odometry_leg(dev, lidar: str, B: int, seqs: int, frames: int, steps: int, wa
         dist.barrier()
     el = max_over_ranks(time.perf_counter() - t0, dev)
     world = dist.get_world_size() if dist else 1
-    # per-kernel device times (HIP events on the launch stream), after the timed region: the IP +
-    # feature kernels of llsr_process_batch and the scan-to-scan grid build + LM of the same step
+    # per-kernel device times (HIP events on the launch stream) of the timed frames: reset, replay
+    # the warm-up frames, then the timed frames again with profiling on (the same state, the same
+    # work): the IP + feature kernels of llsr_process_batch and the scan-to-scan grid build + LM
+    pipe.odometry_reset()
+    n = 0
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
     pipe.set_profiling(True)
-    nprof = 2
-    for _ in range(nprof):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize(dev)
     kt = pipe.kernel_times()
@@ -521,15 +556,23 @@ def odometry_leg(dev, lidar: str, B: int, seqs: int, frames: int, steps: int, wa
     if check:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle_py
-        # slot 0 replays sequence 0 frame (i % frames) for i = 0 .. n-1: the oracle does the same
+        # slot 0 replays sequence 0 frame (i % frames) for i = 0 .. n-1: the oracle does the same,
+        # in the reference's (PCL) VoxelGrid order like the device, and once more in ring order to
+        # show what the summation order alone moves (the less-flat cloud becomes the next scan's
+        # laserCloudSurfLast, FA:2660-2712)
         od = oracle_py.OracleOdometry(cfg)
-        t_cpu = 0.0
+        odi = oracle_py.OracleOdometry(cfg, pcl_voxel_order=False)
+        t_cpu, dord = 0.0, 0.0
         for i in range(n):
             t1 = time.perf_counter()
             o = od.process(seq_scans[0][i % frames])
             t_cpu += time.perf_counter() - t1
+            oi = odi.process(seq_scans[0][i % frames])
+            dord = max(dord, float(np.abs(o["transform_sum"] - oi["transform_sum"]).max()))
         out["pose_delta_max"] = float(max(np.abs(s0["transform_cur"] - o["transform_cur"]).max(),
                                           np.abs(s0["transform_sum"] - o["transform_sum"]).max()))
+        out["voxel_order"] = "pcl (std::sort, as the reference)"
+        out["input_order_transform_sum_delta_max"] = dord
         # CPU baseline: the same restatement, one core, continuing the sequence for ~cpu_seconds
         k = n
         while t_cpu < cpu_seconds and k < n + 1000:
@@ -646,13 +689,11 @@ def mapping_leg(dev, B: int, seqs: int, warmup: int, steps: int, dist, check: bo
                                "sample": f"frames {warmup}..{frames - 1} of drive 0 through the oracle chain "
                                          f"(oracle_py.OracleMapping), 1 thread, {t_cpu:.1f} s"}
         # every host core the box grants this job (16 on the GPU pool): one drive per process
-        import multiprocessing as mp
         nproc = min(16, os.cpu_count() or 1)
         jobs = [(1 + 64 * (q + 4 * rank) + 256 * (q // seqs), frames, warmup, mo_mode, cpu_seconds)
                 for q in range(nproc)]
         t1 = time.perf_counter()
-        with mp.get_context("spawn").Pool(nproc) as pool:
-            res = pool.map(_mapping_cpu_worker, jobs)
+        res = pool_map(_mapping_cpu_worker, jobs, nproc)
         wall = time.perf_counter() - t1
         nf = sum(r[0] for r in res)
         busy = max(r[1] for r in res)
@@ -829,6 +870,8 @@ def main():
     ap.add_argument("--pc2", type=int, default=1, help="PointCloud2 decode leg (0 = skip)")
     ap.add_argument("--mapping", default="256:8:8",
                     help="mapping-chain leg drives_per_gpu:warmup_frames:timed_frames (empty = skip)")
+    ap.add_argument("--voxel-order", choices=("pcl", "input"), default="pcl",
+                    help="less-flat VoxelGrid summation order: pcl = std::sort's (the reference), input = ring order")
     ap.add_argument("--allreduce-scans", type=int, default=8,
                     help="configs[4] leg: scans per step split over all ranks (0 = skip)")
     args = ap.parse_args()
@@ -868,6 +911,8 @@ def main():
     d_off = torch.from_numpy(off).to(dev)
     nS = max(1, args.streams)
     pipes = [Pipeline(cfg, device=dev, max_batch=B, max_points=int(np.diff(off).max())) for _ in range(nS)]
+    for p_ in pipes:
+        p_.set_voxel_order(VOXEL_ORDERS[args.voxel_order])
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nS - 1)]
     pipe = pipes[0]
     torch.cuda.synchronize(dev)
@@ -934,7 +979,7 @@ def main():
         import oracle_py
         from _compare import compare
         # slot 0 of handle 0 has seen every nS-th batch of the same cloud: replay that history
-        ora = oracle_py.Oracle(cfg)
+        ora = oracle_py.Oracle(cfg, pcl_voxel_order=args.voxel_order == "pcl")
         n0 = len(range(0, args.warmup, nS)) + len(range(0, args.steps, nS)) + args.prof_batches
         for _ in range(n0):
             o = ora.process(pts[off[0]:off[1]])
@@ -994,7 +1039,7 @@ def main():
         lid, nb = spec.split(":")
         # frames: one continuous drive through warm-up, timed and profiled steps (no replay jump
         # from the last frame back to the first inside the measured region)
-        odo[lid] = odometry_leg(dev, lid, int(nb), 2, 2 + args.s2m_steps + 2 + 1, args.s2m_steps, 2, dist,
+        odo[lid] = odometry_leg(dev, lid, int(nb), 2, 2 + args.s2m_steps, args.s2m_steps, 2, dist,
                                 rank == 0 and not args.no_cpu and world == 1, min(args.cpu_seconds, 10.0))
 
     pc2 = pc2_decode_leg(dev, pts, off, args.s2m_steps * 4, dist) if args.pc2 else None

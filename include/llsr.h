@@ -78,10 +78,11 @@ int32_t llsr_config_default(llsr_config* cfg, int32_t lidar);
 
 /* The less-flat VoxelGrid of the feature stage (surfPointsLessFlatScan, FA:1268-1270) averages
  * each 0.2 m voxel's points. PCL sums them in the order std::sort leaves its index_vector (equal
- * voxel ids in libstdc++ introsort's order); LLSR_VOXEL_ORDER_PCL reproduces that exactly (one
- * wave per ring emulates the introsort: costs ~6 ms per 1024 VLP-16 scans), the default
- * LLSR_VOXEL_ORDER_INPUT sums each voxel in ring order (a centroid may differ from PCL's in the
- * last bits when its voxel holds three or more points; voxel set, count and order are the same).
+ * voxel ids in libstdc++ introsort's order); the default, LLSR_VOXEL_ORDER_PCL, reproduces that
+ * exactly (each ring's workgroup runs the introsort, partitions level by level). The opt-in
+ * LLSR_VOXEL_ORDER_INPUT sums each voxel in ring order instead (a centroid may differ from PCL's in
+ * the last bits when its voxel holds three or more points; voxel set, count and order are the
+ * same), and the difference reaches the next scan's laserCloudSurfLast and so every later pose.
  * MapOptimization's VoxelGrids (llsr_map_*, llsr_mapping_*) always follow PCL's order. */
 #define LLSR_VOXEL_ORDER_INPUT 0
 #define LLSR_VOXEL_ORDER_PCL 1
@@ -164,7 +165,7 @@ int32_t llsr_query_sizes(const llsr_handle* h, llsr_sizes* out);
 /* Reset the per-slot FeatureAssociation carry-over state (FA:167-198: the H*W arrays that the
  * reference sizes once and never clears). */
 int32_t llsr_reset_state(llsr_handle* h);
-/* LLSR_VOXEL_ORDER_INPUT (default) or LLSR_VOXEL_ORDER_PCL for the less-flat VoxelGrid; takes
+/* LLSR_VOXEL_ORDER_PCL (default) or LLSR_VOXEL_ORDER_INPUT for the less-flat VoxelGrid; takes
  * effect from the next batch. */
 int32_t llsr_set_voxel_order(llsr_handle* h, int32_t order);
 

@@ -102,7 +102,6 @@ struct llsr_handle {
   // scan-to-scan (llsr_scan2scan_*)
   struct {
     int P = 0, ms = 0, f = 0, nc = 0, ns = 0;
-    int launch_ms = 0, launch_f = 0, launch_nc = 0;  // the next launch's largest clouds (0: unknown)
     void* pool = nullptr;
     S2SArgs a{};
     int* host_flag = nullptr;
@@ -111,6 +110,7 @@ struct llsr_handle {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     hipEvent_t p0 = nullptr, p1 = nullptr, p2 = nullptr;  // profiling: start, grids built, LM done
     llsr_s2s_stats stats{};
+    int last_variant = 0;  // kLdsRows of the last k_s2s_lm instantiation launched (diagnostics)
   } s2s;
   // end-to-end odometry (llsr_odometry_*): per-slot FA state + packed clouds, allocated lazily
   struct {
@@ -246,6 +246,7 @@ static void make_devcfg(const llsr_config& c, DevCfg& d) {
   // 72 KB bands: two labelling workgroups per CU (a 512-scan HDL-64E batch runs in one round)
   // (at most 16 rows: a band root's LDS word keeps its members' rows in 16 bits)
   d.lbl_band = std::max(1, std::min(std::min(d.H, 16), 18432 / std::max(1, d.W)));
+  d.exact_vg = 1;  // LLSR_VOXEL_ORDER_PCL: the reference's summation order
   d.dbg_phase = 1 << 30;
 }
 
@@ -584,7 +585,7 @@ extern "C" int32_t llsr_kernel_times_ms(llsr_handle* h, float* out, int32_t cap)
 }
 
 // Diagnostics (not part of the ABI header): the device's exact libstdc++ std::sort (the per-ring
-// curvature sort's tie path, llsr_fa.hip exact_introsort) on n <= 2048 host values; out[k] = the
+// curvature sort's tie path and the PCL-order VoxelGrid, llsr_isort.h block_introsort) on n <= 2048 host values; out[k] = the
 // input position at sorted position k. For tests/test_gpu_features_ties.py.
 extern "C" int32_t llsr_debug_exact_sort(const float* vals, int32_t n, int32_t* out) {
   if (!vals || !out || n < 0 || n > 2048) return LLSR_EINVAL;
@@ -596,7 +597,7 @@ extern "C" int32_t llsr_debug_exact_sort(const float* vals, int32_t n, int32_t* 
   int32_t rc = LLSR_OK;
   if (hipMemcpy(dv, vals, sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess) rc = LLSR_EIO;
   if (rc == LLSR_OK) {
-    k_debug_exact_sort<<<1, 64>>>(dv, n, di);
+    k_debug_exact_sort<<<1, 256>>>(dv, n, di);
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
         hipMemcpy(out, di, sizeof(int) * n, hipMemcpyDeviceToHost) != hipSuccess)
       rc = LLSR_EIO;
@@ -606,8 +607,8 @@ extern "C" int32_t llsr_debug_exact_sort(const float* vals, int32_t n, int32_t* 
   return rc;
 }
 
-// Diagnostics (not part of the ABI header): mean device ms of one exact_introsort of vals[0, n)
-// by one wave (k_debug_exact_sort), over `reps` launches.
+// Diagnostics (not part of the ABI header): mean device ms of one block_introsort of vals[0, n)
+// by one 256-thread workgroup (k_debug_exact_sort), over `reps` launches.
 extern "C" float llsr_debug_exact_sort_ms(const float* vals, int32_t n, int32_t reps) {
   if (!vals || n < 1 || n > 2048 || reps < 1) return -1.f;
   float* dv = nullptr;
@@ -617,9 +618,9 @@ extern "C" float llsr_debug_exact_sort_ms(const float* vals, int32_t n, int32_t 
   if (hipMalloc(&dv, sizeof(float) * n) == hipSuccess && hipMalloc(&di, sizeof(int) * n) == hipSuccess &&
       hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess &&
       hipMemcpy(dv, vals, sizeof(float) * n, hipMemcpyHostToDevice) == hipSuccess) {
-    k_debug_exact_sort<<<1, 64>>>(dv, n, di);
+    k_debug_exact_sort<<<1, 256>>>(dv, n, di);
     (void)hipEventRecord(e0, nullptr);
-    for (int r = 0; r < reps; ++r) k_debug_exact_sort<<<1, 64>>>(dv, n, di);
+    for (int r = 0; r < reps; ++r) k_debug_exact_sort<<<1, 256>>>(dv, n, di);
     (void)hipEventRecord(e1, nullptr);
     if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess) ms /= reps;
   }
@@ -1217,7 +1218,9 @@ extern "C" int32_t llsr_scan2scan_reserve(llsr_handle* h, int32_t P, int32_t ms,
   return LLSR_OK;
 }
 
-extern "C" int32_t llsr_scan2scan_batch(llsr_handle* h, const llsr_s2s_batch* b, void* hip_stream) {
+// hint_q / hint_nc: this launch's largest query count and corner-last cloud when the caller knows
+// them (the odometry chain), else 0 = the reserved capacities; they pick the LM instantiation only
+static int32_t s2s_launch(llsr_handle* h, const llsr_s2s_batch* b, void* hip_stream, int hint_q, int hint_nc) {
   if (!h || !b) return fail(h, LLSR_EINVAL, "null argument");
   auto& m = h->s2s;
   if (!m.pool) return fail(h, LLSR_EINVAL, "llsr_scan2scan_reserve not called");
@@ -1256,15 +1259,18 @@ extern "C" int32_t llsr_scan2scan_batch(llsr_handle* h, const llsr_s2s_batch* b,
   // and corner-last cloud fit it (reserved capacities are the batch maxima)
   // bounds: this launch's largest clouds when the caller knows them (the odometry chain), else
   // the reserved capacities
-  const int bq = std::max(m.launch_ms > 0 ? m.launch_ms : m.ms, m.launch_f > 0 ? m.launch_f : m.f);
-  const int bnc = m.launch_nc > 0 ? m.launch_nc : m.nc;
-  m.launch_ms = m.launch_f = m.launch_nc = 0;
-  if (bq <= 1024 && bnc <= 1024)
+  const int bq = hint_q > 0 ? hint_q : std::max(m.ms, m.f);
+  const int bnc = hint_nc > 0 ? hint_nc : m.nc;
+  if (bq <= 1024 && bnc <= 1024) {
     k_s2s_lm<1024, 1024><<<P, kS2SThreads, 0, s>>>(a);
-  else if (bq <= 2560 && bnc <= 1536)
+    m.last_variant = 1024;
+  } else if (bq <= 2560 && bnc <= 1536) {
     k_s2s_lm<2560, 1536><<<P, kS2SThreads, 0, s>>>(a);
-  else
+    m.last_variant = 2560;
+  } else {
     k_s2s_lm<2048, 2048><<<P, kS2SThreads, 0, s>>>(a);
+    m.last_variant = 2048;
+  }
   HIP_OK(h, hipGetLastError());
   HIP_OK(h, hipEventRecord(h->s2s_done, s));
   h->s2s_rec = true;
@@ -1280,6 +1286,15 @@ extern "C" int32_t llsr_scan2scan_batch(llsr_handle* h, const llsr_s2s_batch* b,
   }
   return LLSR_OK;
 }
+
+extern "C" int32_t llsr_scan2scan_batch(llsr_handle* h, const llsr_s2s_batch* b, void* hip_stream) {
+  return s2s_launch(h, b, hip_stream, 0, 0);
+}
+
+// Diagnostics (not part of the ABI header): the LDS rows (1024, 2560 or 2048) of the k_s2s_lm
+// instantiation the last scan-to-scan launch of this handle used, 0 before any; the two large ones
+// run the whole-wave surf walks (tests/test_gpu_fa_lm.py asserts which one a test exercised).
+extern "C" int32_t llsr_debug_s2s_variant(llsr_handle* h) { return h ? h->s2s.last_variant : -1; }
 
 extern "C" int32_t llsr_scan2scan_stats(llsr_handle* h, llsr_s2s_stats* out) {
   if (!h || !out) return LLSR_EINVAL;
@@ -1478,9 +1493,6 @@ extern "C" int32_t llsr_odometry_batch(llsr_handle* h, const float* d_xyzi, cons
   HIP_OK(h, hipMemcpyAsync(o.off + (4 + nxt) * nb, hns, sizeof(int64_t) * nb, hipMemcpyHostToDevice, s));
   rc = llsr_scan2scan_reserve(h, o.B, mMs > 1 ? mMs : 1, mF, mNc > 1 ? mNc : 1, mNs > 1 ? mNs : 1);
   if (rc != LLSR_OK) return rc;
-  h->s2s.launch_ms = mMs > 1 ? mMs : 1;  // the LM instantiation follows this batch, not the reserve
-  h->s2s.launch_f = mF > 1 ? mF : 1;
-  h->s2s.launch_nc = mNc > 1 ? mNc : 1;
   OdoArgs a{};
   a.B = B;
   a.HW = h->dc.HW;
@@ -1508,7 +1520,8 @@ extern "C" int32_t llsr_odometry_batch(llsr_handle* h, const float* d_xyzi, cons
   sb.transform_cur = o.tcur;
   sb.is_degenerate = o.deg;
   sb.report = o.report;
-  rc = llsr_scan2scan_batch(h, &sb, s);
+  // the LM instantiation follows this batch's clouds, not the (high-water) reserve
+  rc = s2s_launch(h, &sb, s, std::max(std::max(mMs, mF), 1), std::max(mNc, 1));
   if (rc != LLSR_OK) return rc;
   k_odo_finish<<<B, 256, 0, s>>>(a);
   HIP_OK(h, hipGetLastError());

@@ -318,16 +318,16 @@ __device__ __forceinline__ int pow2_ceil(int n) {
   return n2;
 }
 
-// Diagnostics (llsr_debug_exact_sort): exact_introsort on one array of n <= kRingMax values; out
-// receives the original positions in sorted order. One wave.
-__global__ __launch_bounds__(64) void k_debug_exact_sort(const float* vals, int n, int* out) {
+// Diagnostics (llsr_debug_exact_sort): the exact std::sort k_select_ring runs (block_introsort,
+// 256 threads) on one array of n <= kRingMax values; out receives the original positions in sorted
+// order.
+__global__ __launch_bounds__(256) void k_debug_exact_sort(const float* vals, int n, int* out) {
   __shared__ uint64_t key[kRingMax];
   __shared__ uint16_t Lp[kRingMax], Rp[kRingMax];
-  __shared__ int stk[3 * kSortStack];
-  for (int t = threadIdx.x; t < n; t += 64) key[t] = ((uint64_t)__float_as_uint(vals[t]) << 32) | (uint32_t)t;
-  wave_sync_lds();
-  exact_introsort(key, n, Lp, Rp, stk, CurvLess{});
-  for (int t = threadIdx.x; t < n; t += 64) out[t] = (int)(uint32_t)key[t];
+  __shared__ BlockSortLds bsl;
+  for (int t = threadIdx.x; t < n; t += 256) key[t] = ((uint64_t)__float_as_uint(vals[t]) << 32) | (uint32_t)t;
+  block_introsort<256>(key, n, Lp, Rp, bsl, CurvLess{});
+  for (int t = threadIdx.x; t < n; t += 256) out[t] = (int)(uint32_t)key[t];
 }
 
 // Serial greedy pick (FA:1175-1259) over a candidate list already in visiting order, by one wave:
@@ -484,7 +484,7 @@ __global__ __launch_bounds__(256, 5) void k_select_ring(DevCfg c, DevBufs d) {
   const bool ph_in = ph >= ws && ph - ws < wn;
   const float ph_curv = ph < 5 ? 0.0f : curv[ph];  // cloudCurvature[0..4] is never written (FA:819)
   if (sp == 4 && !ph_in && tid == 0) atomicAdd(&d.counts[b * kCnt + C_PHOUT], 1);
-  __shared__ int stk[3 * kSortStack];
+  __shared__ BlockSortLds bsl;  // block_introsort's range lists
   __shared__ int s_flag, s_exact;
   // exact-order triggers: ties between eligible keys (found after each fast sort) and, in ring 0, an
   // exact zero that could take position 4 from the phantom for the next frame
@@ -507,9 +507,7 @@ __global__ __launch_bounds__(256, 5) void k_select_ring(DevCfg c, DevBufs d) {
       const int ind = p == 4 ? ph : p;
       key[t] = ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)ind;
     }
-    __syncthreads();
-    if (tid < 64) exact_introsort(key, nRng, cpos, rstart, stk, CurvLess{});
-    __syncthreads();
+    block_introsort<256>(key, nRng, cpos, rstart, bsl, CurvLess{});
     if (tid == 0) {
       if (sp == 4) d.phantom[b] = (int)(uint32_t)key[0];
       atomicAdd(&d.counts[b * kCnt + C_EXACT], 1);
@@ -722,10 +720,7 @@ __global__ __launch_bounds__(256, 5) void k_select_ring(DevCfg c, DevBufs d) {
     __syncthreads();
     if (c.dbg_phase <= 5) return;
     // Lp = rstart, Rp = the (dead) window bytes
-    // (dbg_phase 100: diagnostic re-launch without the depth limit, to time the heap-sort fallback)
-    if (tid < 64)
-      exact_introsort(key, L, rstart, reinterpret_cast<uint16_t*>(win_raw), stk, VoxLess{}, c.dbg_phase == 100 ? 1000 : -1);
-    __syncthreads();
+    block_introsort<256>(key, L, rstart, reinterpret_cast<uint16_t*>(win_raw), bsl, VoxLess{});
     if (c.dbg_phase <= 6) return;
     // voxel heads in sorted order; sorted position t = u * 256 + tid sits in slot u of a lane, so a
     // wave's heads of one slot are consecutive voxels and their centroids are stored contiguously;

@@ -672,7 +672,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
   const int tid = threadIdx.x;
 #ifdef LLSR_S2S_PROF
   unsigned long long tprev = wall_clock64(), tAks = 0, tAkc = 0, tA = 0, tB = 0, tC = 0, tF = 0, tW = 0;
-  int nfb_total = 0;  // queries the surf / corner shells left to the block-wide scan (report.skipped)
+  int nfb_total = 0;  // queries the surf / corner shells left to the block-wide scan (report.degenerate >> 1)
 #endif
   __shared__ float t[6];
   __shared__ float matP[9];
@@ -1115,7 +1115,9 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
     r.transform_cur[0] = (float)tAks; r.transform_cur[1] = (float)tAkc; r.transform_cur[2] = (float)tA;
     r.transform_cur[3] = (float)tB; r.transform_cur[4] = (float)tC; r.transform_cur[5] = (float)tF;
     r.ms = (float)tW;
-    r.skipped = nfb_total;
+    // the fallback count rides in report.degenerate's upper bits: `skipped` keeps its FA:2506 meaning,
+    // bit 0 stays isDegenerate, and the state itself (a.degen) is untouched
+    r.degenerate = isDeg | (nfb_total << 1);
 #endif
     a.degen[p] = isDeg;
   }

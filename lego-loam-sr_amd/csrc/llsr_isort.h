@@ -305,4 +305,213 @@ __device__ void exact_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp
   wave_sync_lds();
 }
 
+// ---- the whole workgroup on one array ----------------------------------------------------------
+// block_introsort: the same std::sort, with the ranges above 64 elements partitioned level by level
+// by every thread of the workgroup at once. libstdc++'s recursion only ever touches disjoint
+// sub-ranges, each carrying its own depth limit, so the order in which they are partitioned does
+// not change the result: a level partitions every open range (> 64 elements, depth left) together.
+// Per level each thread classifies a contiguous chunk of positions (L stop: !(a < pivot) in
+// (first, last); R stop: !(pivot < a) in [first, last), as in exact_introsort) and ONE block scan of
+// the packed (L, R) counts gives every stop its rank inside its range (ranks minus the range's base;
+// R ranks counted from the right end). The stop lists go to Lp / Rp at the range's own offset, the
+// pairs k < ks swap (the L side of pair k tests L[k] < R[k] and the last such k writes ks), and
+// lane j of wave 0 computes range j's cut and children. Finished ranges (<= 64 elements, or depth 0:
+// libstdc++'s heap sort) get a mark in their first key's payload bits 24-31 (which no caller uses:
+// payloads are indices < 2^24; the comparators read only the high word); after the last level the
+// marks are listed, stripped, and the waves finish the ranges round-robin (small_sort in registers,
+// the rare heap sort by one lane). n <= 2048 = 8 positions per thread.
+constexpr int kBsRanges = 32;  // open ranges have > 64 elements and are disjoint: < 2048 / 64
+struct BlockSortLds {
+  int first[kBsRanges], last[kBsRanges], dep[kBsRanges], ks[kBsRanges];
+  int glf[kBsRanges], grf[kBsRanges], gll[kBsRanges], grl[kBsRanges];  // (L, R) stops before first / last
+  uint64_t piv[kBsRanges];
+  int scan[16];
+  int na, nr;
+};
+constexpr uint32_t kBsMark = 0x80000000u;        // payload bit 31: a finished range starts here
+constexpr uint64_t kBsStrip = ~0xFF000000ull;    // payload bits 24-31: the mark and the range's depth
+
+template <int kNT, class Lt>
+__device__ void block_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp, BlockSortLds& s, Lt lt) {
+  static_assert(kNT % 64 == 0 && kNT * 8 >= 2048, "block_introsort: 8 positions per thread cover 2048");
+  constexpr int kPer = 2048 / kNT;
+  constexpr int kNW = kNT / 64;
+  const int tid = threadIdx.x, l = lane_id(), w = tid >> 6;
+  __syncthreads();  // key[0, n) written by the caller
+  if (n <= 1) return;
+  const int lg = 31 - __clz(n);
+  if (n <= 64) {  // std::sort's whole loop inside one small range
+    if (w == 0) small_sort(key, 0, n, 2 * lg, lt);
+    __syncthreads();
+    return;
+  }
+  if (tid == 0) {
+    s.first[0] = 0;
+    s.last[0] = n;
+    s.dep[0] = 2 * lg;
+    s.na = 1;
+  }
+  __syncthreads();
+  const int per = (n + kNT - 1) / kNT;
+  const int c0 = min(tid * per, n), c1 = min(c0 + per, n);
+  // the open range holding position i, walking up from the chunk's first (ranges sorted by first)
+  auto range_of = [&](int na, int& jj, int i) {
+    while (jj + 1 < na && s.first[jj + 1] <= i) ++jj;
+    return jj >= 0 && i < s.last[jj];
+  };
+  auto chunk_range = [&](int na) {  // the last range with first <= c0, or -1
+    int lo = 0, hi = na - 1;
+    if (s.first[0] > c0) return -1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s.first[mid] <= c0) lo = mid;
+      else hi = mid - 1;
+    }
+    return lo;
+  };
+  while (true) {
+    const int na = s.na;
+    if (na == 0) break;
+    // __move_median_to_first(first, first + 1, mid, last - 1); the pivot
+    if (w == 0 && l < na) {
+      const int f = s.first[l], e = s.last[l];
+      const int a = f + 1, b = f + (e - f) / 2, c = e - 1;
+      const uint64_t va = key[a], vb = key[b], vc = key[c];
+      int m;
+      if (lt(va, vb)) m = lt(vb, vc) ? b : (lt(va, vc) ? c : a);
+      else m = lt(va, vc) ? a : (lt(vb, vc) ? c : b);
+      const uint64_t vm = m == a ? va : (m == b ? vb : vc);
+      key[m] = key[f];
+      key[f] = vm;
+      s.piv[l] = vm;
+      s.ks[l] = 0;
+    }
+    __syncthreads();
+    // stops of this thread's positions
+    const int j0 = chunk_range(na);
+    uint32_t mL = 0, mR = 0;
+    {
+      int jj = j0;
+#pragma unroll 1
+      for (int u = 0; u < kPer; ++u) {
+        const int i = c0 + u;
+        if (i >= c1 || !range_of(na, jj, i)) continue;
+        const uint64_t v = key[i], P = s.piv[jj];
+        if (i > s.first[jj] && !lt(v, P)) mL |= 1u << u;
+        if (!lt(P, v)) mR |= 1u << u;
+      }
+    }
+    int tot;
+    const int ex = block_excl_scan((int)(__popc(mL) | (__popc(mR) << 16)), s.scan, &tot);
+    const int gl0 = ex & 0xffff, gr0 = ex >> 16;  // stops before c0 (whole array)
+    // each range's counts at its first and past its last position
+    {
+      int jj = j0;
+#pragma unroll 1
+      for (int u = 0; u < kPer; ++u) {
+        const int i = c0 + u;
+        if (i >= c1 || !range_of(na, jj, i)) continue;
+        const uint32_t below = (1u << u) - 1u;
+        const int gl = gl0 + __popc(mL & below), gr = gr0 + __popc(mR & below);
+        if (i == s.first[jj]) { s.glf[jj] = gl; s.grf[jj] = gr; }
+        if (i == s.last[jj] - 1) { s.gll[jj] = gl + (int)((mL >> u) & 1u); s.grl[jj] = gr + (int)((mR >> u) & 1u); }
+      }
+    }
+    __syncthreads();
+    // L[k] / R[k] at the range's offset (L ascending, R from the right end)
+    {
+      int jj = j0;
+#pragma unroll 1
+      for (int u = 0; u < kPer; ++u) {
+        const int i = c0 + u;
+        if (i >= c1 || !range_of(na, jj, i)) continue;
+        const uint32_t below = (1u << u) - 1u;
+        const int f = s.first[jj];
+        if ((mL >> u) & 1u) Lp[f + gl0 + __popc(mL & below) - s.glf[jj]] = (uint16_t)i;
+        if ((mR >> u) & 1u) Rp[f + s.grl[jj] - (gr0 + __popc(mR & below)) - 1] = (uint16_t)i;
+      }
+    }
+    __syncthreads();
+    // pairs k < ks swap; the L side of pair k checks L[k] < R[k] (monotone in k)
+    {
+      int jj = j0;
+#pragma unroll 1
+      for (int u = 0; u < kPer; ++u) {
+        const int i = c0 + u;
+        if (i >= c1 || !((mL >> u) & 1u) || !range_of(na, jj, i)) continue;
+        const int f = s.first[jj];
+        const int k = gl0 + __popc(mL & ((1u << u) - 1u)) - s.glf[jj];
+        const int nL = s.gll[jj] - s.glf[jj], nR = s.grl[jj] - s.grf[jj], nm = nL < nR ? nL : nR;
+        if (k < nm) {
+          const int r = Rp[f + k];
+          if (i < r) {
+            const uint64_t a = key[i];
+            key[i] = key[r];
+            key[r] = a;
+            if (!(k + 1 < nm && Lp[f + k + 1] < Rp[f + k + 1])) s.ks[jj] = k + 1;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // lane j of wave 0: range j's cut, its children; open ones (> 64, depth left) form the next
+    // level's list in position order, the others get their start mark (and depth)
+    if (w == 0) {
+      int f = 0, e = 0, cut = 0, d = 0;
+      bool o0 = false, o1 = false;
+      if (l < na) {
+        f = s.first[l];
+        e = s.last[l];
+        d = s.dep[l] - 1;
+        const int ks = s.ks[l], nL = s.gll[l] - s.glf[l];
+        cut = (ks > 0 && (ks >= nL || Lp[f + ks] >= Rp[f + ks - 1])) ? Rp[f + ks - 1] : Lp[f + ks];
+        o0 = cut - f > 64 && d > 0;
+        o1 = e - cut > 64 && d > 0;
+        const uint64_t mk = (uint64_t)(kBsMark | ((uint32_t)d << 24));
+        if (!o0 && cut > f) key[f] |= mk;
+        if (!o1 && e > cut) key[cut] |= mk;
+      }
+      const int c = (o0 ? 1 : 0) + (o1 ? 1 : 0);
+      const int incl = wave_incl_scan_add(c);
+      const int ex0 = incl - c;
+      const int nna = __builtin_amdgcn_readlane(incl, 63);
+      wave_sync_lds();  // every lane has read its old entry
+      if (o0) { s.first[ex0] = f; s.last[ex0] = cut; s.dep[ex0] = d; }
+      if (o1) { const int o = ex0 + (o0 ? 1 : 0); s.first[o] = cut; s.last[o] = e; s.dep[o] = d; }
+      if (l == 0) s.na = nna;
+    }
+    __syncthreads();
+  }
+  // list the finished ranges (starts -> Lp, depths -> Rp) and strip the marks
+  uint32_t mk = 0;
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int i = c0 + u;
+    if (i < c1 && ((uint32_t)key[i] & kBsMark)) mk |= 1u << u;
+  }
+  int nr;
+  const int rb = block_excl_scan(__popc(mk), s.scan, &nr);
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    if (!((mk >> u) & 1u)) continue;
+    const int i = c0 + u;
+    const uint64_t v = key[i];
+    const int k = rb + __popc(mk & ((1u << u) - 1u));
+    Lp[k] = (uint16_t)i;
+    Rp[k] = (uint16_t)(((uint32_t)v >> 24) & 0x7f);
+    key[i] = v & kBsStrip;
+  }
+  __syncthreads();
+  for (int k = w; k < nr; k += kNW) {
+    const int f = Lp[k], e = k + 1 < nr ? Lp[k + 1] : n, d = Rp[k];
+    if (e - f <= 64) {
+      small_sort(key, f, e - f, d, lt);
+    } else {  // depth exhausted above 64 elements: libstdc++'s __partial_sort of the range
+      if (l == 0) heap_sort_range(key, f, e, lt);
+      wave_sync_lds();
+    }
+  }
+  __syncthreads();
+}
+
 }  // namespace llsr

@@ -193,7 +193,8 @@ class Pipeline:
         self._check(lib().llsr_reset_state(self._h), "llsr_reset_state")
 
     def set_voxel_order(self, order: int):
-        """_abi.LLSR_VOXEL_ORDER_INPUT (default) or LLSR_VOXEL_ORDER_PCL (the less-flat VoxelGrid)."""
+        """_abi.LLSR_VOXEL_ORDER_PCL (default: the reference's std::sort order) or LLSR_VOXEL_ORDER_INPUT
+        (ring order inside each voxel) for the less-flat VoxelGrid."""
         self._check(lib().llsr_set_voxel_order(self._h, order), "llsr_set_voxel_order")
 
     def process_scan(self, xyzi: np.ndarray) -> dict:

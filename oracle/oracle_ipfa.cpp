@@ -143,9 +143,9 @@ void voxel_grid(const std::vector<P4>& in, float leaf, std::vector<P4>& out, boo
 
 // ------------------------------------------------------------------------------------------
 struct oracle_state {
-  // true: the less-flat VoxelGrid sums each voxel in input order (the device's default,
-  // LLSR_VOXEL_ORDER_INPUT); false: in std::sort's order, as PCL (LLSR_VOXEL_ORDER_PCL)
-  bool vg_stable = true;
+  // false (default): the less-flat VoxelGrid sums each voxel in std::sort's order, as PCL
+  // (LLSR_VOXEL_ORDER_PCL, the device's default); true: in input order (LLSR_VOXEL_ORDER_INPUT)
+  bool vg_stable = false;
   llsr_config cfg;
   int H, W, HW;
   // IP derived constants (IP:117-121, 849)

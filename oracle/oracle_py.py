@@ -127,7 +127,7 @@ def ref_lib():
 class Oracle:
     """One reference pipeline (IP + FA feature stage) with its own carry-over state."""
 
-    def __init__(self, cfg: _abi.Config, pcl_voxel_order: bool = False):
+    def __init__(self, cfg: _abi.Config, pcl_voxel_order: bool = True):
         self.cfg = cfg
         self._h = lib().oracle_create(C.byref(cfg))
         if not self._h:
@@ -379,7 +379,7 @@ class OracleOdometry:
     feature stage, then updateTransformation against the last clouds, integrateTransformation and
     publishCloudsLast's TransformToEnd (first scan: checkSystemInitialization)."""
 
-    def __init__(self, cfg: _abi.Config, pcl_voxel_order: bool = False):
+    def __init__(self, cfg: _abi.Config, pcl_voxel_order: bool = True):
         self.cfg = cfg
         self.ora = Oracle(cfg, pcl_voxel_order)
         self.shadow = shadow_points()
@@ -563,7 +563,7 @@ class OracleMapping:
     device does; `stable` = True would sum each voxel in input order instead (diagnostics)."""
 
     def __init__(self, cfg: _abi.Config, mo_mode: int, radius=50.0, keypose_leaf=1.0, corner_leaf=0.2,
-                 surf_leaf=0.4, outlier_leaf=0.4, stable: bool = False, pcl_voxel_order: bool = False,
+                 surf_leaf=0.4, outlier_leaf=0.4, stable: bool = False, pcl_voxel_order: bool = True,
                  loop_closure: bool | None = None, search_num: int = 50):
         """loop_closure None: the config block of the lidar (enable_loop_closure true for the
         HDL-64E block, CFG:159; false for VLP-16, CFG:23)."""

@@ -17,6 +17,7 @@ cfg = default_config(lidar, 2048 if lidar == "hdl64e" else None)
 pts, off = synth.make_batch(B, lidar, distinct=int(os.environ.get("DISTINCT", "16")))
 d_pts, d_off = torch.from_numpy(pts).cuda(), torch.from_numpy(off).cuda()
 pipe = Pipeline(cfg, max_batch=B, max_points=int(np.diff(off).max()))
+pipe.set_voxel_order(int(os.environ.get("VOXEL_ORDER", "1")))  # 1 = LLSR_VOXEL_ORDER_PCL
 for _ in range(3):
     pipe.process_batch(d_pts.data_ptr(), d_off.data_ptr(), B)
 pipe.set_profiling(True)

@@ -38,7 +38,23 @@ for k in sorted(set(fetch) | set(write)):
     f = (sum(fv) / len(fv) if fv else 0.0) * 1024 * 2
     w = (sum(wv) / len(wv) if wv else 0.0) * 1024
     out[k] = {"fetch_bytes_x2": f, "write_bytes": w, "hbm_bytes": f + w, "launches": max(len(fv), len(wv))}
+
+
+def measured_build(sub):
+    """The build id the profiled bench itself printed (its JSON line in <sub>.log): the library
+    that was measured, not whatever the parsing process would load."""
+    ids = set()
+    for line in open(os.path.join(d, sub + ".log"), errors="replace"):
+        line = line.strip()
+        if line.startswith("{") and '"build_id"' in line:
+            ids.add(json.loads(line)["build_id"])
+    if len(ids) != 1:
+        raise SystemExit(f"pmc_parse: {sub}.log names build ids {sorted(ids)}, expected exactly one")
+    return ids.pop()
+
+
+bid = {measured_build("fetch"), measured_build("write")}
+if len(bid) != 1:
+    raise SystemExit(f"pmc_parse: the FETCH_SIZE and WRITE_SIZE passes measured different builds {sorted(bid)}")
 # the build these counters measured: bench.py reports the bytes only for the same build
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "lego-loam-sr_amd"))
-import llsr  # noqa: E402
-print(json.dumps({"batch": batch, "build_id": llsr.build_id(), "kernels": out}, indent=1))
+print(json.dumps({"batch": batch, "build_id": bid.pop(), "kernels": out}, indent=1))

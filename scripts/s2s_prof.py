@@ -45,7 +45,8 @@ for n in range(6):  # 2 warm-up batches, then one of each frame
         f = pipe.odometry_fetch(b)
         t = f["lm"]["transform_cur"] / 100.0  # 100 MHz ticks -> us
         rows.append(list(t[:6]) + [f["lm"]["ms"] / 100.0, f["lm"]["surf_iterations"], f["lm"]["corner_iterations"],
-                                   f["lm"]["n_surf_corr"], f["lm"]["n_corner_corr"], f["lm"]["skipped"]])
+                                   f["lm"]["n_surf_corr"], f["lm"]["n_corner_corr"],
+                                   int(f["lm"]["degenerate"]) >> 1])  # the diagnostics build's fallback count
         per.setdefault((n, b % 2), []).append(rows[-1])
 r = np.array(rows)
 print(json.dumps({"lidar": lidar, "B": B,

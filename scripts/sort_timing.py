@@ -1,4 +1,8 @@
-"""Diagnostics: device time of one wave's exact introsort (llsr_isort.h) on ring-like inputs."""
+"""Diagnostics: device time of the exact introsort (llsr_isort.h block_introsort, one 256-thread
+workgroup) on the voxel ids of real less-flat rings and on synthetic inputs.
+
+    python scripts/sort_timing.py [seed:ring ...]   (default: seed 5, rings 0, 3, .., 15)
+"""
 import ctypes as C
 import json
 import os
@@ -23,11 +27,14 @@ def t(a):
 
 
 cfg = _abi.config_for("vlp16")
-o = oracle_py.Oracle(cfg)
-r = o.process(synth.make_scan(5, "vlp16"))
-loam, sr, er, lab = r["loam_xyzi"], r["start_ring_index"], r["end_ring_index"], r["label"]
+todo = [tuple(int(x) for x in a.split(":")) for a in sys.argv[1:]] or [(5, ring) for ring in range(0, 16, 3)]
+scans = {}
 res = {}
-for ring in range(0, 16, 3):
+for seed, ring in todo:
+    if seed not in scans:  # the first scan of a fresh pipeline, as the bench's distinct clouds
+        scans[seed] = oracle_py.Oracle(cfg).process(synth.make_scan(seed, "vlp16"))
+    r = scans[seed]
+    loam, sr, er, lab = r["loam_xyzi"], r["start_ring_index"], r["end_ring_index"], r["label"]
     idx = np.arange(sr[ring], er[ring] + 1)
     p = loam[idx[lab[idx] <= 0]]
     inv = np.float32(5.0)
@@ -39,6 +46,6 @@ for ring in range(0, 16, 3):
     v = (i[:, 0] + i[:, 1] * div[0] + i[:, 2] * div[0] * div[1]).astype(np.float32)
     n = len(v)
     rng = np.random.default_rng(ring)
-    res[f"ring{ring}"] = {"n": n, "voxel_ids_us": t(v), "random_us": t(rng.random(n)), "sorted_us": t(np.arange(n)),
+    res[f"seed{seed}_ring{ring}"] = {"n": n, "voxel_ids_us": t(v), "random_us": t(rng.random(n)), "sorted_us": t(np.arange(n)),
                           "few_values_us": t(rng.integers(0, 8, n)), "all_equal_us": t(np.zeros(n))}
 print(json.dumps(res))

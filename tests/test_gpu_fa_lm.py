@@ -7,11 +7,13 @@ runFeatureAssociation does (oracle_py.fa_lm_inputs). The device sums the normal 
 the oracle's correspondence order, so the bar is bit-exact: transformCur, iteration counts,
 correspondence counts and the degeneracy flag all equal.
 """
+import ctypes as C
+
 import numpy as np
 import pytest
 
 import oracle_py
-from llsr import Pipeline, _abi, default_config, shadow_points, synth
+from llsr import Pipeline, _abi, default_config, lib, shadow_points, synth
 
 pytestmark = pytest.mark.gpu
 
@@ -174,16 +176,21 @@ def test_scan2scan_degenerate_surf_bit_exact(require_gpu):
     assert not errs, "\n".join(errs)
 
 
+@pytest.mark.parametrize("lidar", ["vlp16", "hdl64e"])
 @pytest.mark.parametrize("variant", ["twins", "shuffled", "rings_swapped"])
-def test_scan2scan_surf_cloud_order(require_gpu, variant):
+def test_scan2scan_surf_cloud_order(require_gpu, variant, lidar):
     """The surf tripod search reads the last cloud's order (FA:1737-1803 walk it by index): the
     device walks the cloud from the kNN hit in both directions, skipping 8-point blocks and
     64-point superblocks whose bounding boxes (k_s2s_boxes) cannot beat the current minimum and
     hold no ring stop. Twins (every point repeated in place: every distance ties) pin the tie
     rule; a shuffled cloud and one with two ring blocks swapped break the ring order the stops
-    and boxes see."""
-    cfg, pairs = _pairs("vlp16", [31, 32, 33])
+    and boxes see. VLP-16 pairs run the per-lane walks (the <1024, 1024> instantiation), HDL-64E
+    pairs the whole-wave walks of the large instantiations (asserted)."""
+    hdl = lidar == "hdl64e"
+    cfg, pairs = _pairs(lidar, [41, 42] if hdl else [31, 32, 33], 2048 if hdl else None)
     pipe = Pipeline(cfg)
+    variant_of = lib().llsr_debug_s2s_variant
+    variant_of.restype, variant_of.argtypes = C.c_int32, [C.c_void_p]
     errs = []
     rng = np.random.default_rng(7)
     for k, (sharp, flat, cl, sl) in enumerate(pairs):
@@ -198,6 +205,8 @@ def test_scan2scan_surf_cloud_order(require_gpu, variant):
         sl = np.ascontiguousarray(sl)
         t = np.full(6, 0.002, np.float32)
         g = pipe.scan2scan(sharp, flat, cl, sl, t, 0)
+        used = variant_of(pipe._h)
+        assert (used in (2560, 2048)) if hdl else used == 1024, (lidar, used)
         o = oracle_py.scan2scan(cfg, sharp, flat, cl, sl, t, 0)
         errs += [f"pair {k}: {e}" for e in _same(g, o)]
     pipe.close()

@@ -8,8 +8,8 @@ and at the end the key poses (cloudKeyPoses6D).
 
 Bar: bit-exact end to end — counts, LM reports, every pose and the key poses equal the oracle's.
 MapOptimization's VoxelGrids on both sides sum a voxel in the order libstdc++'s std::sort leaves
-PCL's index_vector, the feature stage's less-flat VoxelGrid in the handle's order (input order by
-default, LLSR_VOXEL_ORDER_PCL in one test), and both LMs sum their normal equations in Eigen's order.
+PCL's index_vector, the feature stage's less-flat VoxelGrid in the handle's order (PCL's by default,
+the opt-in LLSR_VOXEL_ORDER_INPUT in one test), and both LMs sum their normal equations in Eigen's order.
 """
 import numpy as np
 import pytest
@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 POSES = ("transform_sum", "transform_tobe_mapped", "transform_bef_mapped", "transform_aft_mapped")
 
 
-def _drive(mode, seeds, frames, iters=None, pcl=False, lidar="vlp16", search_num=None, divider=1,
+def _drive(mode, seeds, frames, iters=None, pcl=True, lidar="vlp16", search_num=None, divider=1,
            spare_slots=0):
     """search_num None: the lidar's config block through map_cfg NULL (HDL-64E: loop closure,
     search num 50); else the block with that surrounding_keyframe_search_num. spare_slots: the
@@ -40,8 +40,8 @@ def _drive(mode, seeds, frames, iters=None, pcl=False, lidar="vlp16", search_num
         search_num = 50
     else:
         pipe.mapping_init(mode, map_config(lidar, surrounding_keyframe_search_num=search_num))
-    if pcl:
-        pipe.set_voxel_order(_abi.LLSR_VOXEL_ORDER_PCL)
+    if not pcl:
+        pipe.set_voxel_order(_abi.LLSR_VOXEL_ORDER_INPUT)
     oras = [oracle_py.OracleMapping(cfg, mode, pcl_voxel_order=pcl, loop_closure=lc, search_num=search_num)
             for _ in seeds]
     errs, surf_its = [], []
@@ -104,8 +104,8 @@ def test_mapping_chain_lm_applied(require_gpu):
     assert not errs, "\n".join(errs)
 
 
-def test_mapping_chain_pcl_voxel_order(require_gpu):
-    errs, _ = _drive(_abi.LLSR_MODE_LM_APPLIED, [2, 140], 5, pcl=True)
+def test_mapping_chain_input_voxel_order(require_gpu):
+    errs, _ = _drive(_abi.LLSR_MODE_LM_APPLIED, [2, 140], 5, pcl=False)
     assert not errs, "\n".join(errs)
 
 

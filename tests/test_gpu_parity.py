@@ -3,8 +3,8 @@
 Bit-exact for labels / indices / clouds (see _compare.py for the bar). Sequences of scans run
 through one handle so the FeatureAssociation carry-over state (picked / cloudLabel arrays,
 phantom smoothness entry) is exercised exactly as in the reference's long-running node. Both
-less-flat VoxelGrid orders: the default (input order) against the oracle's input-order statement,
-LLSR_VOXEL_ORDER_PCL against its PCL (std::sort order) statement.
+less-flat VoxelGrid orders: the default (LLSR_VOXEL_ORDER_PCL, std::sort's order as the reference)
+against the oracle's PCL statement, the opt-in LLSR_VOXEL_ORDER_INPUT against its input-order one.
 """
 import numpy as np
 import pytest
@@ -16,11 +16,11 @@ import oracle_py
 pytestmark = pytest.mark.gpu
 
 
-def _run_pair(lidar, horizontal, seeds, pcl=False):
+def _run_pair(lidar, horizontal, seeds, pcl=True):
     cfg = default_config(lidar, horizontal)
     pipe = Pipeline(cfg, max_points=2 * cfg.num_vertical_scans * cfg.num_horizontal_scans)
-    if pcl:
-        pipe.set_voxel_order(_abi.LLSR_VOXEL_ORDER_PCL)
+    if not pcl:
+        pipe.set_voxel_order(_abi.LLSR_VOXEL_ORDER_INPUT)
     ora = oracle_py.Oracle(cfg, pcl_voxel_order=pcl)
     failures = []
     for s in seeds:
@@ -39,9 +39,11 @@ def test_vlp16_sequence_bit_exact(require_gpu):
     assert not failures, "\n".join(f"seed {s}:\n  " + "\n  ".join(e) for s, e in failures)
 
 
-def test_pcl_voxel_order_bit_exact(require_gpu):
-    for lidar, hz, seeds in (("vlp16", None, [1, 2, 70]), ("hdl64e", 2048, [5])):
-        failures = _run_pair(lidar, hz, seeds, pcl=True)
+def test_voxel_orders_bit_exact(require_gpu):
+    """HDL-64E in the default (PCL) order, and both lidars in the opt-in input order."""
+    for lidar, hz, seeds, pcl in (("hdl64e", 2048, [5, 6], True), ("vlp16", None, [1, 2, 70], False),
+                                  ("hdl64e", 2048, [5], False)):
+        failures = _run_pair(lidar, hz, seeds, pcl=pcl)
         assert not failures, "\n".join(f"{lidar} seed {s}:\n  " + "\n  ".join(e) for s, e in failures)
 
 
@@ -49,8 +51,8 @@ def test_voxel_orders_differ_only_in_centroid_bits(require_gpu):
     """The two orders give the same voxels in the same order; centroids differ in the last bits at most."""
     cfg = default_config("vlp16")
     a = Pipeline(cfg, max_points=40000)
-    b = Pipeline(cfg, max_points=40000)
-    b.set_voxel_order(_abi.LLSR_VOXEL_ORDER_PCL)
+    a.set_voxel_order(_abi.LLSR_VOXEL_ORDER_INPUT)
+    b = Pipeline(cfg, max_points=40000)  # the default: LLSR_VOXEL_ORDER_PCL
     diff = 0
     for s in (1, 2, 3):
         pts = synth.make_scan(s, "vlp16")
