@@ -31,7 +31,7 @@ template <bool kLds> __global__ void k_label(DevCfg, DevBufs);
 __global__ void k_segment(DevCfg, const float4*, const int64_t*, DevBufs);
 __global__ void k_fa_points(DevCfg, DevBufs);
 __global__ void k_select_ring(DevCfg, DevBufs);
-__global__ void k_debug_exact_sort(const float*, int, int*);
+__global__ void k_debug_exact_sort(const float*, int, int*, long long*);
 __global__ void k_fa_concat(DevCfg, DevBufs);
 __global__ void k_dbscan_adj(DevCfg, DevBufs);
 __global__ void k_vis_clouds(DevCfg, DevBufs, int, float4*, int*);
@@ -597,7 +597,7 @@ extern "C" int32_t llsr_debug_exact_sort(const float* vals, int32_t n, int32_t* 
   int32_t rc = LLSR_OK;
   if (hipMemcpy(dv, vals, sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess) rc = LLSR_EIO;
   if (rc == LLSR_OK) {
-    k_debug_exact_sort<<<1, 256>>>(dv, n, di);
+    k_debug_exact_sort<<<1, 256>>>(dv, n, di, nullptr);
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
         hipMemcpy(out, di, sizeof(int) * n, hipMemcpyDeviceToHost) != hipSuccess)
       rc = LLSR_EIO;
@@ -618,9 +618,9 @@ extern "C" float llsr_debug_exact_sort_ms(const float* vals, int32_t n, int32_t 
   if (hipMalloc(&dv, sizeof(float) * n) == hipSuccess && hipMalloc(&di, sizeof(int) * n) == hipSuccess &&
       hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess &&
       hipMemcpy(dv, vals, sizeof(float) * n, hipMemcpyHostToDevice) == hipSuccess) {
-    k_debug_exact_sort<<<1, 256>>>(dv, n, di);
+    k_debug_exact_sort<<<1, 256>>>(dv, n, di, nullptr);
     (void)hipEventRecord(e0, nullptr);
-    for (int r = 0; r < reps; ++r) k_debug_exact_sort<<<1, 256>>>(dv, n, di);
+    for (int r = 0; r < reps; ++r) k_debug_exact_sort<<<1, 256>>>(dv, n, di, nullptr);
     (void)hipEventRecord(e1, nullptr);
     if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess) ms /= reps;
   }
@@ -629,6 +629,30 @@ extern "C" float llsr_debug_exact_sort_ms(const float* vals, int32_t n, int32_t 
   if (dv) (void)hipFree(dv);
   if (di) (void)hipFree(di);
   return ms;
+}
+
+// Diagnostics (not part of the ABI header): one block_introsort of vals[0, n) with clock stamps;
+// cycles[0..2] = core clocks the sort took, cycles[3] = 0 (phase split: reserved).
+extern "C" int32_t llsr_debug_exact_sort_phases(const float* vals, int32_t n, long long* cycles) {
+  if (!vals || !cycles || n < 1 || n > 2048) return LLSR_EINVAL;
+  float* dv = nullptr;
+  int* di = nullptr;
+  long long* dp = nullptr;
+  int32_t rc = LLSR_OK;
+  if (hipMalloc(&dv, sizeof(float) * n) != hipSuccess || hipMalloc(&di, sizeof(int) * n) != hipSuccess ||
+      hipMalloc(&dp, 4 * sizeof(long long)) != hipSuccess)
+    rc = LLSR_ENODEV;
+  if (rc == LLSR_OK && hipMemcpy(dv, vals, sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess) rc = LLSR_EIO;
+  if (rc == LLSR_OK) {
+    for (int r = 0; r < 3; ++r) k_debug_exact_sort<<<1, 256>>>(dv, n, di, dp);  // warm: the last run counts
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(cycles, dp, 4 * sizeof(long long), hipMemcpyDeviceToHost) != hipSuccess)
+      rc = LLSR_EIO;
+  }
+  if (dv) (void)hipFree(dv);
+  if (di) (void)hipFree(di);
+  if (dp) (void)hipFree(dp);
+  return rc;
 }
 
 // Diagnostics (not part of the ABI header): re-launch kernel k on the last batch's buffers with

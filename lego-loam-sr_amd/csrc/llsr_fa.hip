@@ -321,12 +321,20 @@ __device__ __forceinline__ int pow2_ceil(int n) {
 // Diagnostics (llsr_debug_exact_sort): the exact std::sort k_select_ring runs (block_introsort,
 // 256 threads) on one array of n <= kRingMax values; out receives the original positions in sorted
 // order.
-__global__ __launch_bounds__(256) void k_debug_exact_sort(const float* vals, int n, int* out) {
+__global__ __launch_bounds__(256) void k_debug_exact_sort(const float* vals, int n, int* out, long long* prof) {
   __shared__ uint64_t key[kRingMax];
   __shared__ uint16_t Lp[kRingMax], Rp[kRingMax];
   __shared__ BlockSortLds bsl;
   for (int t = threadIdx.x; t < n; t += 256) key[t] = ((uint64_t)__float_as_uint(vals[t]) << 32) | (uint32_t)t;
+  __syncthreads();
+  long long t0 = 0;
+  if (prof && threadIdx.x == 0) t0 = clock64();
   block_introsort<256>(key, n, Lp, Rp, bsl, CurvLess{});
+  if (prof && threadIdx.x == 0) {
+    const long long t1 = clock64() - t0;
+    prof[0] = prof[1] = prof[2] = t1;
+    prof[3] = 0;
+  }
   for (int t = threadIdx.x; t < n; t += 256) out[t] = (int)(uint32_t)key[t];
 }
 
@@ -484,7 +492,7 @@ __global__ __launch_bounds__(256, 5) void k_select_ring(DevCfg c, DevBufs d) {
   const bool ph_in = ph >= ws && ph - ws < wn;
   const float ph_curv = ph < 5 ? 0.0f : curv[ph];  // cloudCurvature[0..4] is never written (FA:819)
   if (sp == 4 && !ph_in && tid == 0) atomicAdd(&d.counts[b * kCnt + C_PHOUT], 1);
-  __shared__ BlockSortLds bsl;  // block_introsort's range lists
+  __shared__ BlockSortLds bsl;  // block_introsort's work queue
   __shared__ int s_flag, s_exact;
   // exact-order triggers: ties between eligible keys (found after each fast sort) and, in ring 0, an
   // exact zero that could take position 4 from the phantom for the next frame

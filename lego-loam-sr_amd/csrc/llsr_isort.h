@@ -163,14 +163,14 @@ __device__ void small_sort(uint64_t* key, int f, int n, int d, Lt lt) {
   const unsigned long long lem = l == 63 ? ~0ull : (2ull << l) - 1ull;  // bits <= l
   uint64_t v = l < n ? key[f + l] : 0ull;
   int dep = d;                  // depth limit of the range starting at this lane
-  unsigned long long bnd = 1ull, leafm = 0ull;
+  unsigned long long bnd = 1ull, leafm = 0ull, heapm = 0ull;
   int cur = 0;
   while (cur < n) {
     const unsigned long long above = cur == 63 ? 0ull : bnd & ~((2ull << cur) - 1ull);
     const int e = above ? __ffsll((long long)above) - 1 : n;
     const int dd = __builtin_amdgcn_readlane(dep, cur);
     if (e - cur <= 16) { leafm |= 1ull << cur; cur = e; continue; }
-    if (dd == 0) { reg_heap_sort(v, cur, e, lt); leafm |= 1ull << cur; cur = e; continue; }
+    if (dd == 0) { reg_heap_sort(v, cur, e, lt); leafm |= 1ull << cur; heapm |= 1ull << cur; cur = e; continue; }
     // __move_median_to_first(first, first + 1, mid, last - 1)
     const int a = cur + 1, b = cur + (e - cur) / 2, c = e - 1;
     const uint64_t va = rdlane64(v, a), vb = rdlane64(v, b), vc = rdlane64(v, c);
@@ -208,30 +208,120 @@ __device__ void small_sort(uint64_t* key, int f, int n, int d, Lt lt) {
     if (l == cur || l == cut) dep = dd - 1;
     bnd |= 1ull << cut;
   }
-  // each leaf's insertion sort = its stable sort
+  // each leaf's insertion sort = its stable sort (<= 16 elements; a heap-sorted leaf is sorted
+  // already): the rank of every element among its leaf's, the leaf read back from LDS at once
   const int s0 = 63 - __clzll((long long)(leafm & lem));
   const unsigned long long up = leafm & ~lem;
   const int t0 = up ? __ffsll((long long)up) - 1 : n;
-  int len = l < n ? t0 - s0 : 0;
-  int mx = len;
+  const int len = l < n ? t0 - s0 : 0;
+  if (l < n) key[f + l] = v;
+  wave_sync_lds();
+  int rank = l - s0;
+  if (l < n && !((heapm >> s0) & 1ull)) {
+    rank = 0;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) { const int y = __shfl_xor(mx, o); mx = y > mx ? y : mx; }
-  int rank = 0;
-  for (int q = 0; q < mx; ++q) {
-    const int sq = s0 + q;
-    const uint64_t w = shfl64(v, sq < 64 ? sq : 63);
-    if (q < len && (lt(w, v) || (!lt(v, w) && sq < l))) ++rank;
+    for (int h = 0; h < 16; h += 8) {
+      uint32_t w[8];  // the comparators read the high words only
+#pragma unroll
+      for (int q = 0; q < 8; ++q) w[q] = (uint32_t)(key[f + min(s0 + h + q, n - 1)] >> 32);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint64_t wq = (uint64_t)w[q] << 32;
+        if (h + q < len && (lt(wq, v) || (!lt(v, wq) && s0 + h + q < l))) ++rank;
+      }
+    }
   }
+  wave_sync_lds();
   if (l < n) key[f + s0 + rank] = v;
   wave_sync_lds();
 }
 
-// Executed by one full wave (64 lanes). Lp / Rp: n uint16 each; stk: 3 * kSortStack ints.
+// ---- libstdc++'s heap sort of a range above 64 elements, by one wave ---------------------------
+// __make_heap: the sift-downs of one depth touch disjoint subtrees, so a depth's parents run on
+// parallel lanes (deepest depth first, as libstdc++'s decreasing parent order implies). Each pop
+// (__pop_heap + __adjust_heap + __push_heap) is evaluated from the heap as it stands before it: the
+// hole's path to a leaf follows the larger child (right unless right < left), chosen for a whole
+// 6-level subtree below the hole at once (lane i loads the two children of subtree node i; the
+// choices are one ballot, the walk a few scalar steps per level); the values move up the path by
+// one place, and the popped value settles where __push_heap stops: above the deepest path
+// position whose (moved-up) parent is not less than it, which is one ballot over the path.
+template <class Lt>
+__device__ void wave_heap_sort(uint64_t* key, int f, int e, Lt lt) {
+  const int l = lane_id();
+  const int len0 = e - f;
+  if (len0 < 2) return;
+  {
+    const int lastp = (len0 - 2) / 2;
+    for (int d = 31 - __clz(lastp + 1); d >= 0; --d) {
+      const int lo = (1 << d) - 1, hi = min((2 << d) - 2, lastp);
+      for (int p = lo + l; p <= hi; p += 64) heap_adjust(key, f, p, len0, key[f + p], lt);
+      wave_sync_lds();
+    }
+  }
+  for (int len = len0 - 1; len >= 1; --len) {
+    // __pop_heap(first, first + len + 1, first + len): value = last, last = root
+    const uint64_t value = key[f + len];
+    const uint64_t root = key[f];
+    const int lim = (len - 1) / 2;
+    int hole = 0, L = 0;
+    int pnode = 0, pnext = 0;  // lane t < L: path node p_t and the child p_{t+1} the hole moved to
+    uint64_t pchild = 0;       // lane t < L: the value of p_{t+1} before the pop
+    bool more = hole < lim;
+    while (more) {
+      // the subtree of 63 nodes below the hole: lane i = its BFS node i, at absolute index a
+      const int lv = 31 - __clz(l + 1);
+      const int a = ((hole + 1) << lv) - 1 + (l + 1 - (1 << lv));
+      bool right = false;
+      uint64_t chosen = 0;
+      if (l < 63 && a < lim) {
+        const uint64_t cl = key[f + 2 * a + 1], cr = key[f + 2 * a + 2];
+        right = !lt(cr, cl);  // __adjust_heap: second = right child, then -- if right < left
+        chosen = right ? cr : cl;
+      }
+      const unsigned long long rm = __ballot(right);
+      int i = 0, ai = hole;
+      for (int k = 0; k < 6; ++k) {
+        if (!(ai < lim)) break;
+        const int ci = 2 * i + ((rm >> i) & 1ull ? 2 : 1);
+        const int ca = 2 * ai + ((rm >> i) & 1ull ? 2 : 1);
+        const uint64_t cv = rdlane64(chosen, i);
+        if (l == L) { pnode = ai; pnext = ca; pchild = cv; }
+        ++L;
+        i = ci;
+        ai = ca;
+      }
+      hole = ai;
+      more = hole < lim;  // 6 levels done with the hole still above the last parent: next subtree
+    }
+    if ((len & 1) == 0 && hole == (len - 2) / 2) {  // the last parent's only (left) child
+      const uint64_t cv = key[f + 2 * hole + 1];
+      if (l == L) { pnode = hole; pnext = 2 * hole + 1; pchild = cv; }
+      ++L;
+      hole = 2 * hole + 1;
+    }
+    // __push_heap from the hole: path position t + 1 moves up while its new parent value (the old
+    // value of p_{t+1}) is less than `value`; it stops at j = 1 + the deepest t < L where it is not
+    const unsigned long long stay = __ballot(l < L && !lt(pchild, value));
+    const int j = stay ? 64 - __clzll((long long)stay) : 0;
+    const int pj = __builtin_amdgcn_readlane(pnode, j < L ? j : 0);
+    wave_sync_lds();
+    if (l == 0) key[f + len] = root;
+    if (l < j) key[f + pnode] = pchild;
+    if (l == 0) key[f + (j < L ? pj : hole)] = value;
+    wave_sync_lds();
+    (void)pnext;
+  }
+}
+
+// Executed by one full wave (64 lanes). Lp / Rp: n uint16 each; stk: 3 * kStack ints.
 // key[0, n) ends up as std::sort leaves it. depth0 < 0: the whole array (depth limit 2 * lg(n));
 // else a sub-range of a larger sort that inherits the remaining depth limit of its parent range
-// (llsr_map.hip's segmented VoxelGrid). Ranges above 64 elements are partitioned in LDS; each range
-// of at most 64 is finished in registers (small_sort).
-template <class Lt>
+// (llsr_map.hip's segmented VoxelGrid, block_introsort's ranges). Ranges above 64 elements are
+// partitioned in LDS: one pass lists the L stops (ascending) and the R stops (ascending; R[k], the
+// k-th from the right, is Rp[nR - 1 - k]); each range of at most 64 is finished in registers
+// (small_sort), a range above 64 whose depth limit is spent by wave_heap_sort. The stack holds at
+// most one entry per level of the current path: <= depth limit + 1 entries.
+template <class Lt, int kStack = kSortStack>
 __device__ void exact_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp, int* stk, Lt lt,
                                 int depth0 = -1) {
   const int l = lane_id();
@@ -245,53 +335,48 @@ __device__ void exact_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp
     bool heaped = false;
     while (rl - rf > 64) {
       if (rd == 0) {
-        if (l == 0) heap_sort_range(key, rf, rl, lt);
-        wave_sync_lds();
+        wave_heap_sort(key, rf, rl, lt);
         heaped = true;
         break;
       }
       rd--;
-      const int mid = rf + (rl - rf) / 2;
-      if (l == 0) {  // __move_median_to_first(first, first+1, mid, last-1)
-        const int a = rf + 1, b = mid, c = rl - 1;
-        int m;
-        if (lt(key[a], key[b])) m = lt(key[b], key[c]) ? b : (lt(key[a], key[c]) ? c : a);
-        else m = lt(key[a], key[c]) ? a : (lt(key[b], key[c]) ? c : b);
-        const uint64_t t = key[rf]; key[rf] = key[m]; key[m] = t;
-      }
+      // __move_median_to_first(first, first+1, mid, last-1)
+      const int a = rf + 1, b = rf + (rl - rf) / 2, c = rl - 1;
+      const uint64_t va = key[a], vb = key[b], vc = key[c], vf = key[rf];
+      int m;
+      if (lt(va, vb)) m = lt(vb, vc) ? b : (lt(va, vc) ? c : a);
+      else m = lt(va, vc) ? a : (lt(vb, vc) ? c : b);
+      const uint64_t P = m == a ? va : (m == b ? vb : vc);
       wave_sync_lds();
-      const uint64_t P = key[rf];
+      if (l == 0) { key[m] = vf; key[rf] = P; }
+      wave_sync_lds();
       int nL = 0, nR = 0;
-      for (int c0 = rf + 1; c0 < rl; c0 += 64) {
+      for (int c0 = rf; c0 < rl; c0 += 64) {
         const int i = c0 + l;
-        const bool f = i < rl && !lt(key[i], P);
-        const unsigned long long m = __ballot(f);
-        if (f) Lp[nL + __popcll(m & ltm)] = (uint16_t)i;
-        nL += __popcll(m);
-      }
-      for (int c0 = rl - 1; c0 >= rf; c0 -= 64) {
-        const int j = c0 - l;
-        const bool f = j >= rf && !lt(P, key[j]);
-        const unsigned long long m = __ballot(f);
-        if (f) Rp[nR + __popcll(m & ltm)] = (uint16_t)j;
-        nR += __popcll(m);
+        const uint64_t v = i < rl ? key[i] : 0ull;
+        const bool fl = i < rl && i > rf && !lt(v, P);
+        const bool fr = i < rl && !lt(P, v);
+        const unsigned long long mL = __ballot(fl), mR = __ballot(fr);
+        if (fl) Lp[nL + __popcll(mL & ltm)] = (uint16_t)i;
+        if (fr) Rp[nR + __popcll(mR & ltm)] = (uint16_t)i;
+        nL += __popcll(mL);
+        nR += __popcll(mR);
       }
       wave_sync_lds();
       const int nm = nL < nR ? nL : nR;
       int ks = nm;  // first k with !(L[k] < R[k]) (monotone)
       for (int c0 = 0; c0 < nm; c0 += 64) {
         const int k = c0 + l;
-        const unsigned long long m = __ballot(k < nm && !(Lp[k] < Rp[k]));
+        const unsigned long long m = __ballot(k < nm && !(Lp[k] < Rp[nR - 1 - k]));
         if (m) { ks = c0 + __ffsll((long long)m) - 1; break; }
       }
-      const int cut = (ks > 0 && (ks >= nL || Lp[ks] >= Rp[ks - 1])) ? Rp[ks - 1] : Lp[ks];
+      const int cut = (ks > 0 && (ks >= nL || Lp[ks] >= Rp[nR - ks])) ? Rp[nR - ks] : Lp[ks];
       for (int k = l; k < ks; k += 64) {
-        const int a = Lp[k], b = Rp[k];
-        const uint64_t t = key[a]; key[a] = key[b]; key[b] = t;
+        const int a2 = Lp[k], b2 = Rp[nR - 1 - k];
+        const uint64_t t = key[a2]; key[a2] = key[b2]; key[b2] = t;
       }
       wave_sync_lds();
-      // the right part waits (at most one entry per level of the current path: <= 2*lg(n) + 1
-      // <= 23 < kSortStack); the left part continues here
+      // the right part waits; the left part continues here
       if (l == 0) { stk[3 * sp] = cut; stk[3 * sp + 1] = rl; stk[3 * sp + 2] = rd; }
       ++sp;
       rl = cut;
@@ -306,210 +391,120 @@ __device__ void exact_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp
 }
 
 // ---- the whole workgroup on one array ----------------------------------------------------------
-// block_introsort: the same std::sort, with the ranges above 64 elements partitioned level by level
-// by every thread of the workgroup at once. libstdc++'s recursion only ever touches disjoint
-// sub-ranges, each carrying its own depth limit, so the order in which they are partitioned does
-// not change the result: a level partitions every open range (> 64 elements, depth left) together.
-// Per level each thread classifies a contiguous chunk of positions (L stop: !(a < pivot) in
-// (first, last); R stop: !(pivot < a) in [first, last), as in exact_introsort) and ONE block scan of
-// the packed (L, R) counts gives every stop its rank inside its range (ranks minus the range's base;
-// R ranks counted from the right end). The stop lists go to Lp / Rp at the range's own offset, the
-// pairs k < ks swap (the L side of pair k tests L[k] < R[k] and the last such k writes ks), and
-// lane j of wave 0 computes range j's cut and children. Finished ranges (<= 64 elements, or depth 0:
-// libstdc++'s heap sort) get a mark in their first key's payload bits 24-31 (which no caller uses:
-// payloads are indices < 2^24; the comparators read only the high word); after the last level the
-// marks are listed, stripped, and the waves finish the ranges round-robin (small_sort in registers,
-// the rare heap sort by one lane). n <= 2048 = 8 positions per thread.
-constexpr int kBsRanges = 32;  // open ranges have > 64 elements and are disjoint: < 2048 / 64
+// block_introsort: the same std::sort by the workgroup's waves sharing one work queue.
+// libstdc++'s recursion only ever touches disjoint sub-ranges, each carrying its own depth limit,
+// so the order in which they are processed does not change the result. A wave takes a range from
+// the queue and runs libstdc++'s loop on it as exact_introsort does (partition in LDS, continue
+// with the left part), pushing every right part to the queue for any wave to take; a range of at
+// most 64 elements is finished in registers (small_sort), one above 64 with no depth left by
+// wave_heap_sort. The queue is an LDS stack under a lock held by one lane for a few instructions;
+// the waves stop when every element has been finished (a counter of the elements still open).
+// Every wave's work is its own: no workgroup barrier between partitions, and the sort costs about
+// what one wave doing it all would, spread over the waves. n <= 2048.
+constexpr int kBsQueue = 128;  // pending ranges: one per level of the paths being descended (<= 4 x 23)
 struct BlockSortLds {
-  int first[kBsRanges], last[kBsRanges], dep[kBsRanges], ks[kBsRanges];
-  int glf[kBsRanges], grf[kBsRanges], gll[kBsRanges], grl[kBsRanges];  // (L, R) stops before first / last
-  uint64_t piv[kBsRanges];
-  int scan[16];
-  int na, nr;
+  int q[kBsQueue];  // first | last << 12 | depth << 24
+  int top, lock, open;
 };
-constexpr uint32_t kBsMark = 0x80000000u;        // payload bit 31: a finished range starts here
-constexpr uint64_t kBsStrip = ~0xFF000000ull;    // payload bits 24-31: the mark and the range's depth
 
 template <int kNT, class Lt>
-__device__ void block_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp, BlockSortLds& s, Lt lt) {
-  static_assert(kNT % 64 == 0 && kNT * 8 >= 2048, "block_introsort: 8 positions per thread cover 2048");
-  constexpr int kPer = 2048 / kNT;
-  constexpr int kNW = kNT / 64;
-  const int tid = threadIdx.x, l = lane_id(), w = tid >> 6;
+__device__ __forceinline__ void block_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp, BlockSortLds& s, Lt lt) {
+  static_assert(kNT % 64 == 0, "block_introsort: whole waves");
+  const int tid = threadIdx.x, l = lane_id();
+  const unsigned long long ltm = (1ull << l) - 1ull;
   __syncthreads();  // key[0, n) written by the caller
   if (n <= 1) return;
   const int lg = 31 - __clz(n);
   if (n <= 64) {  // std::sort's whole loop inside one small range
-    if (w == 0) small_sort(key, 0, n, 2 * lg, lt);
+    if (tid < 64) small_sort(key, 0, n, 2 * lg, lt);
     __syncthreads();
     return;
   }
   if (tid == 0) {
-    s.first[0] = 0;
-    s.last[0] = n;
-    s.dep[0] = 2 * lg;
-    s.na = 1;
+    s.q[0] = 0 | (n << 12) | ((2 * lg) << 24);
+    s.top = 1;
+    s.lock = 0;
+    s.open = n;
   }
   __syncthreads();
-  const int per = (n + kNT - 1) / kNT;
-  const int c0 = min(tid * per, n), c1 = min(c0 + per, n);
-  // the open range holding position i, walking up from the chunk's first (ranges sorted by first)
-  auto range_of = [&](int na, int& jj, int i) {
-    while (jj + 1 < na && s.first[jj + 1] <= i) ++jj;
-    return jj >= 0 && i < s.last[jj];
+  auto acquire = [&]() {
+    while (atomicCAS(&s.lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   };
-  auto chunk_range = [&](int na) {  // the last range with first <= c0, or -1
-    int lo = 0, hi = na - 1;
-    if (s.first[0] > c0) return -1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (s.first[mid] <= c0) lo = mid;
-      else hi = mid - 1;
-    }
-    return lo;
+  auto release = [&]() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    atomicExch(&s.lock, 0);
   };
   while (true) {
-    const int na = s.na;
-    if (na == 0) break;
-    // __move_median_to_first(first, first + 1, mid, last - 1); the pivot
-    if (w == 0 && l < na) {
-      const int f = s.first[l], e = s.last[l];
-      const int a = f + 1, b = f + (e - f) / 2, c = e - 1;
-      const uint64_t va = key[a], vb = key[b], vc = key[c];
+    // take a range (lane 0 under the lock), or learn that every element is finished
+    int item = -1;
+    if (l == 0) {
+      acquire();
+      if (s.top > 0) item = s.q[--s.top];
+      else if (atomicAdd(&s.open, 0) == 0) item = -2;
+      release();
+    }
+    item = __builtin_amdgcn_readfirstlane(item);
+    if (item == -2) break;
+    if (item == -1) {
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    int rf = item & 0xfff, rl = (item >> 12) & 0xfff, rd = (item >> 24) & 0x3f;
+    while (rl - rf > 64 && rd > 0) {
+      rd--;
+      // __move_median_to_first(first, first+1, mid, last-1)
+      const int a = rf + 1, b = rf + (rl - rf) / 2, c = rl - 1;
+      const uint64_t va = key[a], vb = key[b], vc = key[c], vf = key[rf];
       int m;
       if (lt(va, vb)) m = lt(vb, vc) ? b : (lt(va, vc) ? c : a);
       else m = lt(va, vc) ? a : (lt(vb, vc) ? c : b);
-      const uint64_t vm = m == a ? va : (m == b ? vb : vc);
-      key[m] = key[f];
-      key[f] = vm;
-      s.piv[l] = vm;
-      s.ks[l] = 0;
-    }
-    __syncthreads();
-    // stops of this thread's positions
-    const int j0 = chunk_range(na);
-    uint32_t mL = 0, mR = 0;
-    {
-      int jj = j0;
-#pragma unroll 1
-      for (int u = 0; u < kPer; ++u) {
-        const int i = c0 + u;
-        if (i >= c1 || !range_of(na, jj, i)) continue;
-        const uint64_t v = key[i], P = s.piv[jj];
-        if (i > s.first[jj] && !lt(v, P)) mL |= 1u << u;
-        if (!lt(P, v)) mR |= 1u << u;
-      }
-    }
-    int tot;
-    const int ex = block_excl_scan((int)(__popc(mL) | (__popc(mR) << 16)), s.scan, &tot);
-    const int gl0 = ex & 0xffff, gr0 = ex >> 16;  // stops before c0 (whole array)
-    // each range's counts at its first and past its last position
-    {
-      int jj = j0;
-#pragma unroll 1
-      for (int u = 0; u < kPer; ++u) {
-        const int i = c0 + u;
-        if (i >= c1 || !range_of(na, jj, i)) continue;
-        const uint32_t below = (1u << u) - 1u;
-        const int gl = gl0 + __popc(mL & below), gr = gr0 + __popc(mR & below);
-        if (i == s.first[jj]) { s.glf[jj] = gl; s.grf[jj] = gr; }
-        if (i == s.last[jj] - 1) { s.gll[jj] = gl + (int)((mL >> u) & 1u); s.grl[jj] = gr + (int)((mR >> u) & 1u); }
-      }
-    }
-    __syncthreads();
-    // L[k] / R[k] at the range's offset (L ascending, R from the right end)
-    {
-      int jj = j0;
-#pragma unroll 1
-      for (int u = 0; u < kPer; ++u) {
-        const int i = c0 + u;
-        if (i >= c1 || !range_of(na, jj, i)) continue;
-        const uint32_t below = (1u << u) - 1u;
-        const int f = s.first[jj];
-        if ((mL >> u) & 1u) Lp[f + gl0 + __popc(mL & below) - s.glf[jj]] = (uint16_t)i;
-        if ((mR >> u) & 1u) Rp[f + s.grl[jj] - (gr0 + __popc(mR & below)) - 1] = (uint16_t)i;
-      }
-    }
-    __syncthreads();
-    // pairs k < ks swap; the L side of pair k checks L[k] < R[k] (monotone in k)
-    {
-      int jj = j0;
-#pragma unroll 1
-      for (int u = 0; u < kPer; ++u) {
-        const int i = c0 + u;
-        if (i >= c1 || !((mL >> u) & 1u) || !range_of(na, jj, i)) continue;
-        const int f = s.first[jj];
-        const int k = gl0 + __popc(mL & ((1u << u) - 1u)) - s.glf[jj];
-        const int nL = s.gll[jj] - s.glf[jj], nR = s.grl[jj] - s.grf[jj], nm = nL < nR ? nL : nR;
-        if (k < nm) {
-          const int r = Rp[f + k];
-          if (i < r) {
-            const uint64_t a = key[i];
-            key[i] = key[r];
-            key[r] = a;
-            if (!(k + 1 < nm && Lp[f + k + 1] < Rp[f + k + 1])) s.ks[jj] = k + 1;
-          }
-        }
-      }
-    }
-    __syncthreads();
-    // lane j of wave 0: range j's cut, its children; open ones (> 64, depth left) form the next
-    // level's list in position order, the others get their start mark (and depth)
-    if (w == 0) {
-      int f = 0, e = 0, cut = 0, d = 0;
-      bool o0 = false, o1 = false;
-      if (l < na) {
-        f = s.first[l];
-        e = s.last[l];
-        d = s.dep[l] - 1;
-        const int ks = s.ks[l], nL = s.gll[l] - s.glf[l];
-        cut = (ks > 0 && (ks >= nL || Lp[f + ks] >= Rp[f + ks - 1])) ? Rp[f + ks - 1] : Lp[f + ks];
-        o0 = cut - f > 64 && d > 0;
-        o1 = e - cut > 64 && d > 0;
-        const uint64_t mk = (uint64_t)(kBsMark | ((uint32_t)d << 24));
-        if (!o0 && cut > f) key[f] |= mk;
-        if (!o1 && e > cut) key[cut] |= mk;
-      }
-      const int c = (o0 ? 1 : 0) + (o1 ? 1 : 0);
-      const int incl = wave_incl_scan_add(c);
-      const int ex0 = incl - c;
-      const int nna = __builtin_amdgcn_readlane(incl, 63);
-      wave_sync_lds();  // every lane has read its old entry
-      if (o0) { s.first[ex0] = f; s.last[ex0] = cut; s.dep[ex0] = d; }
-      if (o1) { const int o = ex0 + (o0 ? 1 : 0); s.first[o] = cut; s.last[o] = e; s.dep[o] = d; }
-      if (l == 0) s.na = nna;
-    }
-    __syncthreads();
-  }
-  // list the finished ranges (starts -> Lp, depths -> Rp) and strip the marks
-  uint32_t mk = 0;
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    const int i = c0 + u;
-    if (i < c1 && ((uint32_t)key[i] & kBsMark)) mk |= 1u << u;
-  }
-  int nr;
-  const int rb = block_excl_scan(__popc(mk), s.scan, &nr);
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    if (!((mk >> u) & 1u)) continue;
-    const int i = c0 + u;
-    const uint64_t v = key[i];
-    const int k = rb + __popc(mk & ((1u << u) - 1u));
-    Lp[k] = (uint16_t)i;
-    Rp[k] = (uint16_t)(((uint32_t)v >> 24) & 0x7f);
-    key[i] = v & kBsStrip;
-  }
-  __syncthreads();
-  for (int k = w; k < nr; k += kNW) {
-    const int f = Lp[k], e = k + 1 < nr ? Lp[k + 1] : n, d = Rp[k];
-    if (e - f <= 64) {
-      small_sort(key, f, e - f, d, lt);
-    } else {  // depth exhausted above 64 elements: libstdc++'s __partial_sort of the range
-      if (l == 0) heap_sort_range(key, f, e, lt);
+      const uint64_t P = m == a ? va : (m == b ? vb : vc);
       wave_sync_lds();
+      if (l == 0) { key[m] = vf; key[rf] = P; }
+      wave_sync_lds();
+      // __unguarded_partition: L stops (!(a < P), (rf, rl)) and R stops (!(P < a), [rf, rl)), both
+      // listed ascending (R[k], the k-th from the right, is Rp[nR - 1 - k])
+      int nL = 0, nR = 0;
+      for (int c0 = rf; c0 < rl; c0 += 64) {
+        const int i = c0 + l;
+        const uint64_t v = i < rl ? key[i] : 0ull;
+        const bool fl = i < rl && i > rf && !lt(v, P);
+        const bool fr = i < rl && !lt(P, v);
+        const unsigned long long mL = __ballot(fl), mR = __ballot(fr);
+        if (fl) Lp[rf + nL + __popcll(mL & ltm)] = (uint16_t)i;
+        if (fr) Rp[rf + nR + __popcll(mR & ltm)] = (uint16_t)i;
+        nL += __popcll(mL);
+        nR += __popcll(mR);
+      }
+      wave_sync_lds();
+      const uint16_t* L = Lp + rf;
+      const uint16_t* R = Rp + rf;
+      const int nm = nL < nR ? nL : nR;
+      int ks = nm;  // first k with !(L[k] < R[k]) (monotone)
+      for (int c0 = 0; c0 < nm; c0 += 64) {
+        const int k = c0 + l;
+        const unsigned long long mk = __ballot(k < nm && !(L[k] < R[nR - 1 - k]));
+        if (mk) { ks = c0 + __ffsll((long long)mk) - 1; break; }
+      }
+      const int cut = (ks > 0 && (ks >= nL || L[ks] >= R[nR - ks])) ? R[nR - ks] : L[ks];
+      for (int k = l; k < ks; k += 64) {
+        const int x = L[k], y = R[nR - 1 - k];
+        const uint64_t t = key[x]; key[x] = key[y]; key[y] = t;
+      }
+      wave_sync_lds();
+      // the right part goes to the queue (any wave may take it), the left part continues here
+      if (l == 0) {
+        acquire();
+        s.q[s.top++] = cut | (rl << 12) | (rd << 24);
+        release();
+      }
+      rl = cut;
     }
+    if (rl - rf > 64) wave_heap_sort(key, rf, rl, lt);  // depth limit spent: __partial_sort
+    else if (rl - rf > 1) small_sort(key, rf, rl - rf, rd, lt);
+    wave_sync_lds();
+    if (l == 0) atomicSub(&s.open, rl - rf);
   }
   __syncthreads();
 }

@@ -21,6 +21,19 @@ f = llsr.lib().llsr_debug_exact_sort_ms
 f.restype, f.argtypes = C.c_float, [C.c_void_p, C.c_int32, C.c_int32]
 
 
+g = llsr.lib().llsr_debug_exact_sort_phases
+g.restype, g.argtypes = C.c_int32, [C.c_void_p, C.c_int32, C.c_void_p]
+
+
+def phases(a):
+    """core clocks (from the start) at the end of the levels, the listing and the small ranges, and
+    the number of levels"""
+    a = np.ascontiguousarray(a, np.float32)
+    c = np.zeros(4, np.int64)
+    assert g(a.ctypes.data, len(a), c.ctypes.data) == 0
+    return [int(x) for x in c]
+
+
 def t(a):
     a = np.ascontiguousarray(a, np.float32)
     return round(float(f(a.ctypes.data, len(a), 20)) * 1e3, 1)  # us
@@ -46,6 +59,7 @@ for seed, ring in todo:
     v = (i[:, 0] + i[:, 1] * div[0] + i[:, 2] * div[0] * div[1]).astype(np.float32)
     n = len(v)
     rng = np.random.default_rng(ring)
-    res[f"seed{seed}_ring{ring}"] = {"n": n, "voxel_ids_us": t(v), "random_us": t(rng.random(n)), "sorted_us": t(np.arange(n)),
+    res[f"seed{seed}_ring{ring}"] = {"n": n, "voxel_ids_us": t(v), "voxel_ids_phase_clocks": phases(v),
+                                      "all_equal_phase_clocks": phases(np.zeros(n)), "random_us": t(rng.random(n)), "sorted_us": t(np.arange(n)),
                           "few_values_us": t(rng.integers(0, 8, n)), "all_equal_us": t(np.zeros(n))}
 print(json.dumps(res))
