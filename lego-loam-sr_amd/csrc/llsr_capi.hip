@@ -631,8 +631,9 @@ extern "C" float llsr_debug_exact_sort_ms(const float* vals, int32_t n, int32_t 
   return ms;
 }
 
-// Diagnostics (not part of the ABI header): one block_introsort of vals[0, n) with clock stamps;
-// cycles[0..2] = core clocks the sort took, cycles[3] = 0 (phase split: reserved).
+// Diagnostics (not part of the ABI header): one block_introsort of vals[0, n) with clock stamps:
+// cycles[0] = core clocks of the sort, cycles[1] = the block-wide part, cycles[2 + 4 w + 0..3] =
+// wave w's clocks in partitions, small sorts, heap sorts, and waiting at the end (18 values used).
 extern "C" int32_t llsr_debug_exact_sort_phases(const float* vals, int32_t n, long long* cycles) {
   if (!vals || !cycles || n < 1 || n > 2048) return LLSR_EINVAL;
   float* dv = nullptr;
@@ -640,13 +641,13 @@ extern "C" int32_t llsr_debug_exact_sort_phases(const float* vals, int32_t n, lo
   long long* dp = nullptr;
   int32_t rc = LLSR_OK;
   if (hipMalloc(&dv, sizeof(float) * n) != hipSuccess || hipMalloc(&di, sizeof(int) * n) != hipSuccess ||
-      hipMalloc(&dp, 4 * sizeof(long long)) != hipSuccess)
+      hipMalloc(&dp, 21 * sizeof(long long)) != hipSuccess || hipMemset(dp, 0, 21 * sizeof(long long)) != hipSuccess)
     rc = LLSR_ENODEV;
   if (rc == LLSR_OK && hipMemcpy(dv, vals, sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess) rc = LLSR_EIO;
   if (rc == LLSR_OK) {
     for (int r = 0; r < 3; ++r) k_debug_exact_sort<<<1, 256>>>(dv, n, di, dp);  // warm: the last run counts
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpy(cycles, dp, 4 * sizeof(long long), hipMemcpyDeviceToHost) != hipSuccess)
+        hipMemcpy(cycles, dp, 21 * sizeof(long long), hipMemcpyDeviceToHost) != hipSuccess)
       rc = LLSR_EIO;
   }
   if (dv) (void)hipFree(dv);

@@ -329,12 +329,8 @@ __global__ __launch_bounds__(256) void k_debug_exact_sort(const float* vals, int
   __syncthreads();
   long long t0 = 0;
   if (prof && threadIdx.x == 0) t0 = clock64();
-  block_introsort<256>(key, n, Lp, Rp, bsl, CurvLess{});
-  if (prof && threadIdx.x == 0) {
-    const long long t1 = clock64() - t0;
-    prof[0] = prof[1] = prof[2] = t1;
-    prof[3] = 0;
-  }
+  block_introsort<256>(key, n, Lp, Rp, bsl, CurvLess{}, prof ? prof + 1 : nullptr);
+  if (prof && threadIdx.x == 0) prof[0] = clock64() - t0;
   for (int t = threadIdx.x; t < n; t += 256) out[t] = (int)(uint32_t)key[t];
 }
 
@@ -492,7 +488,7 @@ __global__ __launch_bounds__(256, 5) void k_select_ring(DevCfg c, DevBufs d) {
   const bool ph_in = ph >= ws && ph - ws < wn;
   const float ph_curv = ph < 5 ? 0.0f : curv[ph];  // cloudCurvature[0..4] is never written (FA:819)
   if (sp == 4 && !ph_in && tid == 0) atomicAdd(&d.counts[b * kCnt + C_PHOUT], 1);
-  __shared__ BlockSortLds bsl;  // block_introsort's work queue
+  __shared__ BlockSortLds bsl;  // block_introsort's top ranges and per-wave stacks
   __shared__ int s_flag, s_exact;
   // exact-order triggers: ties between eligible keys (found after each fast sort) and, in ring 0, an
   // exact zero that could take position 4 from the phantom for the next frame

@@ -155,9 +155,12 @@ __device__ void reg_heap_sort(uint64_t& v, int f, int e, Lt lt) {
     reg_heap_adjust(v, f, 0, last - f, val, lt);
   }
 }
-// key[f, f + n), n <= 64, remaining depth limit d: finished exactly as std::sort would.
+// key[f, f + n), n <= 64, remaining depth limit d: finished exactly as std::sort would. Lp[f, f + n)
+// and Rp[f, f + n) are scratch: each partition lists its L stops (ascending) and R stops
+// (ascending; the k-th from the right is R[nR - 1 - k]) there as lane numbers, so the k-th pair,
+// ks and the cut are plain LDS reads.
 template <class Lt>
-__device__ void small_sort(uint64_t* key, int f, int n, int d, Lt lt) {
+__device__ void small_sort(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int f, int n, int d, Lt lt) {
   const int l = lane_id();
   const unsigned long long ltm = (1ull << l) - 1ull;
   const unsigned long long lem = l == 63 ? ~0ull : (2ull << l) - 1ull;  // bits <= l
@@ -165,6 +168,8 @@ __device__ void small_sort(uint64_t* key, int f, int n, int d, Lt lt) {
   int dep = d;                  // depth limit of the range starting at this lane
   unsigned long long bnd = 1ull, leafm = 0ull, heapm = 0ull;
   int cur = 0;
+  uint16_t* L = Lp + f;
+  uint16_t* R = Rp + f;
   while (cur < n) {
     const unsigned long long above = cur == 63 ? 0ull : bnd & ~((2ull << cur) - 1ull);
     const int e = above ? __ffsll((long long)above) - 1 : n;
@@ -187,23 +192,24 @@ __device__ void small_sort(uint64_t* key, int f, int n, int d, Lt lt) {
     if (l == cur) v = vm;
     else if (l == mi) v = v0;
     const uint64_t P = vm;
-    // __unguarded_partition: stop lists L (ascending, (cur, e)) and R (descending, [cur, e))
-    const unsigned long long mL = __ballot(l > cur && l < e && !lt(v, P));
-    const unsigned long long mR = __ballot(l >= cur && l < e && !lt(P, v));
+    // __unguarded_partition: stop lists L ((cur, e)) and R ([cur, e)), ascending, in LDS
+    const bool isL = l > cur && l < e && !lt(v, P), isR = l >= cur && l < e && !lt(P, v);
+    const unsigned long long mL = __ballot(isL), mR = __ballot(isR);
     const int nL = __popcll(mL), nR = __popcll(mR), nm = nL < nR ? nL : nR;
-    const int Lk = l < nL ? select_bit(mL, l) : 64;
-    const int Rk = l < nR ? select_bit(mR, nR - 1 - l) : -1;
+    const int kL = __popcll(mL & ltm), kRa = __popcll(mR & ltm), kR = nR - 1 - kRa;  // kR: rank from the right
+    if (isL) L[kL] = (uint16_t)l;
+    if (isR) R[kRa] = (uint16_t)l;
+    wave_sync_lds();
+    const int Lk = l < nm ? L[l] : 64, Rk = l < nm ? R[nR - 1 - l] : -1;
     const int ks = __popcll(__ballot(l < nm && Lk < Rk));  // monotone: lanes 0 .. ks-1
-    const int Lks = __builtin_amdgcn_readlane(Lk, ks < 63 ? ks : 63);
-    const int Rks = __builtin_amdgcn_readlane(Rk, ks > 0 ? ks - 1 : 0);
+    const int Lks = ks < nL ? L[ks] : 0;
+    const int Rks = ks > 0 ? R[nR - ks] : 0;
     const int cut = (ks > 0 && (ks >= nL || Lks >= Rks)) ? Rks : Lks;
     // pairs k < ks swap L[k] <-> R[k]
-    const int kL = __popcll(mL & ltm);
-    const int kR = l == 63 ? 0 : __popcll(mR >> (l + 1));
-    const int toR = __shfl(Rk, kL & 63), toL = __shfl(Lk, kR & 63);
     int src = l;
-    if (((mL >> l) & 1ull) && kL < ks) src = toR;
-    else if (((mR >> l) & 1ull) && kR < ks) src = toL;
+    if (isL && kL < ks) src = R[nR - 1 - kL];
+    else if (isR && kR < ks) src = L[kR];
+    wave_sync_lds();
     v = shfl64(v, src);
     if (l == cur || l == cut) dep = dd - 1;
     bnd |= 1ull << cut;
@@ -381,7 +387,7 @@ __device__ void exact_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp
       ++sp;
       rl = cut;
     }
-    if (!heaped && rl - rf > 1) small_sort(key, rf, rl - rf, rd, lt);
+    if (!heaped && rl - rf > 1) small_sort(key, Lp, Rp, rf, rl - rf, rd, lt);
     wave_sync_lds();
     if (sp == 0) break;
     --sp;
@@ -391,122 +397,282 @@ __device__ void exact_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp
 }
 
 // ---- the whole workgroup on one array ----------------------------------------------------------
-// block_introsort: the same std::sort by the workgroup's waves sharing one work queue.
-// libstdc++'s recursion only ever touches disjoint sub-ranges, each carrying its own depth limit,
-// so the order in which they are processed does not change the result. A wave takes a range from
-// the queue and runs libstdc++'s loop on it as exact_introsort does (partition in LDS, continue
-// with the left part), pushing every right part to the queue for any wave to take; a range of at
-// most 64 elements is finished in registers (small_sort), one above 64 with no depth left by
-// wave_heap_sort. The queue is an LDS stack under a lock held by one lane for a few instructions;
-// the waves stop when every element has been finished (a counter of the elements still open).
-// Every wave's work is its own: no workgroup barrier between partitions, and the sort costs about
-// what one wave doing it all would, spread over the waves. n <= 2048.
-constexpr int kBsQueue = 128;  // pending ranges: one per level of the paths being descended (<= 4 x 23)
+// block_introsort: the same std::sort by the workgroup. libstdc++'s recursion only ever touches
+// disjoint sub-ranges, each carrying its own depth limit, so the order in which they are processed
+// does not change the result. Ranges above kBsBig elements (the top of the recursion, and the long
+// chains of lopsided splits the voxel ids of a ring produce) are partitioned by the whole
+// workgroup, one at a time (block_partition: each thread classifies a contiguous chunk, one block
+// scan ranks the stops); every smaller range, or a large one whose depth limit is spent, goes to a
+// list that is dealt to the waves (largest first, each to the least loaded wave). Each wave then
+// finishes its ranges on its own as exact_introsort does: partition in LDS (stop lists at the
+// range's own offset of Lp / Rp), continue with the left part, the right part on the wave's private
+// stack; a range of at most 64 elements in registers (small_sort), one above 64 with no depth left
+// by wave_heap_sort. n <= 2048.
+constexpr int kBsBig = 512;
+constexpr int kBsList = 64;   // the dealt ranges: two per block partition at most, and few of those
+constexpr int kBsStack = 24;  // one entry per level of a path: <= depth limit (2 lg 2048 = 22) + 1
 struct BlockSortLds {
-  int q[kBsQueue];  // first | last << 12 | depth << 24
-  int top, lock, open;
+  int rng[kBsList];             // first | last << 12 | depth << 24
+  int owner[kBsList];           // the wave that finishes range k
+  int big[kBsStack];            // the block's pending large ranges
+  int stk[4][kBsStack];         // the waves' pending right parts
+  int scan[16];
+  int nr, ks;
+  uint64_t piv;
 };
 
-template <int kNT, class Lt>
-__device__ __forceinline__ void block_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp, BlockSortLds& s, Lt lt) {
-  static_assert(kNT % 64 == 0, "block_introsort: whole waves");
-  const int tid = threadIdx.x, l = lane_id();
+// One libstdc++ partition step of key[rf, rl) by one wave (rf + 1 < rl): the median of three to
+// rf, __unguarded_partition over (rf, rl) with the stop lists at Lp / Rp + rf; returns the cut.
+template <class Lt>
+__device__ __forceinline__ int wave_partition(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int rf, int rl, Lt lt) {
+  const int l = lane_id();
   const unsigned long long ltm = (1ull << l) - 1ull;
+  // __move_median_to_first(first, first+1, mid, last-1)
+  const int a = rf + 1, b = rf + (rl - rf) / 2, c = rl - 1;
+  const uint64_t va = key[a], vb = key[b], vc = key[c], vf = key[rf];
+  int m;
+  if (lt(va, vb)) m = lt(vb, vc) ? b : (lt(va, vc) ? c : a);
+  else m = lt(va, vc) ? a : (lt(vb, vc) ? c : b);
+  const uint64_t P = m == a ? va : (m == b ? vb : vc);
+  wave_sync_lds();
+  if (l == 0) { key[m] = vf; key[rf] = P; }
+  wave_sync_lds();
+  // __unguarded_partition: L stops (!(a < P), (rf, rl)) and R stops (!(P < a), [rf, rl)), both
+  // listed ascending (R[k], the k-th from the right, is Rp[nR - 1 - k]); two chunks of 64 per step
+  int nL = 0, nR = 0;
+  for (int c0 = rf; c0 < rl; c0 += 128) {
+    const int i0 = c0 + l, i1 = c0 + 64 + l;
+    const uint64_t v0 = i0 < rl ? key[i0] : 0ull, v1 = i1 < rl ? key[i1] : 0ull;
+    const bool fl0 = i0 < rl && i0 > rf && !lt(v0, P), fr0 = i0 < rl && !lt(P, v0);
+    const bool fl1 = i1 < rl && !lt(v1, P), fr1 = i1 < rl && !lt(P, v1);
+    const unsigned long long mL0 = __ballot(fl0), mR0 = __ballot(fr0), mL1 = __ballot(fl1), mR1 = __ballot(fr1);
+    const int nL1 = nL + __popcll(mL0), nR1 = nR + __popcll(mR0);
+    if (fl0) Lp[rf + nL + __popcll(mL0 & ltm)] = (uint16_t)i0;
+    if (fr0) Rp[rf + nR + __popcll(mR0 & ltm)] = (uint16_t)i0;
+    if (fl1) Lp[rf + nL1 + __popcll(mL1 & ltm)] = (uint16_t)i1;
+    if (fr1) Rp[rf + nR1 + __popcll(mR1 & ltm)] = (uint16_t)i1;
+    nL = nL1 + __popcll(mL1);
+    nR = nR1 + __popcll(mR1);
+  }
+  wave_sync_lds();
+  const uint16_t* L = Lp + rf;
+  const uint16_t* R = Rp + rf;
+  const int nm = nL < nR ? nL : nR;
+  int ks = nm;  // first k with !(L[k] < R[k]) (monotone)
+  for (int c0 = 0; c0 < nm; c0 += 128) {
+    const int k0 = c0 + l, k1 = c0 + 64 + l;
+    const int a0 = k0 < nm ? L[k0] : 0, b0 = k0 < nm ? R[nR - 1 - k0] : 0;
+    const int a1 = k1 < nm ? L[k1] : 0, b1 = k1 < nm ? R[nR - 1 - k1] : 0;
+    const unsigned long long m0 = __ballot(k0 < nm && !(a0 < b0)), m1 = __ballot(k1 < nm && !(a1 < b1));
+    if (m0) { ks = c0 + __ffsll((long long)m0) - 1; break; }
+    if (m1) { ks = c0 + 64 + __ffsll((long long)m1) - 1; break; }
+  }
+  const int cut = (ks > 0 && (ks >= nL || L[ks] >= R[nR - ks])) ? R[nR - ks] : L[ks];
+  for (int k0 = l; k0 < ks; k0 += 128) {
+    const int k1 = k0 + 64;
+    const bool two = k1 < ks;
+    const int x0 = L[k0], y0 = R[nR - 1 - k0];
+    const int x1 = two ? L[k1] : 0, y1 = two ? R[nR - 1 - k1] : 0;
+    const uint64_t p0 = key[x0], q0 = key[y0];
+    const uint64_t p1 = two ? key[x1] : 0ull, q1 = two ? key[y1] : 0ull;
+    key[x0] = q0;
+    key[y0] = p0;
+    if (two) { key[x1] = q1; key[y1] = p1; }
+  }
+  wave_sync_lds();
+  return cut;
+}
+
+// One libstdc++ partition step of key[rf, rl) by the whole workgroup (kNT threads); returns the
+// cut (uniform). Thread t classifies positions [rf + t * per, +per); one block scan of the packed
+// (L, R) stop counts gives every stop its rank; the first k with !(L[k] < R[k]) is an LDS min.
+template <int kNT, class Lt>
+__device__ __forceinline__ int block_partition(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int rf, int rl, BlockSortLds& s,
+                                               Lt lt) {
+  const int tid = threadIdx.x;
+  if (tid == 0) {  // __move_median_to_first(first, first+1, mid, last-1)
+    const int a = rf + 1, b = rf + (rl - rf) / 2, c = rl - 1;
+    const uint64_t va = key[a], vb = key[b], vc = key[c], vf = key[rf];
+    int m;
+    if (lt(va, vb)) m = lt(vb, vc) ? b : (lt(va, vc) ? c : a);
+    else m = lt(va, vc) ? a : (lt(vb, vc) ? c : b);
+    const uint64_t P = m == a ? va : (m == b ? vb : vc);
+    key[m] = vf;
+    key[rf] = P;
+    s.piv = P;
+    s.ks = 0x7fffffff;
+  }
+  __syncthreads();
+  const uint64_t P = s.piv;
+  const int per = (rl - rf + kNT - 1) / kNT;
+  const int c0 = min(rf + tid * per, rl), c1 = min(c0 + per, rl);
+  uint32_t mL = 0, mR = 0;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int i = c0 + u;
+    if (i >= c1) continue;
+    const uint64_t v = key[i];
+    if (i > rf && !lt(v, P)) mL |= 1u << u;
+    if (!lt(P, v)) mR |= 1u << u;
+  }
+  int tot;
+  const int ex = block_excl_scan((int)(__popc(mL) | (__popc(mR) << 16)), s.scan, &tot);
+  const int nL = tot & 0xffff, nR = tot >> 16;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const uint32_t below = (1u << u) - 1u;
+    if ((mL >> u) & 1u) Lp[rf + (ex & 0xffff) + __popc(mL & below)] = (uint16_t)(c0 + u);
+    if ((mR >> u) & 1u) Rp[rf + (ex >> 16) + __popc(mR & below)] = (uint16_t)(c0 + u);
+  }
+  __syncthreads();
+  const uint16_t* L = Lp + rf;
+  const uint16_t* R = Rp + rf;
+  const int nm = nL < nR ? nL : nR;
+  {  // ks = the first k with !(L[k] < R[k]) (monotone), nm if none
+    const int pk = (nm + kNT - 1) / kNT;
+    const int k0 = min(tid * pk, nm), k1 = min(k0 + pk, nm);
+    int kf = 0x7fffffff;
+    for (int k = k0; k < k1; ++k)
+      if (!(L[k] < R[nR - 1 - k])) { kf = k; break; }
+    if (kf != 0x7fffffff) atomicMin(&s.ks, kf);
+  }
+  __syncthreads();
+  const int ks = min(s.ks, nm);
+  {
+    const int pk = (ks + kNT - 1) / kNT;
+    const int k0 = min(tid * pk, ks), k1 = min(k0 + pk, ks);
+    for (int k = k0; k < k1; ++k) {
+      const int x = L[k], y = R[nR - 1 - k];
+      const uint64_t t = key[x];
+      key[x] = key[y];
+      key[y] = t;
+    }
+  }
+  const int cut = (ks > 0 && (ks >= nL || L[ks] >= R[nR - ks])) ? R[nR - ks] : L[ks];
+  __syncthreads();
+  return cut;
+}
+
+// prof (diagnostics only, k_debug_exact_sort): prof[0] = clocks of the block-wide part; per wave w,
+// prof[1 + 4 w + 0..3] = clocks in wave partitions, small_sort, wave_heap_sort, and idle at the end
+template <int kNT, class Lt>
+__device__ __forceinline__ void block_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp, BlockSortLds& s, Lt lt,
+                                                long long* prof = nullptr) {
+  static_assert(kNT == 256, "block_introsort: four waves");
+  const int tid = threadIdx.x, l = lane_id(), w = tid >> 6;
+  long long tc = prof ? clock64() : 0, tpw = 0, tsm = 0, thp = 0;
+  auto stamp = [&](long long& acc) {
+    if (prof) {
+      const long long t1 = clock64();
+      acc += t1 - tc;
+      tc = t1;
+    }
+  };
   __syncthreads();  // key[0, n) written by the caller
   if (n <= 1) return;
   const int lg = 31 - __clz(n);
   if (n <= 64) {  // std::sort's whole loop inside one small range
-    if (tid < 64) small_sort(key, 0, n, 2 * lg, lt);
+    if (w == 0) small_sort(key, Lp, Rp, 0, n, 2 * lg, lt);
     __syncthreads();
     return;
   }
-  if (tid == 0) {
-    s.q[0] = 0 | (n << 12) | ((2 * lg) << 24);
-    s.top = 1;
-    s.lock = 0;
-    s.open = n;
+  auto enc = [](int f, int e, int d) { return f | (e << 12) | (d << 24); };
+  // large ranges, block-wide, left part first (the right part waits on the block's stack); the
+  // counters are uniform copies every thread keeps (thread 0 writes the arrays). Near a full list
+  // the remaining ranges go to the list as they are (the waves finish any size).
+  {
+    int rf = 0, rl = n, rd = 2 * lg;
+    int nbig = 0, nr = 0;
+    while (true) {
+      while (rl - rf > kBsBig && rd > 0 && nr < kBsList - 2) {
+        rd--;
+        const int cut = block_partition<kNT>(key, Lp, Rp, rf, rl, s, lt);
+        if (rl - cut > kBsBig && rd > 0) {
+          if (tid == 0) s.big[nbig] = enc(cut, rl, rd);
+          ++nbig;
+        } else if (rl > cut) {
+          if (tid == 0) s.rng[nr] = enc(cut, rl, rd);
+          ++nr;
+        }
+        rl = cut;
+      }
+      if (rl > rf) {
+        if (tid == 0) s.rng[nr] = enc(rf, rl, rd);
+        ++nr;
+      }
+      if (nbig == 0) break;
+      __syncthreads();
+      --nbig;
+      const int it = s.big[nbig];
+      rf = it & 0xfff;
+      rl = (it >> 12) & 0xfff;
+      rd = (it >> 24) & 0x3f;
+    }
+    if (tid == 0) s.nr = nr;
   }
   __syncthreads();
-  auto acquire = [&]() {
-    while (atomicCAS(&s.lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  };
-  auto release = [&]() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    atomicExch(&s.lock, 0);
-  };
-  while (true) {
-    // take a range (lane 0 under the lock), or learn that every element is finished
-    int item = -1;
+  if (prof && tid == 0) prof[0] = clock64() - tc;
+  // deal the list: largest first, each to the least loaded wave (elements as the load)
+  if (w == 0) {
+    const int cnt = s.nr;
+    const int sz = l < cnt ? ((s.rng[l] >> 12) & 0xfff) - (s.rng[l] & 0xfff) : -1;
     if (l == 0) {
-      acquire();
-      if (s.top > 0) item = s.q[--s.top];
-      else if (atomicAdd(&s.open, 0) == 0) item = -2;
-      release();
+      int ld0 = 0, ld1 = 0, ld2 = 0, ld3 = 0;
+      unsigned long long taken = 0;
+      for (int r = 0; r < cnt; ++r) {
+        int best = 0, bs = -1;
+        for (int k = 0; k < cnt; ++k) {
+          const int z = __builtin_amdgcn_readlane(sz, k);
+          if (!((taken >> k) & 1ull) && z > bs) { bs = z; best = k; }
+        }
+        taken |= 1ull << best;
+        const int m01 = min(ld0, ld1), m23 = min(ld2, ld3);
+        const int wm = m01 <= m23 ? (ld0 <= ld1 ? 0 : 1) : (ld2 <= ld3 ? 2 : 3);
+        if (wm == 0) ld0 += bs; else if (wm == 1) ld1 += bs; else if (wm == 2) ld2 += bs; else ld3 += bs;
+        s.owner[best] = wm;
+      }
     }
-    item = __builtin_amdgcn_readfirstlane(item);
-    if (item == -2) break;
-    if (item == -1) {
-      __builtin_amdgcn_s_sleep(2);
-      continue;
-    }
-    int rf = item & 0xfff, rl = (item >> 12) & 0xfff, rd = (item >> 24) & 0x3f;
-    while (rl - rf > 64 && rd > 0) {
-      rd--;
-      // __move_median_to_first(first, first+1, mid, last-1)
-      const int a = rf + 1, b = rf + (rl - rf) / 2, c = rl - 1;
-      const uint64_t va = key[a], vb = key[b], vc = key[c], vf = key[rf];
-      int m;
-      if (lt(va, vb)) m = lt(vb, vc) ? b : (lt(va, vc) ? c : a);
-      else m = lt(va, vc) ? a : (lt(vb, vc) ? c : b);
-      const uint64_t P = m == a ? va : (m == b ? vb : vc);
-      wave_sync_lds();
-      if (l == 0) { key[m] = vf; key[rf] = P; }
-      wave_sync_lds();
-      // __unguarded_partition: L stops (!(a < P), (rf, rl)) and R stops (!(P < a), [rf, rl)), both
-      // listed ascending (R[k], the k-th from the right, is Rp[nR - 1 - k])
-      int nL = 0, nR = 0;
-      for (int c0 = rf; c0 < rl; c0 += 64) {
-        const int i = c0 + l;
-        const uint64_t v = i < rl ? key[i] : 0ull;
-        const bool fl = i < rl && i > rf && !lt(v, P);
-        const bool fr = i < rl && !lt(P, v);
-        const unsigned long long mL = __ballot(fl), mR = __ballot(fr);
-        if (fl) Lp[rf + nL + __popcll(mL & ltm)] = (uint16_t)i;
-        if (fr) Rp[rf + nR + __popcll(mR & ltm)] = (uint16_t)i;
-        nL += __popcll(mL);
-        nR += __popcll(mR);
-      }
-      wave_sync_lds();
-      const uint16_t* L = Lp + rf;
-      const uint16_t* R = Rp + rf;
-      const int nm = nL < nR ? nL : nR;
-      int ks = nm;  // first k with !(L[k] < R[k]) (monotone)
-      for (int c0 = 0; c0 < nm; c0 += 64) {
-        const int k = c0 + l;
-        const unsigned long long mk = __ballot(k < nm && !(L[k] < R[nR - 1 - k]));
-        if (mk) { ks = c0 + __ffsll((long long)mk) - 1; break; }
-      }
-      const int cut = (ks > 0 && (ks >= nL || L[ks] >= R[nR - ks])) ? R[nR - ks] : L[ks];
-      for (int k = l; k < ks; k += 64) {
-        const int x = L[k], y = R[nR - 1 - k];
-        const uint64_t t = key[x]; key[x] = key[y]; key[y] = t;
-      }
-      wave_sync_lds();
-      // the right part goes to the queue (any wave may take it), the left part continues here
-      if (l == 0) {
-        acquire();
-        s.q[s.top++] = cut | (rl << 12) | (rd << 24);
-        release();
-      }
-      rl = cut;
-    }
-    if (rl - rf > 64) wave_heap_sort(key, rf, rl, lt);  // depth limit spent: __partial_sort
-    else if (rl - rf > 1) small_sort(key, rf, rl - rf, rd, lt);
-    wave_sync_lds();
-    if (l == 0) atomicSub(&s.open, rl - rf);
   }
   __syncthreads();
+  // every wave finishes its ranges alone
+  const int nr = s.nr;
+  int* stk = s.stk[w];
+  if (prof) tc = clock64();
+  for (int k = 0; k < nr; ++k) {
+    if (s.owner[k] != w) continue;
+    const int it = s.rng[k];
+    int rf = it & 0xfff, rl = (it >> 12) & 0xfff, rd = (it >> 24) & 0x3f;
+    int sp = 0;
+    while (true) {
+      while (rl - rf > 64 && rd > 0) {
+        rd--;
+        const int cut = wave_partition(key, Lp, Rp, rf, rl, lt);
+        if (l == 0) stk[sp] = enc(cut, rl, rd);
+        ++sp;
+        rl = cut;
+      }
+      stamp(tpw);
+      if (rl - rf > 64) {
+        wave_heap_sort(key, rf, rl, lt);  // depth limit spent: __partial_sort
+        stamp(thp);
+      } else if (rl - rf > 1) {
+        small_sort(key, Lp, Rp, rf, rl - rf, rd, lt);
+        stamp(tsm);
+      }
+      wave_sync_lds();
+      if (sp == 0) break;
+      --sp;
+      const int nx = stk[sp];
+      rf = nx & 0xfff;
+      rl = (nx >> 12) & 0xfff;
+      rd = (nx >> 24) & 0x3f;
+    }
+  }
+  long long tend = prof ? clock64() : 0;
+  __syncthreads();
+  if (prof && l == 0) {
+    prof[1 + 4 * w] = tpw; prof[2 + 4 * w] = tsm; prof[3 + 4 * w] = thp; prof[4 + 4 * w] = clock64() - tend;
+  }
 }
 
 }  // namespace llsr

@@ -26,12 +26,13 @@ g.restype, g.argtypes = C.c_int32, [C.c_void_p, C.c_int32, C.c_void_p]
 
 
 def phases(a):
-    """core clocks (from the start) at the end of the levels, the listing and the small ranges, and
-    the number of levels"""
+    """core clocks of one sort"""
     a = np.ascontiguousarray(a, np.float32)
-    c = np.zeros(4, np.int64)
+    c = np.zeros(21, np.int64)
     assert g(a.ctypes.data, len(a), c.ctypes.data) == 0
-    return [int(x) for x in c]
+    w = c[2:18].reshape(4, 4)
+    return {"total": int(c[0]), "block": int(c[1]), "wave_partition": w[:, 0].tolist(), "small": w[:, 1].tolist(),
+            "heap": w[:, 2].tolist(), "idle_end": w[:, 3].tolist()}
 
 
 def t(a):
