@@ -678,7 +678,8 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
   __shared__ float matP[9];
   __shared__ float sums[12];
   __shared__ int isDeg, stop, n_corr[2], iters[2];
-  __shared__ float4 lrows[kLdsRows];
+  __shared__ float4 lrows_raw[kLdsRows];  // the LDS rows as four arrays (J0, J1, J2, b): phase B
+  float* const lrow4 = reinterpret_cast<float*>(lrows_raw);  // reads 4 consecutive rows of a column at once
   __shared__ uint8_t lvalid[kLdsRows];
   __shared__ uint16_t lvix[kLdsRows];  // phase B: the rows holding a correspondence, in order
   __shared__ float4 lcl[kLdsCorner];
@@ -731,7 +732,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
       const float4* qry = surf ? a.flat + f0 : a.sharp + ms0;
       const int Q = surf ? F : Ms;
       // the rows of this phase: LDS when they fit (phase B re-reads them serially every iteration)
-      float4* rows = Q <= kLdsRows ? lrows : grows;
+      float4* rows = grows;  // (the HBM rows when the phase's rows do not fit LDS)
       uint8_t* vf = Q <= kLdsRows ? lvalid : gvalid;  // row q holds a correspondence (laserCloudOri order)
       if (tid == 0)
         for (int k = 0; k < 9; ++k) matP[k] = (k % 4 == 0) ? 1.0f : 0.0f;
@@ -933,7 +934,13 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
               valid = true;
             }
           }
-          if (Q <= kLdsRows) { lrows[q] = row; lvalid[q] = valid ? 1 : 0; }
+          if (Q <= kLdsRows) {
+            lrow4[q] = row.x;
+            lrow4[kLdsRows + q] = row.y;
+            lrow4[2 * kLdsRows + q] = row.z;
+            lrow4[3 * kLdsRows + q] = row.w;
+            lvalid[q] = valid ? 1 : 0;
+          }
           else { grows[q] = row; gvalid[q] = valid ? 1 : 0; }
           nval += valid ? 1 : 0;
         }
@@ -971,16 +978,23 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
 #pragma unroll
           for (int u = 0; u < kMv; ++u) {
             const int i = tid + u * kThreads;
-            if (i < N) mv[u] = lrows[lvix[i]];
+            if (i < N) {
+              const int r = lvix[i];
+              mv[u] = make_float4(lrow4[r], lrow4[kLdsRows + r], lrow4[2 * kLdsRows + r], lrow4[3 * kLdsRows + r]);
+            }
           }
           __syncthreads();
 #pragma unroll
           for (int u = 0; u < kMv; ++u) {
             const int i = tid + u * kThreads;
-            if (i < N) lrows[i] = mv[u];
+            if (i < N) {
+              lrow4[i] = mv[u].x;
+              lrow4[kLdsRows + i] = mv[u].y;
+              lrow4[2 * kLdsRows + i] = mv[u].z;
+              lrow4[3 * kLdsRows + i] = mv[u].w;
+            }
           }
           __syncthreads();
-          const float* rf = reinterpret_cast<const float*>(lrows);
           const bool lazyAll = N + 6 < 20;
           const int kc = lazyAll ? N : llsr_eigen::gemm_kc(N, 3, 3);
           const int nblk = lazyAll || N == 0 ? 1 : (N + kc - 1) / kc;
@@ -992,31 +1006,33 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
             // is read below whatever nblk is; the GEMM-blocked lanes only when the blocks fit
             const bool act = lazy ? blk == 0 : (blk < nblk && 12 * nblk <= 64);
             const int ra = e < 9 ? e % 3 : e - 9, rb = e < 9 ? e / 3 : 3;
+            const float* ca = lrow4 + ra * kLdsRows;  // the two columns this lane multiplies
+            const float* cb = lrow4 + rb * kLdsRows;
             float c = 0.0f;
             if (act) {
               const int b0 = lazy ? 0 : blk * kc, b1 = lazy ? N : min(N, b0 + kc);
               int i = b0;
-              if (lazy && N > 0) { c = rf[ra] * rf[rb]; i = 1; }  // the coefficient product
-              // software-pipelined: the next 8 rows' LDS loads are in flight while this batch's
-              // products are added in order (the chain of adds is the only serial part)
+              if (lazy && N > 0) { c = ca[0] * cb[0]; i = 1; }  // the coefficient product
+              for (; i < b1 && (i & 7); ++i) c = c + ca[i] * cb[i];
+              // 8 rows per step, each column read as two 16-byte loads; the next step's loads are
+              // in flight while this step's products are added in order (the only serial part)
               if (i + 8 <= b1) {
-                float xa[8], xb[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) { xa[u] = rf[4 * (i + u) + ra]; xb[u] = rf[4 * (i + u) + rb]; }
+                float4 xa0 = *reinterpret_cast<const float4*>(ca + i), xa1 = *reinterpret_cast<const float4*>(ca + i + 4);
+                float4 xb0 = *reinterpret_cast<const float4*>(cb + i), xb1 = *reinterpret_cast<const float4*>(cb + i + 4);
                 for (; i + 16 <= b1; i += 8) {
-                  float ya[8], yb[8];
-#pragma unroll
-                  for (int u = 0; u < 8; ++u) { ya[u] = rf[4 * (i + 8 + u) + ra]; yb[u] = rf[4 * (i + 8 + u) + rb]; }
-#pragma unroll
-                  for (int u = 0; u < 8; ++u) c = c + xa[u] * xb[u];
-#pragma unroll
-                  for (int u = 0; u < 8; ++u) { xa[u] = ya[u]; xb[u] = yb[u]; }
+                  const float4 ya0 = *reinterpret_cast<const float4*>(ca + i + 8);
+                  const float4 ya1 = *reinterpret_cast<const float4*>(ca + i + 12);
+                  const float4 yb0 = *reinterpret_cast<const float4*>(cb + i + 8);
+                  const float4 yb1 = *reinterpret_cast<const float4*>(cb + i + 12);
+                  c = c + xa0.x * xb0.x; c = c + xa0.y * xb0.y; c = c + xa0.z * xb0.z; c = c + xa0.w * xb0.w;
+                  c = c + xa1.x * xb1.x; c = c + xa1.y * xb1.y; c = c + xa1.z * xb1.z; c = c + xa1.w * xb1.w;
+                  xa0 = ya0; xa1 = ya1; xb0 = yb0; xb1 = yb1;
                 }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) c = c + xa[u] * xb[u];
+                c = c + xa0.x * xb0.x; c = c + xa0.y * xb0.y; c = c + xa0.z * xb0.z; c = c + xa0.w * xb0.w;
+                c = c + xa1.x * xb1.x; c = c + xa1.y * xb1.y; c = c + xa1.z * xb1.z; c = c + xa1.w * xb1.w;
                 i += 8;
               }
-              for (; i < b1; ++i) c = c + rf[4 * i + ra] * rf[4 * i + rb];
+              for (; i < b1; ++i) c = c + ca[i] * cb[i];
               if (!lazy) bpart[blk][e] = c;
             }
             wave_sync_lds();
@@ -1031,9 +1047,9 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
                 float tot = 0.0f;
                 for (int b0 = 0; b0 < N; b0 += kc) {
                   const int b1 = min(N, b0 + kc);
-                  float cb = 0.0f;
-                  for (int i = b0; i < b1; ++i) cb = cb + rf[4 * i + ra] * rf[4 * i + rb];
-                  tot = tot + 1.0f * cb;
+                  float cs = 0.0f;
+                  for (int i = b0; i < b1; ++i) cs = cs + ca[i] * cb[i];
+                  tot = tot + 1.0f * cs;
                 }
                 sums[tid] = tot;
               }
