@@ -155,30 +155,37 @@ __device__ void reg_heap_sort(uint64_t& v, int f, int e, Lt lt) {
     reg_heap_adjust(v, f, 0, last - f, val, lt);
   }
 }
-// key[f, f + n), n <= 64, remaining depth limit d: finished exactly as std::sort would. Lp[f, f + n)
-// and Rp[f, f + n) are scratch: each partition lists its L stops (ascending) and R stops
-// (ascending; the k-th from the right is R[nR - 1 - k]) there as lane numbers, so the k-th pair,
-// ks and the cut are plain LDS reads.
+// key[f, f + n), n <= 64, holds one or more independent ranges (the set bits of `bnd`: their
+// starts, bit 0 always set), each with its remaining depth limit in `dep` of its start lane; every
+// range is finished exactly as std::sort would (libstdc++'s loop below 64 elements, then the final
+// insertion sort of its leaves). The ranges' partitions run side by side: each lane works on the
+// range that holds it (a segment of lanes), one partition step of every open segment per pass.
+// Lp[f, f + n) and Rp[f, f + n) are scratch: each step lists a segment's L stops and R stops
+// (ascending) at the segment's own offset as lane numbers, so the k-th pair, ks and the cut are LDS
+// reads. A segment of at most 16 elements is a leaf; one above 16 whose depth limit is spent is
+// heap-sorted in registers (rare), one segment at a time.
 template <class Lt>
-__device__ void small_sort(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int f, int n, int d, Lt lt) {
+__device__ void seg_small_sort(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int f, int n, unsigned long long bnd,
+                               int dep, Lt lt) {
   const int l = lane_id();
   const unsigned long long ltm = (1ull << l) - 1ull;
   const unsigned long long lem = l == 63 ? ~0ull : (2ull << l) - 1ull;  // bits <= l
   uint64_t v = l < n ? key[f + l] : 0ull;
-  int dep = d;                  // depth limit of the range starting at this lane
-  unsigned long long bnd = 1ull, leafm = 0ull, heapm = 0ull;
-  int cur = 0;
-  uint16_t* L = Lp + f;
-  uint16_t* R = Rp + f;
-  while (cur < n) {
-    const unsigned long long above = cur == 63 ? 0ull : bnd & ~((2ull << cur) - 1ull);
-    const int e = above ? __ffsll((long long)above) - 1 : n;
-    const int dd = __builtin_amdgcn_readlane(dep, cur);
-    if (e - cur <= 16) { leafm |= 1ull << cur; cur = e; continue; }
-    if (dd == 0) { reg_heap_sort(v, cur, e, lt); leafm |= 1ull << cur; heapm |= 1ull << cur; cur = e; continue; }
-    // __move_median_to_first(first, first + 1, mid, last - 1)
-    const int a = cur + 1, b = cur + (e - cur) / 2, c = e - 1;
-    const uint64_t va = rdlane64(v, a), vb = rdlane64(v, b), vc = rdlane64(v, c);
+  auto seg_of = [&](int& s, int& e) {  // the segment [s, e) holding this lane
+    s = 63 - __clzll((long long)(bnd & lem));
+    const unsigned long long up = bnd & ~lem;
+    e = up ? __ffsll((long long)up) - 1 : n;
+  };
+  while (true) {
+    int s, e;
+    seg_of(s, e);
+    const int dd = __shfl(dep, s);
+    const bool work = l < n && e - s > 16 && dd > 0;
+    if (!__ballot(work)) break;
+    const unsigned long long segm = (e >= 64 ? ~0ull : ((1ull << e) - 1ull)) & ~((1ull << s) - 1ull);
+    // __move_median_to_first(first, first + 1, mid, last - 1) of this lane's segment
+    const int a = s + 1, b = s + (e - s) / 2, c = e - 1;
+    const uint64_t va = shfl64(v, a & 63), vb = shfl64(v, b & 63), vc = shfl64(v, c & 63), v0 = shfl64(v, s);
     int mi;
     uint64_t vm;
     if (lt(va, vb)) {
@@ -188,22 +195,27 @@ __device__ void small_sort(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int f, int
     } else if (lt(va, vc)) { mi = a; vm = va; }
     else if (lt(vb, vc)) { mi = c; vm = vc; }
     else { mi = b; vm = vb; }
-    const uint64_t v0 = rdlane64(v, cur);
-    if (l == cur) v = vm;
-    else if (l == mi) v = v0;
+    if (work) {
+      if (l == s) v = vm;
+      else if (l == mi) v = v0;
+    }
     const uint64_t P = vm;
-    // __unguarded_partition: stop lists L ((cur, e)) and R ([cur, e)), ascending, in LDS
-    const bool isL = l > cur && l < e && !lt(v, P), isR = l >= cur && l < e && !lt(P, v);
+    // __unguarded_partition: stop lists L ((s, e)) and R ([s, e)), ascending, in LDS
+    const bool isL = work && l > s && !lt(v, P), isR = work && !lt(P, v);
     const unsigned long long mL = __ballot(isL), mR = __ballot(isR);
-    const int nL = __popcll(mL), nR = __popcll(mR), nm = nL < nR ? nL : nR;
-    const int kL = __popcll(mL & ltm), kRa = __popcll(mR & ltm), kR = nR - 1 - kRa;  // kR: rank from the right
+    const int nL = __popcll(mL & segm), nR = __popcll(mR & segm), nm = nL < nR ? nL : nR;
+    const int kL = __popcll(mL & segm & ltm), kRa = __popcll(mR & segm & ltm), kR = nR - 1 - kRa;
+    uint16_t* L = Lp + f + s;
+    uint16_t* R = Rp + f + s;
     if (isL) L[kL] = (uint16_t)l;
     if (isR) R[kRa] = (uint16_t)l;
     wave_sync_lds();
-    const int Lk = l < nm ? L[l] : 64, Rk = l < nm ? R[nR - 1 - l] : -1;
-    const int ks = __popcll(__ballot(l < nm && Lk < Rk));  // monotone: lanes 0 .. ks-1
-    const int Lks = ks < nL ? L[ks] : 0;
-    const int Rks = ks > 0 ? R[nR - ks] : 0;
+    const int k = l - s;
+    const bool kin = work && k < nm;
+    const int Lk = kin ? L[k] : 64, Rk = kin ? R[nR - 1 - k] : -1;
+    const int ks = __popcll(__ballot(kin && Lk < Rk) & segm);  // monotone: the segment's first ks
+    const int Lks = work && ks < nL ? L[ks] : 0;
+    const int Rks = work && ks > 0 ? R[nR - ks] : 0;
     const int cut = (ks > 0 && (ks >= nL || Lks >= Rks)) ? Rks : Lks;
     // pairs k < ks swap L[k] <-> R[k]
     int src = l;
@@ -211,14 +223,30 @@ __device__ void small_sort(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int f, int
     else if (isR && kR < ks) src = L[kR];
     wave_sync_lds();
     v = shfl64(v, src);
-    if (l == cur || l == cut) dep = dd - 1;
-    bnd |= 1ull << cut;
+    // both parts one level deeper; the cut starts the right part (none when cut == e)
+    bnd |= __ballot(work && l == cut);
+    if (work && (l == s || l == cut)) dep = dd - 1;
   }
-  // each leaf's insertion sort = its stable sort (<= 16 elements; a heap-sorted leaf is sorted
+  // segments above 16 with no depth left: libstdc++'s heap sort, in registers
+  unsigned long long heapm = 0ull;
+  {
+    int s, e;
+    seg_of(s, e);
+    const int dd = __shfl(dep, s);
+    unsigned long long hs = __ballot(l < n && l == s && e - s > 16 && dd == 0);
+    heapm = hs;
+    while (hs) {
+      const int hs0 = __ffsll((long long)hs) - 1;
+      hs &= hs - 1ull;
+      const unsigned long long up = bnd & ~(hs0 == 63 ? ~0ull : (2ull << hs0) - 1ull);
+      const int he = up ? __ffsll((long long)up) - 1 : n;
+      reg_heap_sort(v, hs0, he, lt);
+    }
+  }
+  // each leaf's insertion sort = its stable sort (<= 16 elements; a heap-sorted segment is sorted
   // already): the rank of every element among its leaf's, the leaf read back from LDS at once
-  const int s0 = 63 - __clzll((long long)(leafm & lem));
-  const unsigned long long up = leafm & ~lem;
-  const int t0 = up ? __ffsll((long long)up) - 1 : n;
+  int s0, t0;
+  seg_of(s0, t0);
   const int len = l < n ? t0 - s0 : 0;
   if (l < n) key[f + l] = v;
   wave_sync_lds();
@@ -240,6 +268,11 @@ __device__ void small_sort(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int f, int
   wave_sync_lds();
   if (l < n) key[f + s0 + rank] = v;
   wave_sync_lds();
+}
+// one range key[f, f + n), n <= 64, with depth limit d
+template <class Lt>
+__device__ __forceinline__ void small_sort(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int f, int n, int d, Lt lt) {
+  seg_small_sort(key, Lp, Rp, f, n, 1ull, d, lt);
 }
 
 // ---- libstdc++'s heap sort of a range above 64 elements, by one wave ---------------------------
@@ -634,10 +667,33 @@ __device__ __forceinline__ void block_introsort(uint64_t* key, int n, uint16_t* 
     }
   }
   __syncthreads();
-  // every wave finishes its ranges alone
+  // every wave finishes its ranges alone; consecutive ranges of at most 64 elements (left-first
+  // order emits them in position order) are collected in a window of <= 64 lanes and finished
+  // together by seg_small_sort
   const int nr = s.nr;
   int* stk = s.stk[w];
   if (prof) tc = clock64();
+  int wf = 0, wn = 0, wdep = 0;
+  unsigned long long wb = 0ull;
+  auto flush = [&]() {
+    if (wn > 1) seg_small_sort(key, Lp, Rp, wf, wn, wb, wdep, lt);
+    wn = 0;
+  };
+  auto emit = [&](int rf, int rl, int rd) {
+    const int len = rl - rf;
+    if (len <= 0) return;
+    if (wn > 0 && rf == wf + wn && wn + len <= 64) {
+      wb |= 1ull << wn;
+      if (l == wn) wdep = rd;
+      wn += len;
+    } else {
+      flush();
+      wf = rf;
+      wn = len;
+      wb = 1ull;
+      if (l == 0) wdep = rd;
+    }
+  };
   for (int k = 0; k < nr; ++k) {
     if (s.owner[k] != w) continue;
     const int it = s.rng[k];
@@ -655,8 +711,8 @@ __device__ __forceinline__ void block_introsort(uint64_t* key, int n, uint16_t* 
       if (rl - rf > 64) {
         wave_heap_sort(key, rf, rl, lt);  // depth limit spent: __partial_sort
         stamp(thp);
-      } else if (rl - rf > 1) {
-        small_sort(key, Lp, Rp, rf, rl - rf, rd, lt);
+      } else {
+        emit(rf, rl, rd);
         stamp(tsm);
       }
       wave_sync_lds();
@@ -668,6 +724,8 @@ __device__ __forceinline__ void block_introsort(uint64_t* key, int n, uint16_t* 
       rd = (nx >> 24) & 0x3f;
     }
   }
+  flush();
+  stamp(tsm);
   long long tend = prof ? clock64() : 0;
   __syncthreads();
   if (prof && l == 0) {
