@@ -192,7 +192,7 @@ int32_t llsr_fetch_scan(llsr_handle* h, int32_t b, llsr_scan_out* out);
 /* ImageProjection's visualization topics for slot b of the last batch (publishClouds,
  * imageProjection.cpp:933-967), built on the device from the slot's range image, kept points,
  * ground and label images, then copied to the caller's host buffers (each may be NULL: skipped):
- *   full_cloud / full_info_cloud  [H*W][4]  /full_cloud_projected, /full_cloud_info: per cell
+ *   full_cloud / full_info_cloud  [H*W][4]  /full_cloud (IP:54), /full_cloud_info: per cell
  *       x, y, z with intensity row + col / 1e4 resp. the range (IP:337-347); resetParameters'
  *       nanPoint (NaN x, y, z, intensity 0) where no point landed (IP:170-179)
  *   ground / nonground / unknownground_cloud  [<= H*W][4]  the full-cloud points of the cells

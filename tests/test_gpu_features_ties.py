@@ -43,7 +43,7 @@ def test_device_exact_sort_matches_std_sort(require_gpu):
     f.restype, f.argtypes = C.c_int32, [C.c_void_p, C.c_int32, C.c_void_p]
     rng = np.random.default_rng(11)
     cases = []
-    for n in (0, 1, 2, 16, 17, 33, 100, 511, 1024, 1800, 2048):
+    for n in (0, 1, 2, 16, 17, 33, 100, 129, 200, 300, 420, 511, 700, 1024, 1800, 2048):
         for levels in (1, 3, 20, 1000):
             cases.append((rng.integers(0, levels, n) * 0.25).astype(np.float32))
     k = 1024  # a median-of-3 killer: exhausts the depth limit -> libstdc++'s heap-sort fallback
