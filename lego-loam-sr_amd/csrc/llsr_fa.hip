@@ -724,8 +724,10 @@ __global__ __launch_bounds__(256, 5) void k_select_ring(DevCfg c, DevBufs d) {
     __syncthreads();
     if (c.dbg_phase <= 5) return;
     // Lp = rstart, Rp = the (dead) window bytes
-    block_introsort<256>(key, L, rstart, reinterpret_cast<uint16_t*>(win_raw), bsl, VoxLess{});
-    if (c.dbg_phase <= 6) return;
+    // (diagnostic phases 100 / 101: the sort's block-wide part / its partitions only)
+    block_introsort<256>(key, L, rstart, reinterpret_cast<uint16_t*>(win_raw), bsl, VoxLess{}, nullptr,
+                         c.dbg_phase >= 100 ? c.dbg_phase - 100 : 1 << 30);
+    if (c.dbg_phase <= 6 || (c.dbg_phase >= 100 && c.dbg_phase < 102)) return;
     // voxel heads in sorted order; sorted position t = u * 256 + tid sits in slot u of a lane, so a
     // wave's heads of one slot are consecutive voxels and their centroids are stored contiguously;
     // output positions come from per-(slot, wave) ballot counts scanned in (slot, wave) = sorted order.

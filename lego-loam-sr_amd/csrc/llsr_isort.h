@@ -176,10 +176,15 @@ __device__ void seg_small_sort(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int f,
     const unsigned long long up = bnd & ~lem;
     e = up ? __ffsll((long long)up) - 1 : n;
   };
+  {  // every lane holds its segment's depth limit (given on each range's first lane)
+    int s, e;
+    seg_of(s, e);
+    dep = __shfl(dep, s);
+  }
   while (true) {
     int s, e;
     seg_of(s, e);
-    const int dd = __shfl(dep, s);
+    const int dd = dep;
     const bool work = l < n && e - s > 16 && dd > 0;
     if (!__ballot(work)) break;
     const unsigned long long segm = (e >= 64 ? ~0ull : ((1ull << e) - 1ull)) & ~((1ull << s) - 1ull);
@@ -200,7 +205,8 @@ __device__ void seg_small_sort(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int f,
       else if (l == mi) v = v0;
     }
     const uint64_t P = vm;
-    // __unguarded_partition: stop lists L ((s, e)) and R ([s, e)), ascending, in LDS
+    // __unguarded_partition: stop lists L ((s, e)) and R ([s, e)), ascending, in LDS; one round of
+    // reads gives every lane its pair (k = l - s) and, for a stop, the partner it would swap with
     const bool isL = work && l > s && !lt(v, P), isR = work && !lt(P, v);
     const unsigned long long mL = __ballot(isL), mR = __ballot(isR);
     const int nL = __popcll(mL & segm), nR = __popcll(mR & segm), nm = nL < nR ? nL : nR;
@@ -213,27 +219,28 @@ __device__ void seg_small_sort(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int f,
     const int k = l - s;
     const bool kin = work && k < nm;
     const int Lk = kin ? L[k] : 64, Rk = kin ? R[nR - 1 - k] : -1;
-    const int ks = __popcll(__ballot(kin && Lk < Rk) & segm);  // monotone: the segment's first ks
-    const int Lks = work && ks < nL ? L[ks] : 0;
-    const int Rks = work && ks > 0 ? R[nR - ks] : 0;
-    const int cut = (ks > 0 && (ks >= nL || Lks >= Rks)) ? Rks : Lks;
-    // pairs k < ks swap L[k] <-> R[k]
-    int src = l;
-    if (isL && kL < ks) src = R[nR - 1 - kL];
-    else if (isR && kR < ks) src = L[kR];
+    const int pl = isL && kL < nm ? R[nR - 1 - kL] : l;  // L[kL]'s pair R_kL
+    const int pr = isR && kR < nm ? L[kR] : l;           // R_kR's pair L[kR]
     wave_sync_lds();
+    const int ks = __popcll(__ballot(kin && Lk < Rk) & segm);  // monotone: the segment's first ks
+    // L[ks] and R_{ks-1} (the k-th R stop from the right) are the lanes holding those ranks
+    const unsigned long long bL = __ballot(isL && kL == ks) & segm, bR = __ballot(isR && kR == ks - 1) & segm;
+    const int Lks = bL ? __ffsll((long long)bL) - 1 : 0;
+    const int Rks = bR ? __ffsll((long long)bR) - 1 : 0;
+    const int cut = (ks > 0 && (ks >= nL || Lks >= Rks)) ? Rks : Lks;
+    // pairs k < ks swap L[k] <-> R_k
+    const int src = isL && kL < ks ? pl : (isR && kR < ks ? pr : l);
     v = shfl64(v, src);
     // both parts one level deeper; the cut starts the right part (none when cut == e)
     bnd |= __ballot(work && l == cut);
-    if (work && (l == s || l == cut)) dep = dd - 1;
+    if (work) dep = dd - 1;
   }
   // segments above 16 with no depth left: libstdc++'s heap sort, in registers
   unsigned long long heapm = 0ull;
   {
     int s, e;
     seg_of(s, e);
-    const int dd = __shfl(dep, s);
-    unsigned long long hs = __ballot(l < n && l == s && e - s > 16 && dd == 0);
+    unsigned long long hs = __ballot(l < n && l == s && e - s > 16 && dep == 0);
     heapm = hs;
     while (hs) {
       const int hs0 = __ffsll((long long)hs) - 1;
@@ -590,7 +597,7 @@ __device__ __forceinline__ int block_partition(uint64_t* key, uint16_t* Lp, uint
 // prof[1 + 4 w + 0..3] = clocks in wave partitions, small_sort, wave_heap_sort, and idle at the end
 template <int kNT, class Lt>
 __device__ __forceinline__ void block_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp, BlockSortLds& s, Lt lt,
-                                                long long* prof = nullptr) {
+                                                long long* prof = nullptr, int stop = 1 << 30) {
   static_assert(kNT == 256, "block_introsort: four waves");
   const int tid = threadIdx.x, l = lane_id(), w = tid >> 6;
   long long tc = prof ? clock64() : 0, tpw = 0, tsm = 0, thp = 0;
@@ -645,6 +652,7 @@ __device__ __forceinline__ void block_introsort(uint64_t* key, int n, uint16_t* 
   }
   __syncthreads();
   if (prof && tid == 0) prof[0] = clock64() - tc;
+  if (stop <= 0) return;  // diagnostics (phase timing): the block-wide part only
   // deal the list: largest first, each to the least loaded wave (elements as the load)
   if (w == 0) {
     const int cnt = s.nr;
@@ -676,7 +684,7 @@ __device__ __forceinline__ void block_introsort(uint64_t* key, int n, uint16_t* 
   int wf = 0, wn = 0, wdep = 0;
   unsigned long long wb = 0ull;
   auto flush = [&]() {
-    if (wn > 1) seg_small_sort(key, Lp, Rp, wf, wn, wb, wdep, lt);
+    if (wn > 1 && stop > 1) seg_small_sort(key, Lp, Rp, wf, wn, wb, wdep, lt);  // stop 1: partitions only
     wn = 0;
   };
   auto emit = [&](int rf, int rl, int rd) {
