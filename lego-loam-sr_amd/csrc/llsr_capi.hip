@@ -31,6 +31,7 @@ template <bool kLds> __global__ void k_label(DevCfg, DevBufs);
 __global__ void k_segment(DevCfg, const float4*, const int64_t*, DevBufs);
 __global__ void k_fa_points(DevCfg, DevBufs);
 __global__ void k_select_ring(DevCfg, DevBufs);
+__global__ void k_vox_pcl(DevCfg, DevBufs);
 __global__ void k_debug_exact_sort(const float*, int, int*, long long*);
 __global__ void k_fa_concat(DevCfg, DevBufs);
 __global__ void k_dbscan_adj(DevCfg, DevBufs);
@@ -52,8 +53,8 @@ using namespace llsr;
 namespace {
 const char* kKernelNames[] = {"init",          "k_project",    "k_gather_column", "k_ground_add",
                               "k_ground_elev_ransac", "k_label", "k_segment",      "k_fa_points",
-                              "k_select_ring", "k_fa_concat", "k_dbscan_adj", "k_dbscan_merge"};
-constexpr int kNumKernels = 12;
+                              "k_select_ring", "k_vox_pcl", "k_fa_concat", "k_dbscan_adj", "k_dbscan_merge"};
+constexpr int kNumKernels = 13;
 }  // namespace
 
 struct llsr_handle {
@@ -546,6 +547,8 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   mark();
   k_select_ring<<<dim3(c.H, B), 256, 0, s>>>(c, h->d);
   mark();
+  if (c.exact_vg) k_vox_pcl<<<dim3(c.H, B), 256, 0, s>>>(c, h->d);  // the PCL-order VoxelGrid
+  mark();
   k_fa_concat<<<B, 256, 0, s>>>(c, h->d);
   mark();
   k_dbscan_adj<<<dim3(32, B), 256, 0, s>>>(c, h->d);
@@ -668,6 +671,20 @@ extern "C" float llsr_debug_phase_ms(llsr_handle* h, int32_t k, int32_t phase, i
   const int B = h->last_B;
   hipEvent_t e0 = h->ev[0][0], e1 = h->ev[0][1];
   if (sync_last(h) != LLSR_OK) return -1.f;
+  if (k == 9) {  // k_vox_pcl needs the keys k_select_ring leaves: both re-run before each launch
+    float tot = 0.f;
+    for (int r = 0; r < reps; ++r) {
+      k_fa_points<<<B, 512, 0, s>>>(h->dc, h->d);
+      k_select_ring<<<dim3(c.H, B), 256, 0, s>>>(h->dc, h->d);
+      (void)hipEventRecord(e0, s);
+      k_vox_pcl<<<dim3(c.H, B), 256, 0, s>>>(c, h->d);
+      (void)hipEventRecord(e1, s);
+      float ms = 0.f;
+      if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) return -1.f;
+      tot += ms;
+    }
+    return tot / reps;
+  }
   if (k == 8) {
     // k_select_ring consumes the picked / label state k_fa_points leaves (and overwrites it):
     // k_fa_points restores it before every timed launch, so each phase sees the batch's real work
@@ -687,9 +704,9 @@ extern "C" float llsr_debug_phase_ms(llsr_handle* h, int32_t k, int32_t phase, i
   for (int r = 0; r < reps; ++r) {
     switch (k) {
       case 8: k_select_ring<<<dim3(c.H, B), 256, 0, s>>>(c, h->d); break;
-      case 9: k_fa_concat<<<B, 256, 0, s>>>(c, h->d); break;
-      case 10: k_dbscan_adj<<<dim3(32, B), 256, 0, s>>>(c, h->d); break;
-      case 11:
+      case 10: k_fa_concat<<<B, 256, 0, s>>>(c, h->d); break;
+      case 11: k_dbscan_adj<<<dim3(32, B), 256, 0, s>>>(c, h->d); break;
+      case 12:
         if (c.HW <= 32768) k_dbscan_merge<1024><<<B, 64, 0, s>>>(c, h->d);
         else k_dbscan_merge<2048><<<B, 64, 0, s>>>(c, h->d);
         break;

@@ -714,55 +714,20 @@ __global__ __launch_bounds__(256, 5) void k_select_ring(DevCfg c, DevBufs d) {
   int V;
   if (c.exact_vg) {
     // LLSR_VOXEL_ORDER_PCL (llsr_set_voxel_order): std::sort(index_vector) by voxel id alone (PCL
-    // 1.10 voxel_grid.hpp): equal ids keep the order libstdc++'s introsort leaves them in, and each
-    // centroid sums its points in that order.
+    // 1.10 voxel_grid.hpp) and the centroids summed in that order run in k_vox_pcl, a kernel of
+    // its own with a smaller LDS footprint (more rings per CU for the sort's dependent chains): the
+    // ring's (voxel id, candidate) keys and candidate positions go to the scratch slots of its
+    // positions (ccl_b / ccl_a, dead since k_label), and rc[2H + i] = -1 - L marks the ring pending
 #pragma unroll
     for (int u = 0; u < kLp; ++u) {
       const int t = tid + u * 256;
-      if (t < L) key[t] = ((uint64_t)vkr[u] << 32) | (uint32_t)t;
-    }
-    __syncthreads();
-    if (c.dbg_phase <= 5) return;
-    // Lp = rstart, Rp = the (dead) window bytes
-    // (diagnostic phases 100 / 101: the sort's block-wide part / its partitions only)
-    block_introsort<256>(key, L, rstart, reinterpret_cast<uint16_t*>(win_raw), bsl, VoxLess{}, nullptr,
-                         c.dbg_phase >= 100 ? c.dbg_phase - 100 : 1 << 30);
-    if (c.dbg_phase <= 6 || (c.dbg_phase >= 100 && c.dbg_phase < 102)) return;
-    // voxel heads in sorted order; sorted position t = u * 256 + tid sits in slot u of a lane, so a
-    // wave's heads of one slot are consecutive voxels and their centroids are stored contiguously;
-    // output positions come from per-(slot, wave) ballot counts scanned in (slot, wave) = sorted order.
-    unsigned long long mH[kLp];
-#pragma unroll
-    for (int u = 0; u < kLp; ++u) {
-      const int t = u * 256 + tid;
-      const bool head = t < L && (t == 0 || (key[t] >> 32) != (key[t - 1] >> 32));
-      mH[u] = __ballot(head);
-      if (ln == 0) scnt[u * 4 + wv] = (int)__popcll(mH[u]);
-    }
-    __syncthreads();
-    if (wv == 0) {  // exclusive scan of scnt[0 .. kLp*4) in place, total in scnt[kLp*4]
-      const int v = ln < kLp * 4 ? scnt[ln] : 0;
-      const int incl = wave_incl_scan_add(v);
-      if (ln < kLp * 4) scnt[ln] = incl - v;
-      if (ln == 63) scnt[kLp * 4] = incl;
-    }
-    __syncthreads();
-    V = scnt[kLp * 4];
-#pragma unroll
-    for (int u = 0; u < kLp; ++u) {
-      const int t = u * 256 + tid;
-      if (!((mH[u] >> ln) & 1ull)) continue;
-      const uint32_t vid = (uint32_t)(key[t] >> 32);
-      float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
-      int e = t;
-      for (; e < L && (uint32_t)(key[e] >> 32) == vid; ++e) {
-        const float4 p = lp[cpos[(uint32_t)key[e]]];
-        sx += p.x; sy += p.y; sz += p.z; si += p.w;
+      if (t < L) {
+        d.ccl_b[base + sp + t] = ((uint64_t)vkr[u] << 32) | (uint32_t)t;
+        d.ccl_a[base + sp + t] = cpos[t];
       }
-      const float nn = (float)(e - t);
-      const int vo = scnt[u * 4 + wv] + (int)__popcll(mH[u] & ltm);
-      out[vo] = make_float4(sx / nn, sy / nn, sz / nn, si / nn);
     }
+    if (tid == 0) rc[2 * H + i] = -1 - L;
+    return;
   } else {
     // LLSR_VOXEL_ORDER_INPUT (default): runs of equal voxel id in ring order -> one sort key per
     // run: (voxel id, run index), each voxel summed run by run in ring order. Position
@@ -843,6 +808,77 @@ __global__ __launch_bounds__(256, 5) void k_select_ring(DevCfg c, DevBufs d) {
       const int vo = scnt[u * 4 + wv] + (int)__popcll(mH[u] & ltm);
       out[vo] = make_float4(sx / nn, sy / nn, sz / nn, si / nn);
     }
+  }
+  if (tid == 0) rc[2 * H + i] = V;
+}
+
+// ---------------------------------------------------------------------------------------------
+// K8b the less-flat VoxelGrid in PCL order (LLSR_VOXEL_ORDER_PCL; FA:1268-1271, PCL 1.10
+// VoxelGrid::applyFilter): each pending ring's (voxel id << 32 | candidate) keys sorted by voxel id
+// exactly as libstdc++'s std::sort leaves them (block_introsort, llsr_isort.h), then one lane per
+// voxel sums its points in that order. Split from k_select_ring so the sort runs at 6 workgroups
+// per CU (25 KB LDS, <= 85 VGPRs) instead of 5: its chains of dependent LDS steps want rings in
+// flight. grid (H, B), block 256.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 6) void k_vox_pcl(DevCfg c, DevBufs d) {
+  __shared__ uint64_t key[kRingMax];
+  __shared__ uint16_t Lp[kRingMax], Rp[kRingMax];
+  __shared__ BlockSortLds bsl;
+  constexpr int kLp = kRingMax / 256;
+  __shared__ int scnt[kLp * 4 + 1];
+  const int i = blockIdx.x, b = blockIdx.y, H = c.H;
+  int* rc = d.ring_cnt + (size_t)b * 3 * H;
+  const int r = rc[2 * H + i];
+  if (r >= 0) return;  // no candidates, or written by k_select_ring (input order / oversized grid)
+  const int L = -1 - r;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int sp = d.start_ring[b * H + i];
+  const size_t base = (size_t)b * c.HW;
+  for (int t = tid; t < L; t += nt) key[t] = d.ccl_b[base + sp + t];
+  // barriers on entry and exit (diagnostic phases 100 / 101 / 102: the block-wide part, the
+  // partitions, the whole sort)
+  block_introsort<256>(key, L, Lp, Rp, bsl, VoxLess{}, nullptr, c.dbg_phase >= 100 ? c.dbg_phase - 100 : 1 << 30);
+  if (c.dbg_phase <= 102) return;
+  uint16_t* cpos = Lp;  // the sort's scratch is free again
+  for (int t = tid; t < L; t += nt) cpos[t] = (uint16_t)d.ccl_a[base + sp + t];
+  const float4* lp = d.loam + base + sp;
+  float4* out = d.lflat_tmp + base + sp;
+  const int wv = tid >> 6, ln = lane_id();
+  const unsigned long long ltm = (1ull << ln) - 1ull;
+  // voxel heads in sorted order; sorted position t = u * 256 + tid sits in slot u of a lane, so a
+  // wave's heads of one slot are consecutive voxels and their centroids are stored contiguously;
+  // output positions come from per-(slot, wave) ballot counts scanned in (slot, wave) = sorted order.
+  unsigned long long mH[kLp];
+#pragma unroll
+  for (int u = 0; u < kLp; ++u) {
+    const int t = u * 256 + tid;
+    const bool head = t < L && (t == 0 || (key[t] >> 32) != (key[t - 1] >> 32));
+    mH[u] = __ballot(head);
+    if (ln == 0) scnt[u * 4 + wv] = (int)__popcll(mH[u]);
+  }
+  __syncthreads();
+  if (wv == 0) {  // exclusive scan of scnt[0 .. kLp*4) in place, total in scnt[kLp*4]
+    const int v = ln < kLp * 4 ? scnt[ln] : 0;
+    const int incl = wave_incl_scan_add(v);
+    if (ln < kLp * 4) scnt[ln] = incl - v;
+    if (ln == 63) scnt[kLp * 4] = incl;
+  }
+  __syncthreads();
+  const int V = scnt[kLp * 4];
+#pragma unroll
+  for (int u = 0; u < kLp; ++u) {
+    const int t = u * 256 + tid;
+    if (!((mH[u] >> ln) & 1ull)) continue;
+    const uint32_t vid = (uint32_t)(key[t] >> 32);
+    float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
+    int e = t;
+    for (; e < L && (uint32_t)(key[e] >> 32) == vid; ++e) {
+      const float4 p = lp[cpos[(uint32_t)key[e]]];
+      sx += p.x; sy += p.y; sz += p.z; si += p.w;
+    }
+    const float nn = (float)(e - t);
+    const int vo = scnt[u * 4 + wv] + (int)__popcll(mH[u] & ltm);
+    out[vo] = make_float4(sx / nn, sy / nn, sz / nn, si / nn);
   }
   if (tid == 0) rc[2 * H + i] = V;
 }

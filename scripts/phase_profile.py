@@ -25,7 +25,7 @@ for _ in range(3):  # kernel_times() averages over the profiled batches (bench.p
     pipe.process_batch(d_pts.data_ptr(), d_off.data_ptr(), B)
 res = {"kernels": pipe.kernel_times()}
 names = {3: "k_ground_add", 4: "k_ground_elev_ransac", 5: "k_label", 6: "k_segment", 7: "k_fa_points",
-         8: "k_select_ring", 9: "k_fa_concat", 10: "k_dbscan_adj", 11: "k_dbscan_merge"}
+         8: "k_select_ring", 9: "k_vox_pcl", 10: "k_fa_concat", 11: "k_dbscan_adj", 12: "k_dbscan_merge"}
 names[1] = "k_project_fused"
 todo = []
 for x in os.environ.get("PHASES", "8:8").split(","):  # "k:n" = phases 0..n-1, "k:a:b" = a..b-1
