@@ -712,37 +712,20 @@ __global__ __launch_bounds__(256, 5) void k_select_ring(DevCfg c, DevBufs d) {
   const int wv = tid >> 6, ln = lane_id();
   const unsigned long long ltm = (1ull << ln) - 1ull;
   int V;
-  if (c.exact_vg) {
-    // LLSR_VOXEL_ORDER_PCL (llsr_set_voxel_order): std::sort(index_vector) by voxel id alone (PCL
-    // 1.10 voxel_grid.hpp) and the centroids summed in that order run in k_vox_pcl, a kernel of
-    // its own with a smaller LDS footprint (more rings per CU for the sort's dependent chains): the
-    // ring's (voxel id, candidate) keys and candidate positions go to the scratch slots of its
-    // positions (ccl_b / ccl_a, dead since k_label), and rc[2H + i] = -1 - L marks the ring pending
-#pragma unroll
-    for (int u = 0; u < kLp; ++u) {
-      const int t = tid + u * 256;
-      if (t < L) {
-        d.ccl_b[base + sp + t] = ((uint64_t)vkr[u] << 32) | (uint32_t)t;
-        d.ccl_a[base + sp + t] = cpos[t];
-      }
+  auto slot_scan = [&]() {  // exclusive scan of scnt[0 .. kLp*4) in place, total in scnt[kLp*4]
+    __syncthreads();
+    if (wv == 0) {
+      const int v = ln < kLp * 4 ? scnt[ln] : 0;
+      const int incl = wave_incl_scan_add(v);
+      if (ln < kLp * 4) scnt[ln] = incl - v;
+      if (ln == 63) scnt[kLp * 4] = incl;
     }
-    if (tid == 0) rc[2 * H + i] = -1 - L;
-    return;
-  } else {
-    // LLSR_VOXEL_ORDER_INPUT (default): runs of equal voxel id in ring order -> one sort key per
-    // run: (voxel id, run index), each voxel summed run by run in ring order. Position
-    // t = u * 256 + tid in slot u of a lane; run indices from per-(slot, wave) ballot counts scanned in
-    // (slot, wave) = ring order.
-    auto slot_scan = [&]() {  // exclusive scan of scnt[0 .. kLp*4) in place, total in scnt[kLp*4]
-      __syncthreads();
-      if (wv == 0) {
-        const int v = ln < kLp * 4 ? scnt[ln] : 0;
-        const int incl = wave_incl_scan_add(v);
-        if (ln < kLp * 4) scnt[ln] = incl - v;
-        if (ln == 63) scnt[kLp * 4] = incl;
-      }
-      __syncthreads();
-    };
+    __syncthreads();
+  };
+  // runs of equal voxel id in ring order -> one sort key per run, (voxel id, run index), sorted
+  // (block4_sort); run starts in rstart. Position t = u * 256 + tid in slot u of a lane; run
+  // indices from per-(slot, wave) ballot counts scanned in (slot, wave) = ring order.
+  auto sort_runs = [&]() {
     unsigned long long mR[kLp];
 #pragma unroll
     for (int u = 0; u < kLp; ++u) {
@@ -764,8 +747,49 @@ __global__ __launch_bounds__(256, 5) void k_select_ring(DevCfg c, DevBufs d) {
     const int R2 = max(pow2_ceil(R), 64);
     for (int t = R + tid; t < R2; t += nt) key[t] = ~0ull;
     __syncthreads();
-    if (c.dbg_phase <= 5) return;
     block4_sort<uint64_t>(key, R2);
+    return R;
+  };
+  if (c.exact_vg) {
+    // LLSR_VOXEL_ORDER_PCL (llsr_set_voxel_order): std::sort(index_vector) by voxel id alone (PCL
+    // 1.10 voxel_grid.hpp) and the centroids summed in that order run in k_vox_pcl, a kernel of
+    // its own with a small LDS footprint (more rings per CU for the sort's dependent chains). It
+    // sorts 32-bit keys (rank << 11 | candidate): each voxel id replaced by its dense rank among the
+    // ring's ids, which keeps the outcome of every comparison; the ranks come from the sorted voxel
+    // runs. The keys and the candidate positions go to the scratch slots of the ring's positions
+    // (ccl_a / ccl_b, dead since k_label), and rc[2H + i] = -1 - L marks the ring pending.
+    if (c.dbg_phase <= 5) return;
+    const int R = sort_runs();
+    uint16_t* rrank = reinterpret_cast<uint16_t*>(win_raw);  // run -> rank of its voxel id
+    const unsigned long long lem = ltm | (1ull << ln);
+    unsigned long long mH[kLp];
+#pragma unroll
+    for (int u = 0; u < kLp; ++u) {
+      const int t = u * 256 + tid;
+      mH[u] = __ballot(t < R && (t == 0 || (key[t] >> 32) != (key[t - 1] >> 32)));
+      if (ln == 0) scnt[u * 4 + wv] = (int)__popcll(mH[u]);
+    }
+    slot_scan();
+#pragma unroll
+    for (int u = 0; u < kLp; ++u) {
+      const int t = u * 256 + tid;
+      if (t < R) rrank[(uint32_t)key[t]] = (uint16_t)(scnt[u * 4 + wv] + (int)__popcll(mH[u] & lem) - 1);
+    }
+    __syncthreads();
+    uint32_t* gk = reinterpret_cast<uint32_t*>(d.ccl_a + base) + sp;
+    uint16_t* gc = reinterpret_cast<uint16_t*>(d.ccl_b + base) + sp;
+    for (int r = tid; r < R; r += nt) {
+      const uint32_t rk = (uint32_t)rrank[r] << 11;
+      const int qe = rstart[r + 1];
+      for (int q = rstart[r]; q < qe; ++q) gk[q] = rk | (uint32_t)q;
+    }
+    for (int t = tid; t < L; t += nt) gc[t] = cpos[t];
+    if (tid == 0) rc[2 * H + i] = -1 - L;
+    return;
+  } else {
+    // LLSR_VOXEL_ORDER_INPUT: each voxel summed run by run in ring order (sorted runs)
+    if (c.dbg_phase <= 5) return;
+    const int R = sort_runs();
     if (c.dbg_phase <= 6) return;
     // voxels = groups of sorted runs with equal id; sum members in (run start, position) order.
     // Sorted run t = u * 256 + tid sits in slot u of a lane, so a wave's voxel heads of one slot are
@@ -816,12 +840,12 @@ __global__ __launch_bounds__(256, 5) void k_select_ring(DevCfg c, DevBufs d) {
 // K8b the less-flat VoxelGrid in PCL order (LLSR_VOXEL_ORDER_PCL; FA:1268-1271, PCL 1.10
 // VoxelGrid::applyFilter): each pending ring's (voxel id << 32 | candidate) keys sorted by voxel id
 // exactly as libstdc++'s std::sort leaves them (block_introsort, llsr_isort.h), then one lane per
-// voxel sums its points in that order. Split from k_select_ring so the sort runs at 6 workgroups
-// per CU (25 KB LDS, <= 85 VGPRs) instead of 5: its chains of dependent LDS steps want rings in
-// flight. grid (H, B), block 256.
+// voxel sums its points in that order. Split from k_select_ring so the sort runs at 8 workgroups
+// per CU (32-bit keys: 17 KB LDS, <= 64 VGPRs) instead of 5: its chains of dependent LDS steps
+// want rings in flight. grid (H, B), block 256.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 6) void k_vox_pcl(DevCfg c, DevBufs d) {
-  __shared__ uint64_t key[kRingMax];
+__global__ __launch_bounds__(256, 8) void k_vox_pcl(DevCfg c, DevBufs d) {
+  __shared__ uint32_t key[kRingMax];
   __shared__ uint16_t Lp[kRingMax], Rp[kRingMax];
   __shared__ BlockSortLds bsl;
   constexpr int kLp = kRingMax / 256;
@@ -834,13 +858,15 @@ __global__ __launch_bounds__(256, 6) void k_vox_pcl(DevCfg c, DevBufs d) {
   const int tid = threadIdx.x, nt = blockDim.x;
   const int sp = d.start_ring[b * H + i];
   const size_t base = (size_t)b * c.HW;
-  for (int t = tid; t < L; t += nt) key[t] = d.ccl_b[base + sp + t];
+  const uint32_t* gk = reinterpret_cast<const uint32_t*>(d.ccl_a + base) + sp;
+  const uint16_t* gc = reinterpret_cast<const uint16_t*>(d.ccl_b + base) + sp;
+  for (int t = tid; t < L; t += nt) key[t] = gk[t];
   // barriers on entry and exit (diagnostic phases 100 / 101 / 102: the block-wide part, the
   // partitions, the whole sort)
-  block_introsort<256>(key, L, Lp, Rp, bsl, VoxLess{}, nullptr, c.dbg_phase >= 100 ? c.dbg_phase - 100 : 1 << 30);
+  block_introsort<256>(key, L, Lp, Rp, bsl, VoxLess32{}, nullptr, c.dbg_phase >= 100 ? c.dbg_phase - 100 : 1 << 30);
   if (c.dbg_phase <= 102) return;
   uint16_t* cpos = Lp;  // the sort's scratch is free again
-  for (int t = tid; t < L; t += nt) cpos[t] = (uint16_t)d.ccl_a[base + sp + t];
+  for (int t = tid; t < L; t += nt) cpos[t] = gc[t];
   const float4* lp = d.loam + base + sp;
   float4* out = d.lflat_tmp + base + sp;
   const int wv = tid >> 6, ln = lane_id();
@@ -852,7 +878,7 @@ __global__ __launch_bounds__(256, 6) void k_vox_pcl(DevCfg c, DevBufs d) {
 #pragma unroll
   for (int u = 0; u < kLp; ++u) {
     const int t = u * 256 + tid;
-    const bool head = t < L && (t == 0 || (key[t] >> 32) != (key[t - 1] >> 32));
+    const bool head = t < L && (t == 0 || (key[t] >> 11) != (key[t - 1] >> 11));
     mH[u] = __ballot(head);
     if (ln == 0) scnt[u * 4 + wv] = (int)__popcll(mH[u]);
   }
@@ -869,11 +895,11 @@ __global__ __launch_bounds__(256, 6) void k_vox_pcl(DevCfg c, DevBufs d) {
   for (int u = 0; u < kLp; ++u) {
     const int t = u * 256 + tid;
     if (!((mH[u] >> ln) & 1ull)) continue;
-    const uint32_t vid = (uint32_t)(key[t] >> 32);
+    const uint32_t vr = key[t] >> 11;
     float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
     int e = t;
-    for (; e < L && (uint32_t)(key[e] >> 32) == vid; ++e) {
-      const float4 p = lp[cpos[(uint32_t)key[e]]];
+    for (; e < L && (key[e] >> 11) == vr; ++e) {
+      const float4 p = lp[cpos[key[e] & 0x7ffu]];
       sx += p.x; sy += p.y; sz += p.z; si += p.w;
     }
     const float nn = (float)(e - t);

@@ -6,7 +6,8 @@
 //   * pcl::VoxelGrid's std::sort of (voxel id, point index) by voxel id (PCL 1.10 voxel_grid.hpp,
 //     every downSizeFilter of FA / MO): each centroid sums its voxel's points in that order
 //     (llsr_fa.hip's per-ring less-flat filter, llsr_map.hip's segmented filter).
-// Keys are uint64 (sort key << 32 | payload); the comparator sees the whole word.
+// Keys are uint64 (sort key << 32 | payload) or uint32 (VoxLess32: dense voxel rank << 11 | candidate);
+// the comparator reads the sort-key bits only.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -37,13 +38,17 @@ struct CurvLess {
 struct VoxLess {
   __device__ bool operator()(uint64_t a, uint64_t b) const { return (uint32_t)(a >> 32) < (uint32_t)(b >> 32); }
 };
+// 32-bit VoxelGrid keys (dense voxel rank << 11 | candidate): the rank bits only
+struct VoxLess32 {
+  __device__ bool operator()(uint32_t a, uint32_t b) const { return (a >> 11) < (b >> 11); }
+};
 __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
 // libstdc++ __adjust_heap (with __push_heap) on key[f, f+len), one lane
-template <class Lt>
-__device__ void heap_adjust(uint64_t* key, int f, int hole, int len, uint64_t val, Lt lt) {
+template <class K, class Lt>
+__device__ void heap_adjust(K* key, int f, int hole, int len, K val, Lt lt) {
   const int top = hole;
   int second = hole;
   while (second < (len - 1) / 2) {
@@ -66,8 +71,8 @@ __device__ void heap_adjust(uint64_t* key, int f, int hole, int len, uint64_t va
   key[f + hole] = val;
 }
 // __partial_sort(first, last, last) = __make_heap + __sort_heap, one lane
-template <class Lt>
-__device__ void heap_sort_range(uint64_t* key, int f, int l, Lt lt) {
+template <class K, class Lt>
+__device__ void heap_sort_range(K* key, int f, int l, Lt lt) {
   const int len = l - f;
   if (len >= 2)
     for (int parent = (len - 2) / 2;; --parent) {
@@ -76,7 +81,7 @@ __device__ void heap_sort_range(uint64_t* key, int f, int l, Lt lt) {
     }
   for (int last = l; last - f > 1;) {
     --last;
-    const uint64_t val = key[last];
+    const K val = key[last];
     key[last] = key[f];
     heap_adjust(key, f, 0, last - f, val, lt);
   }
@@ -88,16 +93,26 @@ constexpr int kSortStack = 64;
 // the range's leaves (an insertion sort with a strict comparator is a stable sort, so each leaf's
 // result is its stable sort, computed from ranks) all run on register values with ballots and
 // lane shuffles; only the load and the final store touch LDS.
-__device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
+__device__ __forceinline__ uint64_t rdlane_k(uint64_t v, int l) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
   return ((uint64_t)hi << 32) | lo;
 }
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+__device__ __forceinline__ uint32_t rdlane_k(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ uint64_t shfl_k(uint64_t v, int src) {
   const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src);
   const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
   return ((uint64_t)hi << 32) | lo;
 }
+__device__ __forceinline__ uint32_t shfl_k(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src); }
+// the word the comparators read (VoxLess / CurvLess: the high word of a 64-bit key; a 32-bit key
+// whole) and a key holding only that word
+__device__ __forceinline__ uint32_t cmp_word(uint64_t k) { return (uint32_t)(k >> 32); }
+__device__ __forceinline__ uint32_t cmp_word(uint32_t k) { return k; }
+__device__ __forceinline__ void from_cmp_word(uint32_t w, uint64_t& k) { k = (uint64_t)w << 32; }
+__device__ __forceinline__ void from_cmp_word(uint32_t w, uint32_t& k) { k = w; }
 // position of the k-th (0-based) set bit of m, from bit 0; k < popcount(m)
 __device__ __forceinline__ int select_bit(uint64_t m, int k) {
   int pos = 0;
@@ -111,46 +126,46 @@ __device__ __forceinline__ int select_bit(uint64_t m, int k) {
   return pos;
 }
 // libstdc++ heap sort of lanes [f, e) (all lanes execute; every index is wave-uniform)
-template <class Lt>
-__device__ void reg_heap_adjust(uint64_t& v, int f, int hole, int len, uint64_t val, Lt lt) {
+template <class K, class Lt>
+__device__ void reg_heap_adjust(K& v, int f, int hole, int len, K val, Lt lt) {
   const int l = lane_id();
   const int top = hole;
   int second = hole;
   while (second < (len - 1) / 2) {
     second = 2 * (second + 1);
-    if (lt(rdlane64(v, f + second), rdlane64(v, f + second - 1))) second--;
-    const uint64_t x = rdlane64(v, f + second);
+    if (lt(rdlane_k(v, f + second), rdlane_k(v, f + second - 1))) second--;
+    const K x = rdlane_k(v, f + second);
     if (l == f + hole) v = x;
     hole = second;
   }
   if ((len & 1) == 0 && second == (len - 2) / 2) {
     second = 2 * (second + 1);
-    const uint64_t x = rdlane64(v, f + second - 1);
+    const K x = rdlane_k(v, f + second - 1);
     if (l == f + hole) v = x;
     hole = second - 1;
   }
   int parent = (hole - 1) / 2;
-  while (hole > top && lt(rdlane64(v, f + parent), val)) {
-    const uint64_t x = rdlane64(v, f + parent);
+  while (hole > top && lt(rdlane_k(v, f + parent), val)) {
+    const K x = rdlane_k(v, f + parent);
     if (l == f + hole) v = x;
     hole = parent;
     parent = (hole - 1) / 2;
   }
   if (l == f + hole) v = val;
 }
-template <class Lt>
-__device__ void reg_heap_sort(uint64_t& v, int f, int e, Lt lt) {
+template <class K, class Lt>
+__device__ void reg_heap_sort(K& v, int f, int e, Lt lt) {
   const int l = lane_id();
   const int len = e - f;
   if (len >= 2)
     for (int parent = (len - 2) / 2;; --parent) {
-      reg_heap_adjust(v, f, parent, len, rdlane64(v, f + parent), lt);
+      reg_heap_adjust(v, f, parent, len, rdlane_k(v, f + parent), lt);
       if (parent == 0) break;
     }
   for (int last = e; last - f > 1;) {
     --last;
-    const uint64_t val = rdlane64(v, last);
-    const uint64_t top = rdlane64(v, f);
+    const K val = rdlane_k(v, last);
+    const K top = rdlane_k(v, f);
     if (l == last) v = top;
     reg_heap_adjust(v, f, 0, last - f, val, lt);
   }
@@ -164,13 +179,13 @@ __device__ void reg_heap_sort(uint64_t& v, int f, int e, Lt lt) {
 // (ascending) at the segment's own offset as lane numbers, so the k-th pair, ks and the cut are LDS
 // reads. A segment of at most 16 elements is a leaf; one above 16 whose depth limit is spent is
 // heap-sorted in registers (rare), one segment at a time.
-template <class Lt>
-__device__ void seg_small_sort(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int f, int n, unsigned long long bnd,
+template <class K, class Lt>
+__device__ void seg_small_sort(K* key, uint16_t* Lp, uint16_t* Rp, int f, int n, unsigned long long bnd,
                                int dep, Lt lt) {
   const int l = lane_id();
   const unsigned long long ltm = (1ull << l) - 1ull;
   const unsigned long long lem = l == 63 ? ~0ull : (2ull << l) - 1ull;  // bits <= l
-  uint64_t v = l < n ? key[f + l] : 0ull;
+  K v = l < n ? key[f + l] : K(0);
   auto seg_of = [&](int& s, int& e) {  // the segment [s, e) holding this lane
     s = 63 - __clzll((long long)(bnd & lem));
     const unsigned long long up = bnd & ~lem;
@@ -190,9 +205,9 @@ __device__ void seg_small_sort(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int f,
     const unsigned long long segm = (e >= 64 ? ~0ull : ((1ull << e) - 1ull)) & ~((1ull << s) - 1ull);
     // __move_median_to_first(first, first + 1, mid, last - 1) of this lane's segment
     const int a = s + 1, b = s + (e - s) / 2, c = e - 1;
-    const uint64_t va = shfl64(v, a & 63), vb = shfl64(v, b & 63), vc = shfl64(v, c & 63), v0 = shfl64(v, s);
+    const K va = shfl_k(v, a & 63), vb = shfl_k(v, b & 63), vc = shfl_k(v, c & 63), v0 = shfl_k(v, s);
     int mi;
-    uint64_t vm;
+    K vm;
     if (lt(va, vb)) {
       if (lt(vb, vc)) { mi = b; vm = vb; }
       else if (lt(va, vc)) { mi = c; vm = vc; }
@@ -204,7 +219,7 @@ __device__ void seg_small_sort(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int f,
       if (l == s) v = vm;
       else if (l == mi) v = v0;
     }
-    const uint64_t P = vm;
+    const K P = vm;
     // __unguarded_partition: stop lists L ((s, e)) and R ([s, e)), ascending, in LDS; one round of
     // reads gives every lane its pair (k = l - s) and, for a stop, the partner it would swap with
     const bool isL = work && l > s && !lt(v, P), isR = work && !lt(P, v);
@@ -230,7 +245,7 @@ __device__ void seg_small_sort(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int f,
     const int cut = (ks > 0 && (ks >= nL || Lks >= Rks)) ? Rks : Lks;
     // pairs k < ks swap L[k] <-> R_k
     const int src = isL && kL < ks ? pl : (isR && kR < ks ? pr : l);
-    v = shfl64(v, src);
+    v = shfl_k(v, src);
     // both parts one level deeper; the cut starts the right part (none when cut == e)
     bnd |= __ballot(work && l == cut);
     if (work) dep = dd - 1;
@@ -262,12 +277,13 @@ __device__ void seg_small_sort(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int f,
     rank = 0;
 #pragma unroll
     for (int h = 0; h < 16; h += 8) {
-      uint32_t w[8];  // the comparators read the high words only
+      uint32_t w[8];  // the comparators read one word of the key (cmp_word)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) w[q] = (uint32_t)(key[f + min(s0 + h + q, n - 1)] >> 32);
+      for (int q = 0; q < 8; ++q) w[q] = cmp_word(key[f + min(s0 + h + q, n - 1)]);
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const uint64_t wq = (uint64_t)w[q] << 32;
+        K wq;
+        from_cmp_word(w[q], wq);
         if (h + q < len && (lt(wq, v) || (!lt(v, wq) && s0 + h + q < l))) ++rank;
       }
     }
@@ -277,8 +293,8 @@ __device__ void seg_small_sort(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int f,
   wave_sync_lds();
 }
 // one range key[f, f + n), n <= 64, with depth limit d
-template <class Lt>
-__device__ __forceinline__ void small_sort(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int f, int n, int d, Lt lt) {
+template <class K, class Lt>
+__device__ __forceinline__ void small_sort(K* key, uint16_t* Lp, uint16_t* Rp, int f, int n, int d, Lt lt) {
   seg_small_sort(key, Lp, Rp, f, n, 1ull, d, lt);
 }
 
@@ -291,8 +307,8 @@ __device__ __forceinline__ void small_sort(uint64_t* key, uint16_t* Lp, uint16_t
 // choices are one ballot, the walk a few scalar steps per level); the values move up the path by
 // one place, and the popped value settles where __push_heap stops: above the deepest path
 // position whose (moved-up) parent is not less than it, which is one ballot over the path.
-template <class Lt>
-__device__ void wave_heap_sort(uint64_t* key, int f, int e, Lt lt) {
+template <class K, class Lt>
+__device__ void wave_heap_sort(K* key, int f, int e, Lt lt) {
   const int l = lane_id();
   const int len0 = e - f;
   if (len0 < 2) return;
@@ -306,21 +322,21 @@ __device__ void wave_heap_sort(uint64_t* key, int f, int e, Lt lt) {
   }
   for (int len = len0 - 1; len >= 1; --len) {
     // __pop_heap(first, first + len + 1, first + len): value = last, last = root
-    const uint64_t value = key[f + len];
-    const uint64_t root = key[f];
+    const K value = key[f + len];
+    const K root = key[f];
     const int lim = (len - 1) / 2;
     int hole = 0, L = 0;
     int pnode = 0, pnext = 0;  // lane t < L: path node p_t and the child p_{t+1} the hole moved to
-    uint64_t pchild = 0;       // lane t < L: the value of p_{t+1} before the pop
+    K pchild = 0;       // lane t < L: the value of p_{t+1} before the pop
     bool more = hole < lim;
     while (more) {
       // the subtree of 63 nodes below the hole: lane i = its BFS node i, at absolute index a
       const int lv = 31 - __clz(l + 1);
       const int a = ((hole + 1) << lv) - 1 + (l + 1 - (1 << lv));
       bool right = false;
-      uint64_t chosen = 0;
+      K chosen = 0;
       if (l < 63 && a < lim) {
-        const uint64_t cl = key[f + 2 * a + 1], cr = key[f + 2 * a + 2];
+        const K cl = key[f + 2 * a + 1], cr = key[f + 2 * a + 2];
         right = !lt(cr, cl);  // __adjust_heap: second = right child, then -- if right < left
         chosen = right ? cr : cl;
       }
@@ -330,7 +346,7 @@ __device__ void wave_heap_sort(uint64_t* key, int f, int e, Lt lt) {
         if (!(ai < lim)) break;
         const int ci = 2 * i + ((rm >> i) & 1ull ? 2 : 1);
         const int ca = 2 * ai + ((rm >> i) & 1ull ? 2 : 1);
-        const uint64_t cv = rdlane64(chosen, i);
+        const K cv = rdlane_k(chosen, i);
         if (l == L) { pnode = ai; pnext = ca; pchild = cv; }
         ++L;
         i = ci;
@@ -340,7 +356,7 @@ __device__ void wave_heap_sort(uint64_t* key, int f, int e, Lt lt) {
       more = hole < lim;  // 6 levels done with the hole still above the last parent: next subtree
     }
     if ((len & 1) == 0 && hole == (len - 2) / 2) {  // the last parent's only (left) child
-      const uint64_t cv = key[f + 2 * hole + 1];
+      const K cv = key[f + 2 * hole + 1];
       if (l == L) { pnode = hole; pnext = 2 * hole + 1; pchild = cv; }
       ++L;
       hole = 2 * hole + 1;
@@ -367,8 +383,8 @@ __device__ void wave_heap_sort(uint64_t* key, int f, int e, Lt lt) {
 // k-th from the right, is Rp[nR - 1 - k]); each range of at most 64 is finished in registers
 // (small_sort), a range above 64 whose depth limit is spent by wave_heap_sort. The stack holds at
 // most one entry per level of the current path: <= depth limit + 1 entries.
-template <class Lt, int kStack = kSortStack>
-__device__ void exact_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp, int* stk, Lt lt,
+template <class K, class Lt, int kStack = kSortStack>
+__device__ void exact_introsort(K* key, int n, uint16_t* Lp, uint16_t* Rp, int* stk, Lt lt,
                                 int depth0 = -1) {
   const int l = lane_id();
   const unsigned long long ltm = (1ull << l) - 1ull;
@@ -388,18 +404,18 @@ __device__ void exact_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp
       rd--;
       // __move_median_to_first(first, first+1, mid, last-1)
       const int a = rf + 1, b = rf + (rl - rf) / 2, c = rl - 1;
-      const uint64_t va = key[a], vb = key[b], vc = key[c], vf = key[rf];
+      const K va = key[a], vb = key[b], vc = key[c], vf = key[rf];
       int m;
       if (lt(va, vb)) m = lt(vb, vc) ? b : (lt(va, vc) ? c : a);
       else m = lt(va, vc) ? a : (lt(vb, vc) ? c : b);
-      const uint64_t P = m == a ? va : (m == b ? vb : vc);
+      const K P = m == a ? va : (m == b ? vb : vc);
       wave_sync_lds();
       if (l == 0) { key[m] = vf; key[rf] = P; }
       wave_sync_lds();
       int nL = 0, nR = 0;
       for (int c0 = rf; c0 < rl; c0 += 64) {
         const int i = c0 + l;
-        const uint64_t v = i < rl ? key[i] : 0ull;
+        const K v = i < rl ? key[i] : K(0);
         const bool fl = i < rl && i > rf && !lt(v, P);
         const bool fr = i < rl && !lt(P, v);
         const unsigned long long mL = __ballot(fl), mR = __ballot(fr);
@@ -419,7 +435,7 @@ __device__ void exact_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp
       const int cut = (ks > 0 && (ks >= nL || Lp[ks] >= Rp[nR - ks])) ? Rp[nR - ks] : Lp[ks];
       for (int k = l; k < ks; k += 64) {
         const int a2 = Lp[k], b2 = Rp[nR - 1 - k];
-        const uint64_t t = key[a2]; key[a2] = key[b2]; key[b2] = t;
+        const K t = key[a2]; key[a2] = key[b2]; key[b2] = t;
       }
       wave_sync_lds();
       // the right part waits; the left part continues here
@@ -463,17 +479,17 @@ struct BlockSortLds {
 
 // One libstdc++ partition step of key[rf, rl) by one wave (rf + 1 < rl): the median of three to
 // rf, __unguarded_partition over (rf, rl) with the stop lists at Lp / Rp + rf; returns the cut.
-template <class Lt>
-__device__ __forceinline__ int wave_partition(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int rf, int rl, Lt lt) {
+template <class K, class Lt>
+__device__ __forceinline__ int wave_partition(K* key, uint16_t* Lp, uint16_t* Rp, int rf, int rl, Lt lt) {
   const int l = lane_id();
   const unsigned long long ltm = (1ull << l) - 1ull;
   // __move_median_to_first(first, first+1, mid, last-1)
   const int a = rf + 1, b = rf + (rl - rf) / 2, c = rl - 1;
-  const uint64_t va = key[a], vb = key[b], vc = key[c], vf = key[rf];
+  const K va = key[a], vb = key[b], vc = key[c], vf = key[rf];
   int m;
   if (lt(va, vb)) m = lt(vb, vc) ? b : (lt(va, vc) ? c : a);
   else m = lt(va, vc) ? a : (lt(vb, vc) ? c : b);
-  const uint64_t P = m == a ? va : (m == b ? vb : vc);
+  const K P = m == a ? va : (m == b ? vb : vc);
   wave_sync_lds();
   if (l == 0) { key[m] = vf; key[rf] = P; }
   wave_sync_lds();
@@ -482,7 +498,7 @@ __device__ __forceinline__ int wave_partition(uint64_t* key, uint16_t* Lp, uint1
   int nL = 0, nR = 0;
   for (int c0 = rf; c0 < rl; c0 += 128) {
     const int i0 = c0 + l, i1 = c0 + 64 + l;
-    const uint64_t v0 = i0 < rl ? key[i0] : 0ull, v1 = i1 < rl ? key[i1] : 0ull;
+    const K v0 = i0 < rl ? key[i0] : K(0), v1 = i1 < rl ? key[i1] : K(0);
     const bool fl0 = i0 < rl && i0 > rf && !lt(v0, P), fr0 = i0 < rl && !lt(P, v0);
     const bool fl1 = i1 < rl && !lt(v1, P), fr1 = i1 < rl && !lt(P, v1);
     const unsigned long long mL0 = __ballot(fl0), mR0 = __ballot(fr0), mL1 = __ballot(fl1), mR1 = __ballot(fr1);
@@ -513,8 +529,8 @@ __device__ __forceinline__ int wave_partition(uint64_t* key, uint16_t* Lp, uint1
     const bool two = k1 < ks;
     const int x0 = L[k0], y0 = R[nR - 1 - k0];
     const int x1 = two ? L[k1] : 0, y1 = two ? R[nR - 1 - k1] : 0;
-    const uint64_t p0 = key[x0], q0 = key[y0];
-    const uint64_t p1 = two ? key[x1] : 0ull, q1 = two ? key[y1] : 0ull;
+    const K p0 = key[x0], q0 = key[y0];
+    const K p1 = two ? key[x1] : K(0), q1 = two ? key[y1] : K(0);
     key[x0] = q0;
     key[y0] = p0;
     if (two) { key[x1] = q1; key[y1] = p1; }
@@ -526,24 +542,24 @@ __device__ __forceinline__ int wave_partition(uint64_t* key, uint16_t* Lp, uint1
 // One libstdc++ partition step of key[rf, rl) by the whole workgroup (kNT threads); returns the
 // cut (uniform). Thread t classifies positions [rf + t * per, +per); one block scan of the packed
 // (L, R) stop counts gives every stop its rank; the first k with !(L[k] < R[k]) is an LDS min.
-template <int kNT, class Lt>
-__device__ __forceinline__ int block_partition(uint64_t* key, uint16_t* Lp, uint16_t* Rp, int rf, int rl, BlockSortLds& s,
+template <int kNT, class K, class Lt>
+__device__ __forceinline__ int block_partition(K* key, uint16_t* Lp, uint16_t* Rp, int rf, int rl, BlockSortLds& s,
                                                Lt lt) {
   const int tid = threadIdx.x;
   if (tid == 0) {  // __move_median_to_first(first, first+1, mid, last-1)
     const int a = rf + 1, b = rf + (rl - rf) / 2, c = rl - 1;
-    const uint64_t va = key[a], vb = key[b], vc = key[c], vf = key[rf];
+    const K va = key[a], vb = key[b], vc = key[c], vf = key[rf];
     int m;
     if (lt(va, vb)) m = lt(vb, vc) ? b : (lt(va, vc) ? c : a);
     else m = lt(va, vc) ? a : (lt(vb, vc) ? c : b);
-    const uint64_t P = m == a ? va : (m == b ? vb : vc);
+    const K P = m == a ? va : (m == b ? vb : vc);
     key[m] = vf;
     key[rf] = P;
     s.piv = P;
     s.ks = 0x7fffffff;
   }
   __syncthreads();
-  const uint64_t P = s.piv;
+  const K P = (K)s.piv;
   const int per = (rl - rf + kNT - 1) / kNT;
   const int c0 = min(rf + tid * per, rl), c1 = min(c0 + per, rl);
   uint32_t mL = 0, mR = 0;
@@ -551,7 +567,7 @@ __device__ __forceinline__ int block_partition(uint64_t* key, uint16_t* Lp, uint
   for (int u = 0; u < 8; ++u) {
     const int i = c0 + u;
     if (i >= c1) continue;
-    const uint64_t v = key[i];
+    const K v = key[i];
     if (i > rf && !lt(v, P)) mL |= 1u << u;
     if (!lt(P, v)) mR |= 1u << u;
   }
@@ -583,7 +599,7 @@ __device__ __forceinline__ int block_partition(uint64_t* key, uint16_t* Lp, uint
     const int k0 = min(tid * pk, ks), k1 = min(k0 + pk, ks);
     for (int k = k0; k < k1; ++k) {
       const int x = L[k], y = R[nR - 1 - k];
-      const uint64_t t = key[x];
+      const K t = key[x];
       key[x] = key[y];
       key[y] = t;
     }
@@ -595,8 +611,8 @@ __device__ __forceinline__ int block_partition(uint64_t* key, uint16_t* Lp, uint
 
 // prof (diagnostics only, k_debug_exact_sort): prof[0] = clocks of the block-wide part; per wave w,
 // prof[1 + 4 w + 0..3] = clocks in wave partitions, small_sort, wave_heap_sort, and idle at the end
-template <int kNT, class Lt>
-__device__ __forceinline__ void block_introsort(uint64_t* key, int n, uint16_t* Lp, uint16_t* Rp, BlockSortLds& s, Lt lt,
+template <int kNT, class K, class Lt>
+__device__ __forceinline__ void block_introsort(K* key, int n, uint16_t* Lp, uint16_t* Rp, BlockSortLds& s, Lt lt,
                                                 long long* prof = nullptr, int stop = 1 << 30) {
   static_assert(kNT == 256, "block_introsort: four waves");
   const int tid = threadIdx.x, l = lane_id(), w = tid >> 6;
