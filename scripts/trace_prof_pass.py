@@ -13,7 +13,7 @@ from collections import defaultdict
 
 path, W, K, P = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
 KERNELS = ("k_project_fused", "k_ground_add", "k_ground_elev_ransac", "k_label", "k_segment", "k_fa_points",
-           "k_select_ring", "k_fa_concat", "k_dbscan_adj", "k_dbscan_merge")
+           "k_select_ring", "k_vox_pcl", "k_fa_concat", "k_dbscan_adj", "k_dbscan_merge")
 runs = defaultdict(list)
 for row in csv.DictReader(open(path)):
     name = row["Kernel_Name"].split("(")[0].replace("void ", "").replace("llsr::", "").split("<")[0]
