@@ -1304,13 +1304,13 @@ static int32_t s2s_launch(llsr_handle* h, const llsr_s2s_batch* b, void* hip_str
   const int bq = hint_q > 0 ? hint_q : std::max(m.ms, m.f);
   const int bnc = hint_nc > 0 ? hint_nc : m.nc;
   if (bq <= 1024 && bnc <= 1024) {
-    k_s2s_lm<1024, 1024><<<P, kS2SThreads, 0, s>>>(a);
+    k_s2s_lm<1024, 1024, 256><<<P, 256, 0, s>>>(a);
     m.last_variant = 1024;
   } else if (bq <= 2560 && bnc <= 1536) {
-    k_s2s_lm<2560, 1536><<<P, kS2SThreads, 0, s>>>(a);
+    k_s2s_lm<2560, 1536, 512><<<P, 512, 0, s>>>(a);
     m.last_variant = 2560;
   } else {
-    k_s2s_lm<2048, 2048><<<P, kS2SThreads, 0, s>>>(a);
+    k_s2s_lm<2048, 2048, 512><<<P, 512, 0, s>>>(a);
     m.last_variant = 2048;
   }
   HIP_OK(h, hipGetLastError());

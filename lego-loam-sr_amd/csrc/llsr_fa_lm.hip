@@ -1,7 +1,8 @@
 // llsr_fa_lm.hip — FeatureAssociation scan-to-scan LM on gfx950 (updateTransformation,
 // featureAssociation.cpp:2505-2535) for a batch of independent scans.
 //
-// k_s2s_lm: one kS2SThreads-thread workgroup per scan runs the whole two-phase optimisation in-kernel
+// k_s2s_lm: one kThreads-thread workgroup per scan (512, or 256 for the <1024, 1024> instantiation,
+// llsr_s2s.h) runs the whole two-phase optimisation in-kernel
 // (no host round trips): surf phase (FA:2508-2516) then corner phase (FA:2519-2527), each up to
 // 100 iterations. Per iteration:
 //   A  on iterations % 5 == 0 the kNN-1 of every query (q = tid, tid + kThreads, ...) after
@@ -40,7 +41,6 @@ using llsr_libm::sqrt_;
 
 namespace {
 
-constexpr int kThreads = kS2SThreads;
 constexpr int kMaxShell = 2;  // grid shells searched before the exact block-wide scan (queries in sparse regions)
 constexpr int kFbMax = 256;       // queries per kNN iteration whose shells did not settle (block scan)
 constexpr int kIx = 5;            // ints per query in S2SArgs::idx
@@ -142,8 +142,9 @@ __device__ __forceinline__ void nn1_scan(const float4* pts, int n, float4 q, int
 // reduced with the index tie-break — equal to nn1_scan per query, with one pass over the cloud
 // for kMulti queries. Contains barriers: every thread of the block must call it.
 constexpr int kMulti = 2;  // 2 (from 4): 113 instead of 166 spilled VGPRs at the 4-waves bound
+template <int kNT>
 __device__ void nn1_block_multi(const float4* pts, int n, const float4* qs, int nq, int* bi, float* bd,
-                                float (*red_d)[kThreads / 64], int (*red_i)[kThreads / 64]) {
+                                float (*red_d)[kNT / 64], int (*red_i)[kNT / 64]) {
   float d[kMulti];
   int id[kMulti];
 #pragma unroll
@@ -666,8 +667,9 @@ __global__ void k_s2s_boxes(S2SArgs a) {
 // (39 KB, 4 workgroups per CU: VLP-16-sized scans), 2560 / 1536 (78 KB, 2 per CU: HDL-64E, whose
 // ~2.1-2.2k flat queries would otherwise sum their rows from HBM every surf iteration) and
 // 2048 / 2048 (77 KB) otherwise.
-template <int kLdsRows, int kLdsCorner>
-__global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
+template <int kLdsRows, int kLdsCorner, int kNT>
+__global__ __launch_bounds__(kNT, 4) void k_s2s_lm(S2SArgs a) {
+  constexpr int kThreads = kNT;  // (shadows the default: the instantiation's workgroup size)
   const int p = blockIdx.x;
   const int tid = threadIdx.x;
 #ifdef LLSR_S2S_PROF
@@ -843,7 +845,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
             for (int j = 0; j < kMulti; ++j) qs[j] = j < m ? to_start(tl, qry[fbq[k0 + j]]) : make_float4(0.f, 0.f, 0.f, 0.f);
             int nn[kMulti];
             float nd[kMulti];
-            nn1_block_multi(surf ? sl : clg, surf ? Ns : Nc, qs, m, nn, nd, red_d, red_i);
+            nn1_block_multi<kThreads>(surf ? sl : clg, surf ? Ns : Nc, qs, m, nn, nd, red_d, red_i);
 #pragma unroll
             for (int j = 0; j < kMulti; ++j)
               if (j < m && tid == j) park(fbq[k0 + j], nn[j], nd[j]);
@@ -1139,8 +1141,8 @@ __global__ __launch_bounds__(kThreads, 4) void k_s2s_lm(S2SArgs a) {
   }
 }
 
-template __global__ void k_s2s_lm<2048, 2048>(S2SArgs);
-template __global__ void k_s2s_lm<2560, 1536>(S2SArgs);
-template __global__ void k_s2s_lm<1024, 1024>(S2SArgs);
+template __global__ void k_s2s_lm<2048, 2048, 512>(S2SArgs);
+template __global__ void k_s2s_lm<2560, 1536, 512>(S2SArgs);
+template __global__ void k_s2s_lm<1024, 1024, 256>(S2SArgs);
 
 }  // namespace llsr

@@ -30,10 +30,13 @@ struct S2SArgs {
 // cannot hold a nearer point); grid (ceil(ceil(cap / 8) / 256), P), block 256
 __global__ void k_s2s_boxes(S2SArgs a);
 
-// threads per scan-to-scan workgroup (one workgroup per problem)
-constexpr int kS2SThreads = 512;  // measured: 256 -> 512 HDL-64E LM 39.3 -> 32.6 ms, VLP-16 9.1 -> 8.4 ms; 1024 slower on VLP-16
+// threads per scan-to-scan workgroup (one workgroup per problem): 512 for the large instantiations
+// (HDL-64E clouds: 256 -> 512 took the LM 39.3 -> 32.6 ms in round 2), 256 for <1024, 1024>: four
+// workgroups per CU instead of two, so a 1024-scan VLP-16 batch runs in one round instead of two
+// (LM 6.98 -> 4.82 ms, round 5)
+constexpr int kS2SThreads = 512;
 
-template <int kLdsRows, int kLdsCorner>
-__global__ void k_s2s_lm(S2SArgs a);  // instantiated for <1024, 1024>, <2560, 1536>, <2048, 2048>
+template <int kLdsRows, int kLdsCorner, int kNT>
+__global__ void k_s2s_lm(S2SArgs a);  // instantiated for <1024, 1024, 256>, <2560, 1536, 512>, <2048, 2048, 512>
 
 }  // namespace llsr
