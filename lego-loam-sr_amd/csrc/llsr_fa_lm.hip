@@ -975,28 +975,32 @@ __global__ __launch_bounds__(kNT, 4) void k_s2s_lm(S2SArgs a) {
           }
           __syncthreads();
           const int N = nrow;
-          constexpr int kMv = (kLdsRows + kThreads - 1) / kThreads;
-          float4 mv[kMv];
+          // in steps of 2 rows per lane (fewer registers live across the barrier): a step's sources
+          // lvix[i] >= i lie at or beyond its destinations and beyond every earlier step's
+          constexpr int kMvS = 2;
+          for (int c0 = 0; c0 < N; c0 += kMvS * kThreads) {
+            float4 mv[kMvS];
 #pragma unroll
-          for (int u = 0; u < kMv; ++u) {
-            const int i = tid + u * kThreads;
-            if (i < N) {
-              const int r = lvix[i];
-              mv[u] = make_float4(lrow4[r], lrow4[kLdsRows + r], lrow4[2 * kLdsRows + r], lrow4[3 * kLdsRows + r]);
+            for (int u = 0; u < kMvS; ++u) {
+              const int i = c0 + tid + u * kThreads;
+              if (i < N) {
+                const int r = lvix[i];
+                mv[u] = make_float4(lrow4[r], lrow4[kLdsRows + r], lrow4[2 * kLdsRows + r], lrow4[3 * kLdsRows + r]);
+              }
             }
-          }
-          __syncthreads();
+            __syncthreads();
 #pragma unroll
-          for (int u = 0; u < kMv; ++u) {
-            const int i = tid + u * kThreads;
-            if (i < N) {
-              lrow4[i] = mv[u].x;
-              lrow4[kLdsRows + i] = mv[u].y;
-              lrow4[2 * kLdsRows + i] = mv[u].z;
-              lrow4[3 * kLdsRows + i] = mv[u].w;
+            for (int u = 0; u < kMvS; ++u) {
+              const int i = c0 + tid + u * kThreads;
+              if (i < N) {
+                lrow4[i] = mv[u].x;
+                lrow4[kLdsRows + i] = mv[u].y;
+                lrow4[2 * kLdsRows + i] = mv[u].z;
+                lrow4[3 * kLdsRows + i] = mv[u].w;
+              }
             }
+            __syncthreads();
           }
-          __syncthreads();
           const bool lazyAll = N + 6 < 20;
           const int kc = lazyAll ? N : llsr_eigen::gemm_kc(N, 3, 3);
           const int nblk = lazyAll || N == 0 ? 1 : (N + kc - 1) / kc;
