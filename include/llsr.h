@@ -520,6 +520,17 @@ int32_t llsr_mapping_associate(const float transform_sum_fa[6], const float tran
                                float transform_tobe_mapped[6], float transform_incre[6]);
 
 
+/* ---- FA end of scan on the FA node's thread (host side, no handle) ----
+ * For a node whose FeatureAssociation thread owns its own clouds and calls llsr_scan2scan on its
+ * own handle: integrateTransformation (FA:2537-2568, no IMU) updates
+ * transform_sum in place from transformCur; TransformToEnd (FA:1414-1490, the
+ * use_imu_undistortion == false branch) moves n float4 rows (x, y, z, intensity; intensity =
+ * ring + relTime / 10 as adjustDistortion leaves it) to the scan's end with transformCur, as
+ * publishCloudsLast does for the less-sharp / less-flat and sharp / flat clouds (FA:2666-2707).
+ * out_xyzi may equal in_xyzi. Bit-identical to the device odometry path (llsr_odometry_batch). */
+int32_t llsr_integrate_transformation(float transform_sum[6], const float transform_cur[6]);
+int32_t llsr_transform_to_end(const float transform_cur[6], const float* in_xyzi, int32_t n, float* out_xyzi);
+
 /* ---- TransformFusion (transformFusion.cpp) ----
  * The fourth node of the reference fuses the 10 Hz scan-to-scan odometry with the slower mapped
  * pose. It is scalar host work per message, so these entry points run on the host side of the

@@ -7,14 +7,26 @@
 // Seams (reference file:line):
 //   ImageProjection::cloudHandler            imageProjection.cpp:189-222 -> Projection::run
 //   FeatureAssociation feature stage         featureAssociation.cpp:2769-2775 (+ 1310-1314 shadow points)
-//                                                                         -> Projection::features
+//                                            -> Projection::handoff (on the IP thread, into ProjectionOut)
+//   runFeatureAssociation after the features featureAssociation.cpp:2777-2796, 2291-2315, 2660-2712
+//                                            -> Odometry::step (on the FA thread, its own handle)
 //   FeatureAssociation::updateTransformation featureAssociation.cpp:2505-2535 -> update_transformation
 //   MapOptimization::scan2MapOptimization    mapOptmization.cpp:1572-1610 -> scan2map_optimization
+//
+// Threads. The reference runs IP, FA and MO on their own executor threads joined by one-slot
+// Channels (main.cpp:10-11, channel.h:24-54); IP's blocking send waits only until FA has *taken*
+// the previous scan, so IP's next cloudHandler overlaps FA's work on the last one. A handle is
+// single-threaded and its host buffers are overwritten by the next scan, so nothing that FA uses
+// may point into the IP node's Projection: the feature stage keeps FA's carry-over state
+// (FA:167-198) in the IP handle and runs with the rest of the scan on the IP thread, and
+// Projection::handoff copies its clouds into the ProjectionOut that crosses the channel
+// (FeatureClouds below). FA's Odometry and MO's scan-to-map each own another handle.
 #pragma once
 #include <stdint.h>
 
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "llsr.h"
@@ -125,6 +137,70 @@ void features(const llsr_scan_out& o, const float* shadow, int32_t ns, Cloud& se
   unpack_xyzi(o.less_flat_xyzi, o.n_less_flat, surf_less_flat);
 }
 
+// The feature clouds of one scan as runFeatureAssociation holds them after extractFeaturesOurs
+// (FA:2769-2775): computed on the IP thread and carried to FA inside ProjectionOut. A maintainer
+// adds the member `llsr_ros2::FeatureClouds<pcl::PointCloud<PointType>> features;` to ProjectionOut
+// (UT:63-72). Values, not pointers into a handle's buffers: the IP thread's next scan cannot touch
+// them once they are in the channel.
+template <class Cloud>
+struct FeatureClouds {
+  Cloud segmented;          // segmentedCloud after adjustDistortion (LOAM frame)
+  Cloud corner_sharp;       // cornerPointsSharp
+  Cloud corner_less_sharp;  // cornerPointsLessSharp
+  Cloud surf_flat;          // surfPointsFlat + the shadow points (FA:1310-1314)
+  Cloud surf_less_flat;     // surfPointsLessFlat (per-ring VoxelGrid)
+};
+
+// TransformToEnd (FA:1414-1490) of every point of `in` into `out` (may be the same cloud)
+template <class Cloud>
+void transform_to_end(const float transform_cur[6], const Cloud& in, Cloud& out) {
+  std::vector<float> a;
+  repack_xyzi(in, a);
+  const int32_t n = (int32_t)(a.size() / 4);
+  check(llsr_transform_to_end(transform_cur, a.data(), n, a.data()), nullptr, "llsr_transform_to_end");
+  unpack_xyzi(a.data(), n, out);
+}
+
+template <class Cloud>
+void append_xyzi(const float* xyzi, int32_t n, Cloud& c) {
+  const size_t f = c.points.size();
+  c.points.resize(f + (size_t)n);
+  for (int32_t k = 0; k < n; ++k) {
+    auto& p = c.points[f + (size_t)k];
+    p.x = xyzi[4 * k];
+    p.y = xyzi[4 * k + 1];
+    p.z = xyzi[4 * k + 2];
+    p.intensity = xyzi[4 * k + 3];
+  }
+  c.width = (uint32_t)c.points.size();
+  c.height = 1;
+}
+
+// An llsr handle owned by one node thread (FA's scan-to-scan, MO's scan-to-map): one scan slot,
+// the LMs' buffers grow on first use. mode: LLSR_MODE_FAITHFUL / LLSR_MODE_LM_APPLIED (MO:1539-1545)
+class Handle {
+ public:
+  explicit Handle(int32_t lidar, int32_t device = 0, int32_t mode = LLSR_MODE_LM_APPLIED) {
+    llsr_config cfg;
+    check(llsr_config_default(&cfg, lidar), nullptr, "llsr_config_default");
+    if (llsr_abi_version() != LLSR_ABI_VERSION) throw std::runtime_error("llsr: library ABI version differs from llsr.h");
+    cfg.mode = mode;
+    llsr_handle* h = nullptr;
+    const int32_t rc = llsr_create(&cfg, device, 1, cfg.num_vertical_scans * cfg.num_horizontal_scans, &h);
+    if (rc != LLSR_OK || !h) throw std::runtime_error("llsr: llsr_create failed (no HIP device?)");
+    h_ = h;
+  }
+  ~Handle() {
+    if (h_) llsr_destroy(h_);
+  }
+  Handle(const Handle&) = delete;
+  Handle& operator=(const Handle&) = delete;
+  llsr_handle* get() const { return h_; }
+
+ private:
+  llsr_handle* h_ = nullptr;
+};
+
 // One handle and its host output buffers (capacity H*W per array, llsr_query_sizes), for the
 // single-scan call shape the nodes use; one per pipeline thread, as the reference runs one thread
 // per node.
@@ -207,6 +283,14 @@ class Projection {
     llsr_ros2::features(o_, shadow_.data(), (int32_t)(shadow_.size() / 4), segmented_cloud, corner_sharp,
                         corner_less_sharp, surf_flat, surf_less_flat);
   }
+  // publishClouds' ProjectionOut (IP:933-1000) with this scan's feature clouds in po.features, built
+  // on the IP thread before Channel::send; po.segmented_cloud / outlier_cloud must be allocated
+  template <class ProjOut>
+  void handoff(ProjOut& po) const {
+    projection_out(po, *po.segmented_cloud, *po.outlier_cloud);
+    features(po.features.segmented, po.features.corner_sharp, po.features.corner_less_sharp, po.features.surf_flat,
+             po.features.surf_less_flat);
+  }
 
  private:
   llsr_handle* h_ = nullptr;
@@ -238,6 +322,56 @@ llsr_s2s_report update_transformation(llsr_handle* h, const Cloud& corner_sharp,
   is_degenerate = deg != 0;
   return rep;
 }
+
+// runFeatureAssociation from `if (!systemInitedLM)` on (FA:2777-2796) for the FA node's thread, on
+// its own handle and its own clouds: checkSystemInitialization (FA:2291-2315) on the first scan,
+// then updateTransformation (FA:2505-2535), integrateTransformation (FA:2537-2568) and
+// publishCloudsLast (FA:2660-2712: TransformToEnd of the less-sharp / less-flat clouds, which
+// become the last clouds + the shadow points, and of the sharp / flat clouds, MO's scan clouds).
+// updateInitialGuess (FA:2790) and publishOdometry stay node code; without an IMU, transformCur
+// carries over as the next LM's initial guess (LLSR_MODE_LM_APPLIED semantics).
+template <class Cloud>
+class Odometry {
+ public:
+  explicit Odometry(int32_t lidar, int32_t device = 0) : h_(lidar, device) {
+    shadow_.resize(4 * 160);
+    check(llsr_shadow_points(shadow_.data()), nullptr, "llsr_shadow_points");
+  }
+  llsr_handle* handle() const { return h_.get(); }
+
+  // one scan's features (moved from the channel's ProjectionOut); false on the initialisation scan
+  bool step(FeatureClouds<Cloud>& f) {
+    if (!inited_) {
+      corner_last = std::move(f.corner_less_sharp);
+      surf_last = std::move(f.surf_less_flat);
+      append_xyzi(shadow_.data(), (int32_t)(shadow_.size() / 4), surf_last);
+      inited_ = true;
+      return false;
+    }
+    report = update_transformation(h_.get(), f.corner_sharp, f.surf_flat, corner_last, surf_last, transform_cur,
+                                   is_degenerate);
+    check(llsr_integrate_transformation(transform_sum, transform_cur), nullptr, "llsr_integrate_transformation");
+    transform_to_end(transform_cur, f.corner_less_sharp, corner_last);
+    transform_to_end(transform_cur, f.surf_less_flat, surf_last);
+    append_xyzi(shadow_.data(), (int32_t)(shadow_.size() / 4), surf_last);
+    transform_to_end(transform_cur, f.corner_sharp, corner_scan);
+    transform_to_end(transform_cur, f.surf_flat, surf_scan);
+    return true;
+  }
+
+  // FA's member state after the last step
+  float transform_cur[6] = {0, 0, 0, 0, 0, 0};
+  float transform_sum[6] = {0, 0, 0, 0, 0, 0};
+  bool is_degenerate = false;
+  llsr_s2s_report report = llsr_s2s_report();
+  Cloud corner_last, surf_last;   // laserCloudCornerLast / laserCloudSurfLast
+  Cloud corner_scan, surf_scan;   // laserCloudCornerScan / laserCloudSurfScan (AssociationOut)
+
+ private:
+  Handle h_;
+  bool inited_ = false;
+  std::vector<float> shadow_;
+};
 
 // scan2MapOptimization (MO:1572-1610) once its guard (MO:1573: corner map > 10, surf map > 100)
 // holds: kd-tree builds, corner / surf optimisation and LMOptimization on transformTobeMapped;

@@ -6,6 +6,7 @@
 #include <cfloat>
 #include <climits>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -32,7 +33,9 @@ __global__ void k_segment(DevCfg, const float4*, const int64_t*, DevBufs);
 __global__ void k_fa_points(DevCfg, DevBufs);
 __global__ void k_select_ring(DevCfg, DevBufs);
 __global__ void k_vox_pcl(DevCfg, DevBufs);
+__global__ void k_vox_pcl_w(DevCfg, DevBufs);
 __global__ void k_debug_exact_sort(const float*, int, int*, long long*);
+__global__ void k_debug_exact_sort32(const uint32_t*, int, int, int*);
 __global__ void k_fa_concat(DevCfg, DevBufs);
 __global__ void k_dbscan_adj(DevCfg, DevBufs);
 __global__ void k_vis_clouds(DevCfg, DevBufs, int, float4*, int*);
@@ -80,6 +83,7 @@ struct llsr_handle {
   const float4* last_pts = nullptr;  // inputs of the last batch (diagnostic re-launches only)
   const int64_t* last_off = nullptr;
   bool profiling = false;
+  bool debug_sync = false;  // LLSR_DEBUG_SYNC=1: wait after every feature-batch kernel, name a failing one
   // Event sets for up to kRing in-flight profiled batches; retired sets are summed into ksum.
   static constexpr int kRing = 64;
   hipEvent_t ev[kRing][kNumKernels + 1] = {};
@@ -171,6 +175,13 @@ static int label_lds(const DevCfg& c) { return c.HW * (int)(sizeof(int) + 1); }
 
 static int label_band_lds(const DevCfg& c) { return c.lbl_band * c.W * (int)sizeof(int); }
 static bool use_fused(const llsr_handle* h) { return h->dc.ccl_lds != 0; }
+
+// the PCL-order less-flat VoxelGrid of every pending ring: one wave per small ring, then a
+// workgroup per large one (each kernel skips the other's rings)
+static void launch_vox_pcl(const DevCfg& c, const DevBufs& d, int B, hipStream_t s) {
+  k_vox_pcl_w<<<dim3((c.H + kVoxRings - 1) / kVoxRings, B), 64 * kVoxRings, 0, s>>>(c, d);
+  k_vox_pcl<<<dim3(c.H, B), 256, 0, s>>>(c, d);
+}
 
 static int32_t fail(llsr_handle* h, int32_t code, const std::string& msg) {
   if (h) h->err = msg;
@@ -357,6 +368,10 @@ extern "C" int32_t llsr_create(const llsr_config* cfg, int32_t hip_device, int32
     llsr_destroy(h);
     return LLSR_ENOMEM;
   }
+  {
+    const char* ds = std::getenv("LLSR_DEBUG_SYNC");
+    h->debug_sync = ds && ds[0] == '1';
+  }
   for (auto& set : h->ev)
     for (auto& e : set)
       if (hipEventCreate(&e) != hipSuccess) { llsr_destroy(h); return LLSR_ENODEV; }
@@ -513,6 +528,10 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   hipEvent_t* evs = h->ev[h->ring_head];
   auto mark = [&]() {
     if (h->profiling) (void)hipEventRecord(evs[k], s);
+    if (h->debug_sync) {  // diagnostics: the kernel that faults is the last one named
+      const hipError_t e = hipStreamSynchronize(s);
+      std::fprintf(stderr, "llsr debug: after %s: %s\n", k < kNumKernels ? kKernelNames[k] : "?", hipGetErrorString(e));
+    }
     ++k;
   };
   mark();
@@ -547,7 +566,7 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   mark();
   k_select_ring<<<dim3(c.H, B), 256, 0, s>>>(c, h->d);
   mark();
-  if (c.exact_vg) k_vox_pcl<<<dim3(c.H, B), 256, 0, s>>>(c, h->d);  // the PCL-order VoxelGrid
+  if (c.exact_vg) launch_vox_pcl(c, h->d, B, s);  // the PCL-order VoxelGrid
   mark();
   k_fa_concat<<<B, 256, 0, s>>>(c, h->d);
   mark();
@@ -610,6 +629,32 @@ extern "C" int32_t llsr_debug_exact_sort(const float* vals, int32_t n, int32_t* 
   return rc;
 }
 
+// Diagnostics (not part of the ABI header): the PCL-order VoxelGrid's exact sort of 32-bit keys
+// (VoxLess32: voxel rank << 11 | position) on n <= 2048 host ranks < 2^21, by the workgroup
+// (mode 0, k_vox_pcl's block_introsort) or one wave (mode 1, k_vox_pcl_w's wave_introsort); out[k] =
+// the input position at sorted position k. For tests/test_gpu_features_ties.py.
+extern "C" int32_t llsr_debug_exact_sort32(const uint32_t* ranks, int32_t n, int32_t mode, int32_t* out) {
+  if (!ranks || !out || n < 0 || n > 2048 || mode < 0 || mode > 1) return LLSR_EINVAL;
+  for (int32_t t = 0; t < n; ++t)
+    if (ranks[t] >= (1u << 21)) return LLSR_EINVAL;
+  if (n == 0) return LLSR_OK;
+  uint32_t* dv = nullptr;
+  int* di = nullptr;
+  if (hipMalloc(&dv, sizeof(uint32_t) * n) != hipSuccess) return LLSR_ENODEV;
+  if (hipMalloc(&di, sizeof(int) * n) != hipSuccess) { (void)hipFree(dv); return LLSR_ENODEV; }
+  int32_t rc = LLSR_OK;
+  if (hipMemcpy(dv, ranks, sizeof(uint32_t) * n, hipMemcpyHostToDevice) != hipSuccess) rc = LLSR_EIO;
+  if (rc == LLSR_OK) {
+    k_debug_exact_sort32<<<1, 256>>>(dv, n, mode, di);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(out, di, sizeof(int) * n, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = LLSR_EIO;
+  }
+  (void)hipFree(dv);
+  (void)hipFree(di);
+  return rc;
+}
+
 // Diagnostics (not part of the ABI header): mean device ms of one block_introsort of vals[0, n)
 // by one 256-thread workgroup (k_debug_exact_sort), over `reps` launches.
 extern "C" float llsr_debug_exact_sort_ms(const float* vals, int32_t n, int32_t reps) {
@@ -659,6 +704,18 @@ extern "C" int32_t llsr_debug_exact_sort_phases(const float* vals, int32_t n, lo
   return rc;
 }
 
+// After diagnostic launches of the selection stage that stop early: the whole stage once more with
+// the handle's configuration, so every ring's less-flat count is final again (k_select_ring leaves
+// a pending ring's count negative until the PCL-order VoxelGrid writes it; a later k_fa_concat
+// builds its ring offsets from these counts).
+static void restore_selection(llsr_handle* h, int B, hipStream_t s) {
+  const DevCfg& c = h->dc;
+  k_fa_points<<<B, 512, 0, s>>>(c, h->d);
+  k_select_ring<<<dim3(c.H, B), 256, 0, s>>>(c, h->d);
+  if (c.exact_vg) launch_vox_pcl(c, h->d, B, s);
+  (void)hipStreamSynchronize(s);
+}
+
 // Diagnostics (not part of the ABI header): re-launch kernel k on the last batch's buffers with
 // an early exit at `phase`, `reps` times; returns the mean device ms per launch (< 0 on error).
 // Used to attribute a kernel's time to its phases; results of such launches are meaningless.
@@ -677,12 +734,13 @@ extern "C" float llsr_debug_phase_ms(llsr_handle* h, int32_t k, int32_t phase, i
       k_fa_points<<<B, 512, 0, s>>>(h->dc, h->d);
       k_select_ring<<<dim3(c.H, B), 256, 0, s>>>(h->dc, h->d);
       (void)hipEventRecord(e0, s);
-      k_vox_pcl<<<dim3(c.H, B), 256, 0, s>>>(c, h->d);
+      launch_vox_pcl(c, h->d, B, s);
       (void)hipEventRecord(e1, s);
       float ms = 0.f;
       if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) return -1.f;
       tot += ms;
     }
+    restore_selection(h, B, s);
     return tot / reps;
   }
   if (k == 8) {
@@ -698,6 +756,7 @@ extern "C" float llsr_debug_phase_ms(llsr_handle* h, int32_t k, int32_t phase, i
       if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) return -1.f;
       tot += ms;
     }
+    restore_selection(h, B, s);
     return tot / reps;
   }
   (void)hipEventRecord(e0, s);
@@ -1220,7 +1279,8 @@ extern "C" int32_t llsr_scan2scan_reserve(llsr_handle* h, int32_t P, int32_t ms,
   const size_t capq = (size_t)(ms > f ? ms : f) + 1;
   const size_t bytes = sizeof(CellSlot) * P * (Tc + Ts) + (sizeof(float4) + sizeof(int2)) * P * ((size_t)nc + ns) +
                        sizeof(int) * 2 * P + (5 * sizeof(int) + sizeof(float4) + 1) * P * capq +
-                       sizeof(float4) * 2 * P * (((size_t)ns + 7) / 8 + ((size_t)ns + 63) / 64) + 64 + 15 * 256;
+                       sizeof(float4) * 2 * P * (((size_t)ns + 7) / 8 + ((size_t)ns + 63) / 64) +
+                       sizeof(float) * 8 * P + 64 + 16 * 256;
   if (hipMalloc(&m.pool, bytes) != hipSuccess) {
     m.pool = nullptr;
     m.P = 0;
@@ -1247,6 +1307,7 @@ extern "C" int32_t llsr_scan2scan_reserve(llsr_handle* h, int32_t P, int32_t ms,
   a.error = carve<int>(q, 1);
   a.sbox = carve<float4>(q, 2 * (size_t)P * (((size_t)ns + 7) / 8));
   a.sbox2 = carve<float4>(q, 2 * (size_t)P * (((size_t)ns + 63) / 64));
+  a.prof = carve<float>(q, 8 * (size_t)P);
 
   a.cap_sharp = ms;
   a.cap_flat = f;
@@ -1304,13 +1365,13 @@ static int32_t s2s_launch(llsr_handle* h, const llsr_s2s_batch* b, void* hip_str
   const int bq = hint_q > 0 ? hint_q : std::max(m.ms, m.f);
   const int bnc = hint_nc > 0 ? hint_nc : m.nc;
   if (bq <= 1024 && bnc <= 1024) {
-    k_s2s_lm<1024, 1024, 256><<<P, 256, 0, s>>>(a);
+    s2s_lm_launch<1024, 1024, 256>(P, s, a);
     m.last_variant = 1024;
   } else if (bq <= 2560 && bnc <= 1536) {
-    k_s2s_lm<2560, 1536, 512><<<P, 512, 0, s>>>(a);
+    s2s_lm_launch<2560, 1536, 512>(P, s, a);
     m.last_variant = 2560;
   } else {
-    k_s2s_lm<2048, 2048, 512><<<P, 512, 0, s>>>(a);
+    s2s_lm_launch<2048, 2048, 512>(P, s, a);
     m.last_variant = 2048;
   }
   HIP_OK(h, hipGetLastError());
@@ -1337,6 +1398,21 @@ extern "C" int32_t llsr_scan2scan_batch(llsr_handle* h, const llsr_s2s_batch* b,
 // instantiation the last scan-to-scan launch of this handle used, 0 before any; the two large ones
 // run the whole-wave surf walks (tests/test_gpu_fa_lm.py asserts which one a test exercised).
 extern "C" int32_t llsr_debug_s2s_variant(llsr_handle* h) { return h ? h->s2s.last_variant : -1; }
+
+// Diagnostics (not part of the ABI header): the diagnostics build's per-problem phase ticks of the
+// last scan-to-scan launch (k_s2s_lm, LLSR_S2S_PROF: knn surf / corner, A rows, B sums, C solve,
+// corner / surf walks, whole kernel, 100 MHz; [7] the shell fallback queries), [P][8] into out.
+// Synchronises. The product build leaves the buffer unwritten.
+extern "C" int32_t llsr_debug_s2s_prof(llsr_handle* h, float* out, int32_t cap) {
+  if (!h || !out || cap < 0) return LLSR_EINVAL;
+  auto& m = h->s2s;
+  if (!m.pool) return fail(h, LLSR_EINVAL, "no scan-to-scan batch");
+  HIP_OK(h, hipSetDevice(h->device));
+  HIP_OK(h, sync_handle_streams(h));
+  const int n = cap < m.P ? cap : m.P;
+  HIP_OK(h, hipMemcpy(out, m.a.prof, sizeof(float) * 8 * (size_t)n, hipMemcpyDeviceToHost));
+  return n;
+}
 
 extern "C" int32_t llsr_scan2scan_stats(llsr_handle* h, llsr_s2s_stats* out) {
   if (!h || !out) return LLSR_EINVAL;
@@ -2087,6 +2163,39 @@ extern "C" int32_t llsr_fusion_aft_mapped(llsr_fusion_state* st, const llsr_odom
   for (int k = 0; k < 3; ++k) {                                       // TF:299-304
     st->transform_bef_mapped[k] = (float)m->twist_angular[k];
     st->transform_bef_mapped[3 + k] = (float)m->twist_linear[k];
+  }
+  return LLSR_OK;
+}
+
+// ---- FA end of scan on the FA node's own thread (host side, no handle) ------------------------
+// integrateTransformation (FA:2537-2568) and TransformToEnd (FA:1414-1490) as k_odo_finish runs
+// them, for a node whose FA thread owns its clouds: the same functions
+// (llsr_odo.h) compiled for the host, with the same glibc-exact sin / cos / asin / atan2 ports.
+extern "C" int32_t llsr_integrate_transformation(float* transform_sum, const float* transform_cur) {
+  if (!transform_sum || !transform_cur) return LLSR_EINVAL;
+  float ts[6], tc[6];
+  for (int k = 0; k < 6; ++k) {
+    ts[k] = transform_sum[k];
+    tc[k] = transform_cur[k];
+  }
+  llsr::odo_integrate(ts, tc);
+  for (int k = 0; k < 6; ++k) transform_sum[k] = ts[k];
+  return LLSR_OK;
+}
+
+extern "C" int32_t llsr_transform_to_end(const float* transform_cur, const float* in_xyzi, int32_t n,
+                                         float* out_xyzi) {
+  if (!transform_cur || n < 0 || (n > 0 && (!in_xyzi || !out_xyzi))) return LLSR_EINVAL;
+  float tc[6];
+  for (int k = 0; k < 6; ++k) tc[k] = transform_cur[k];
+  for (int32_t i = 0; i < n; ++i) {  // in place allowed: each row is read before it is written
+    const float* r = in_xyzi + 4 * (size_t)i;
+    const float4 q = llsr::odo_to_end(tc, make_float4(r[0], r[1], r[2], r[3]));
+    float* o = out_xyzi + 4 * (size_t)i;
+    o[0] = q.x;
+    o[1] = q.y;
+    o[2] = q.z;
+    o[3] = q.w;
   }
   return LLSR_OK;
 }

@@ -87,6 +87,10 @@ struct DevBufs {
 
 // DBSCAN adjacency capacity per scan (edge candidates); larger M falls back to on-the-fly rows.
 constexpr int kAdjCap = 2048;
+// the PCL-order less-flat VoxelGrid: rings of at most kVoxWave candidates are sorted by one wave
+// each (k_vox_pcl_w, kVoxRings rings per workgroup), larger ones by a 256-thread workgroup (k_vox_pcl)
+constexpr int kVoxWave = 512;
+constexpr int kVoxRings = 1;
 constexpr int kAdjWords = kAdjCap / 32;
 
 // fullCloud's intensity of cell (row i, col j): (float)(i + j / 10000.0) (IP:341); the double
@@ -215,7 +219,7 @@ __device__ __forceinline__ int block_reduce_min(int v, int* tmp) {
 }
 
 // x86-64 truncating conversions (cvttss2si / cvttsd2si): NaN / out of range -> INT_MIN.
-__device__ __forceinline__ int trunc_i32(double v) {
+__host__ __device__ __forceinline__ int trunc_i32(double v) {
   if (!(v > -2147483649.0 && v < 2147483648.0)) return (int)0x80000000;
   return (int)v;
 }

@@ -1134,12 +1134,11 @@ __global__ __launch_bounds__(kNT, 4) void k_s2s_lm(S2SArgs a) {
     }
     r.ms = 0.0f;
 #ifdef LLSR_S2S_PROF
-    r.transform_cur[0] = (float)tAks; r.transform_cur[1] = (float)tAkc; r.transform_cur[2] = (float)tA;
-    r.transform_cur[3] = (float)tB; r.transform_cur[4] = (float)tC; r.transform_cur[5] = (float)tF;
-    r.ms = (float)tW;
-    // the fallback count rides in report.degenerate's upper bits: `skipped` keeps its FA:2506 meaning,
-    // bit 0 stays isDegenerate, and the state itself (a.degen) is untouched
-    r.degenerate = isDeg | (nfb_total << 1);
+    // phase ticks and the shell fallback count to the diagnostics buffer (llsr_debug_s2s_prof); the
+    // report keeps its ABI meaning in every build
+    float* pf = a.prof + 8 * (size_t)p;
+    pf[0] = (float)tAks; pf[1] = (float)tAkc; pf[2] = (float)tA; pf[3] = (float)tB;
+    pf[4] = (float)tC; pf[5] = (float)tF; pf[6] = (float)tW; pf[7] = (float)nfb_total;
 #endif
     a.degen[p] = isDeg;
   }

@@ -44,6 +44,7 @@ EXPORTS = [
     "llsr_mapping_init", "llsr_mapping_batch", "llsr_mapping_fetch", "llsr_mapping_keyposes", "llsr_mapping_reset",
     "llsr_mapping_associate", "llsr_set_voxel_order", "llsr_scan2scan_stats", "llsr_fusion_init",
     "llsr_pose_to_odometry", "llsr_odometry_to_transform", "llsr_fusion_laser_odometry", "llsr_fusion_aft_mapped",
+    "llsr_integrate_transformation", "llsr_transform_to_end",
 ]
 
 
@@ -98,6 +99,8 @@ def lib():
                                                  C.POINTER(_abi.OdometryMsg)]
         L.llsr_fusion_aft_mapped.argtypes = [C.POINTER(_abi.FusionState), C.POINTER(_abi.OdometryMsg)]
         L.llsr_shadow_points.argtypes = [C.c_void_p]
+        L.llsr_integrate_transformation.argtypes = [C.c_void_p, C.c_void_p]
+        L.llsr_transform_to_end.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
         L.llsr_scan2scan_reserve.argtypes = [C.c_void_p] + [C.c_int32] * 5
         L.llsr_scan2scan_batch.argtypes = [C.c_void_p, C.POINTER(_abi.S2SBatch), C.c_void_p]
         L.llsr_scan2scan_check.argtypes = [C.c_void_p]
@@ -479,6 +482,27 @@ def shadow_points() -> np.ndarray:
     rc = lib().llsr_shadow_points(out.ctypes.data)
     if rc != 0:
         raise LlsrError(f"llsr_shadow_points: {rc}")
+    return out
+
+
+def integrate_transformation(transform_sum, transform_cur) -> np.ndarray:
+    """integrateTransformation (FA:2537-2568) on the host side of the library: the new transformSum."""
+    ts = np.array(transform_sum, np.float32).reshape(6).copy()
+    tc = np.ascontiguousarray(transform_cur, np.float32).reshape(6)
+    rc = lib().llsr_integrate_transformation(ts.ctypes.data, tc.ctypes.data)
+    if rc != 0:
+        raise LlsrError(f"llsr_integrate_transformation: {rc}")
+    return ts
+
+
+def transform_to_end(transform_cur, xyzi) -> np.ndarray:
+    """TransformToEnd (FA:1414-1490) of float4 rows on the host side of the library."""
+    tc = np.ascontiguousarray(transform_cur, np.float32).reshape(6)
+    a = np.ascontiguousarray(xyzi, np.float32).reshape(-1, 4)
+    out = np.empty_like(a)
+    rc = lib().llsr_transform_to_end(tc.ctypes.data, a.ctypes.data, len(a), out.ctypes.data)
+    if rc != 0:
+        raise LlsrError(f"llsr_transform_to_end: {rc}")
     return out
 
 

@@ -41,12 +41,13 @@ for n in range(6):  # 2 warm-up batches, then one of each frame
     torch.cuda.synchronize()
     if n < 2:
         continue
+    prof = np.zeros((B, 8), np.float32)
+    pipe.debug_s2s_prof(prof)
     for b in list(range(0, B, max(1, B // 64))) + [1, 3]:
         f = pipe.odometry_fetch(b)
-        t = f["lm"]["transform_cur"] / 100.0  # 100 MHz ticks -> us
-        rows.append(list(t[:6]) + [f["lm"]["ms"] / 100.0, f["lm"]["surf_iterations"], f["lm"]["corner_iterations"],
-                                   f["lm"]["n_surf_corr"], f["lm"]["n_corner_corr"],
-                                   int(f["lm"]["degenerate"]) >> 1])  # the diagnostics build's fallback count
+        t = prof[b] / 100.0  # 100 MHz ticks -> us (problem b of the launch = slot b)
+        rows.append(list(t[:7]) + [f["lm"]["surf_iterations"], f["lm"]["corner_iterations"],
+                                   f["lm"]["n_surf_corr"], f["lm"]["n_corner_corr"], float(prof[b, 7])])
         per.setdefault((n, b % 2), []).append(rows[-1])
 r = np.array(rows)
 print(json.dumps({"lidar": lidar, "B": B,

@@ -8,12 +8,22 @@
 //   node <lidar> <in.bin> <out.bin>  (GPU): llsr_ros2::Projection on one scan (float4 rows), then
 //                    the marshalled CloudInfo arrays and feature clouds written for the test to
 //                    compare with the ctypes pipeline's outputs
+//   drive <lidar> <frames.bin> <map.bin> <out.bin>  (GPU): the reference's thread layout
+//                    (main.cpp:10-11): an IP thread (Projection::run + handoff, blocking one-slot
+//                    send), an FA thread (Odometry::step on its own handle: updateTransformation,
+//                    integrateTransformation, publishCloudsLast) and an MO thread
+//                    (scan2map_optimization on a third handle, non-blocking send as
+//                    association_out_channel(false)); every frame's features, poses and clouds
+//                    written for the test to compare with the oracle
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <condition_variable>
 #include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../integration/ros2/llsr_ros2.hpp"
@@ -37,10 +47,45 @@ struct CloudInfo {  // cloud_msgs/msg/CloudInfo.msg
   std::vector<uint32_t> segmented_cloud_col_ind;
   std::vector<float> segmented_cloud_range;
 };
-struct ProjectionOut {  // utility.h:63-72
+struct ProjectionOut {  // utility.h:63-72, with the member INTEGRATION.md §2 adds
   std::shared_ptr<Cloud> segmented_cloud, outlier_cloud;
   CloudInfo seg_msg;
   std::vector<double> outlierCloud_Intensity, segmentedCloud_Intensity;
+  llsr_ros2::FeatureClouds<Cloud> features;
+};
+struct AssociationOut {  // utility.h:75-83 (the odometry message left out: not compared here)
+  Header header;
+  std::shared_ptr<Cloud> cloud_corner_last, cloud_surf_last, cloud_corner_scan, cloud_surf_scan;
+  float transform_sum[6];
+};
+
+// One writer, one reader, one slot: send waits for an empty slot when blocking and otherwise
+// overwrites; receive waits for an item and empties the slot (the semantics of channel.h:24-54).
+template <class T>
+class Channel {
+ public:
+  explicit Channel(bool blocking_send) : blocking_(blocking_send) {}
+  void send(T&& v) {
+    std::unique_lock<std::mutex> lk(m_);
+    if (blocking_) cv_.wait(lk, [this] { return !full_; });
+    slot_ = std::move(v);
+    full_ = true;
+    cv_.notify_all();
+  }
+  void receive(T& v) {
+    std::unique_lock<std::mutex> lk(m_);
+    cv_.wait(lk, [this] { return full_; });
+    v = std::move(slot_);
+    full_ = false;
+    cv_.notify_all();
+  }
+
+ private:
+  bool blocking_;
+  bool full_ = false;
+  T slot_;
+  std::mutex m_;
+  std::condition_variable cv_;
 };
 }  // namespace mock
 
@@ -173,11 +218,195 @@ static int node(int lidar, const char* in, const char* out) {
 }
 #endif
 
+#ifdef LLSR_ADAPTER_NODE
+static bool read_cloud(FILE* f, mock::Cloud& c) {
+  int32_t n = 0;
+  if (fread(&n, 4, 1, f) != 1 || n < 0) return false;
+  std::vector<float> rows(4 * (size_t)n);
+  if (n && fread(rows.data(), 4, rows.size(), f) != rows.size()) return false;
+  llsr_ros2::unpack_xyzi(rows.data(), n, c);
+  return true;
+}
+
+static void put_cloud(FILE* g, const mock::Cloud& c) {
+  const int32_t n = (int32_t)c.points.size();
+  fwrite(&n, 4, 1, g);
+  for (const auto& p : c.points) {
+    const float r[4] = {p.x, p.y, p.z, p.intensity};
+    fwrite(r, 4, 4, g);
+  }
+}
+
+// per FA frame: what FA received and what Odometry::step left
+struct FaRecord {
+  int32_t seq = -1, lm = 0;
+  mock::Cloud sharp, less_sharp, flat, less_flat;
+  float tcur[6], tsum[6];
+  int32_t degenerate = 0;
+  llsr_s2s_report rep = llsr_s2s_report();
+  mock::Cloud corner_last, surf_last, corner_scan, surf_scan;
+};
+struct MoRecord {
+  int32_t seq = -1;
+  float pose[6];
+  llsr_lm_report rep;
+};
+
+static int drive(int lidar, const char* frames_path, const char* map_path, const char* out) {
+  FILE* f = fopen(frames_path, "rb");
+  if (!f) return 2;
+  int32_t F = 0;
+  if (fread(&F, 4, 1, f) != 1 || F < 1) return 2;
+  std::vector<mock::Cloud> frames((size_t)F);
+  for (auto& c : frames)
+    if (!read_cloud(f, c)) return 2;
+  fclose(f);
+  mock::Cloud corner_map, surf_map;
+  float pose0[6];
+  FILE* m = fopen(map_path, "rb");
+  if (!m || !read_cloud(m, corner_map) || !read_cloud(m, surf_map) || fread(pose0, 4, 6, m) != 6) return 2;
+  fclose(m);
+
+  mock::Channel<mock::ProjectionOut> ip_to_fa(true);    // projection_out_channel(true)
+  mock::Channel<mock::AssociationOut> fa_to_mo(false);  // association_out_channel(false)
+  std::vector<FaRecord> fa_rec;
+  std::vector<MoRecord> mo_rec;
+  std::string err;
+  std::mutex err_m;
+  auto guard = [&](const char* who, const std::exception& e) {
+    std::lock_guard<std::mutex> lk(err_m);
+    err += std::string(who) + ": " + e.what() + "\n";
+  };
+
+  std::thread ip([&] {  // ImageProjection::cloudHandler per message, then publishClouds' send
+    try {
+      llsr_ros2::Projection proj(lidar, 0);
+      for (int32_t k = 0; k <= F; ++k) {
+        mock::ProjectionOut po;
+        po.seg_msg.header.sec = k < F ? k : -1;  // -1: end of the drive
+        if (k < F) {
+          proj.run(frames[(size_t)k]);
+          po.segmented_cloud = std::make_shared<mock::Cloud>();
+          po.outlier_cloud = std::make_shared<mock::Cloud>();
+          proj.handoff(po);
+          po.seg_msg.header.sec = k;
+        }
+        ip_to_fa.send(std::move(po));
+      }
+    } catch (const std::exception& e) {
+      guard("ip", e);
+      mock::ProjectionOut end;
+      end.seg_msg.header.sec = -1;
+      ip_to_fa.send(std::move(end));
+    }
+  });
+  std::thread fa([&] {  // runFeatureAssociation's loop (FA:2742-2853) on its own handle
+    bool dead = false;
+    try {
+      llsr_ros2::Odometry<mock::Cloud> odo(lidar, 0);
+      while (true) {
+        mock::ProjectionOut po;
+        ip_to_fa.receive(po);
+        if (po.seg_msg.header.sec < 0) break;
+        if (dead) continue;
+        FaRecord r;
+        r.seq = po.seg_msg.header.sec;
+        r.sharp = po.features.corner_sharp;
+        r.less_sharp = po.features.corner_less_sharp;
+        r.flat = po.features.surf_flat;
+        r.less_flat = po.features.surf_less_flat;
+        r.lm = odo.step(po.features) ? 1 : 0;
+        for (int i = 0; i < 6; ++i) {
+          r.tcur[i] = odo.transform_cur[i];
+          r.tsum[i] = odo.transform_sum[i];
+        }
+        r.degenerate = odo.is_degenerate ? 1 : 0;
+        r.rep = odo.report;
+        r.corner_last = odo.corner_last;
+        r.surf_last = odo.surf_last;
+        if (r.lm) {
+          r.corner_scan = odo.corner_scan;
+          r.surf_scan = odo.surf_scan;
+          mock::AssociationOut ao;  // _output_channel.send (FA:2822-2852), mapping_frequency_divider 1
+          ao.header.sec = r.seq;
+          ao.cloud_corner_last = std::make_shared<mock::Cloud>(odo.corner_last);
+          ao.cloud_surf_last = std::make_shared<mock::Cloud>(odo.surf_last);
+          ao.cloud_corner_scan = std::make_shared<mock::Cloud>(odo.corner_scan);
+          ao.cloud_surf_scan = std::make_shared<mock::Cloud>(odo.surf_scan);
+          for (int i = 0; i < 6; ++i) ao.transform_sum[i] = odo.transform_sum[i];
+          fa_to_mo.send(std::move(ao));
+        }
+        fa_rec.push_back(std::move(r));
+      }
+    } catch (const std::exception& e) {
+      guard("fa", e);
+      dead = true;
+      mock::ProjectionOut po;  // drain so that IP's blocking send returns
+      do ip_to_fa.receive(po); while (po.seg_msg.header.sec >= 0);
+    }
+    mock::AssociationOut end;
+    end.header.sec = -1;
+    fa_to_mo.send(std::move(end));
+  });
+  std::thread mo([&] {  // MapOptimization's loop: scan2MapOptimization on a third handle
+    try {
+      llsr_ros2::Handle h(lidar, 0, LLSR_MODE_LM_APPLIED);
+      while (true) {
+        mock::AssociationOut ao;
+        fa_to_mo.receive(ao);
+        if (ao.header.sec < 0) break;
+        MoRecord r;
+        r.seq = ao.header.sec;
+        for (int i = 0; i < 6; ++i) r.pose[i] = pose0[i];
+        r.rep = llsr_ros2::scan2map_optimization(h.get(), *ao.cloud_corner_scan, *ao.cloud_surf_scan, corner_map,
+                                                 surf_map, r.pose);
+        mo_rec.push_back(r);
+      }
+    } catch (const std::exception& e) {
+      guard("mo", e);
+      mock::AssociationOut ao;
+      do fa_to_mo.receive(ao); while (ao.header.sec >= 0);
+    }
+  });
+  ip.join();
+  fa.join();
+  mo.join();
+  if (!err.empty()) {
+    fprintf(stderr, "%s", err.c_str());
+    return 1;
+  }
+  FILE* g = fopen(out, "wb");
+  if (!g) return 2;
+  const int32_t nf = (int32_t)fa_rec.size(), nm = (int32_t)mo_rec.size();
+  fwrite(&nf, 4, 1, g);
+  for (const auto& r : fa_rec) {
+    const int32_t hdr[9] = {r.seq, r.lm, r.degenerate, r.rep.surf_iterations, r.rep.corner_iterations,
+                            r.rep.n_surf_corr, r.rep.n_corner_corr, r.rep.degenerate, r.rep.skipped};
+    fwrite(hdr, 4, 9, g);
+    fwrite(r.tcur, 4, 6, g);
+    fwrite(r.tsum, 4, 6, g);
+    for (const mock::Cloud* c : {&r.sharp, &r.less_sharp, &r.flat, &r.less_flat, &r.corner_last, &r.surf_last,
+                                 &r.corner_scan, &r.surf_scan})
+      put_cloud(g, *c);
+  }
+  fwrite(&nm, 4, 1, g);
+  for (const auto& r : mo_rec) {
+    fwrite(&r.seq, 4, 1, g);
+    fwrite(r.pose, 4, 6, g);
+    fwrite(&r.rep.iterations, 4, 1, g);
+  }
+  fclose(g);
+  return 0;
+}
+#endif
+
 int main(int argc, char** argv) {
   if (argc >= 2 && !strcmp(argv[1], "marshal")) return marshal();
 #ifdef LLSR_ADAPTER_NODE
   if (argc >= 5 && !strcmp(argv[1], "node")) return node(atoi(argv[2]), argv[3], argv[4]);
+  if (argc >= 6 && !strcmp(argv[1], "drive")) return drive(atoi(argv[2]), argv[3], argv[4], argv[5]);
 #endif
-  fprintf(stderr, "usage: %s marshal | node <lidar> <in.bin> <out.bin>\n", argv[0]);
+  fprintf(stderr, "usage: %s marshal | node <lidar> <in.bin> <out.bin> | drive <lidar> <frames.bin> <map.bin> <out.bin>\n",
+          argv[0]);
   return 2;
 }

@@ -75,3 +75,42 @@ def test_phantom_carry_bit_exact(require_gpu):
 def test_ransac_rng_decisive_bit_exact(require_gpu):
     fails = _sequence([synth.make_scan(7, ground_ramp=(2.0, 0.15)), synth.make_scan(8, ground_ramp=(3.0, 0.2))])
     assert not fails, "\n".join(fails)
+
+
+def _voxel_rank_cases(rng):
+    """Rank sequences like a ring's voxel ranks (runs of equal ranks along a piecewise-monotone
+    sweep) plus tie-heavy random ones, at the sizes around the one-wave / block thresholds, and the
+    median-of-3 killer (heap-sort fallback)."""
+    cases = []
+    for n in (0, 1, 2, 16, 17, 64, 65, 100, 200, 420, 511, 512, 513, 700, 1024, 1500, 2048):
+        for levels in (1, 3, 50, 1000):
+            cases.append(rng.integers(0, levels, n).astype(np.uint32))
+        if n > 2:  # a sweep: ranks rise, fall and rise again in runs of 1-6 equal values
+            runs = rng.integers(1, 7, n)
+            seq = np.repeat(np.arange(len(runs)), runs)[:n]
+            turn = n // 3
+            seq = np.concatenate([seq[:turn], seq[turn:2 * turn][::-1], seq[2 * turn:]])
+            cases.append(seq.astype(np.uint32))
+    k = 1024
+    killer = np.empty(2 * k, np.uint32)
+    for i in range(k):
+        killer[i] = (i + 1) if i % 2 == 0 else (k + i + 1)
+        killer[k + i] = 2 * (i + 1)
+    cases += [killer, killer // 3, killer[:512], killer[:512] // 5]
+    return cases
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["block", "wave"])
+def test_device_exact_sort32_matches_std_sort(require_gpu, mode):
+    """The PCL-order VoxelGrid's 32-bit-key sorts (VoxLess32: rank << 11 | position) against
+    libstdc++'s std::sort: k_vox_pcl's block_introsort (mode 0) and k_vox_pcl_w's wave_introsort
+    (mode 1), including the heap-sort fallback and chains of lopsided partitions."""
+    f = lib().llsr_debug_exact_sort32
+    f.restype, f.argtypes = C.c_int32, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]
+    bad = []
+    for j, v in enumerate(_voxel_rank_cases(np.random.default_rng(12))):
+        out = np.zeros(len(v), np.int32)
+        assert f(v.ctypes.data, len(v), mode, out.ctypes.data) == 0
+        if not np.array_equal(out, oracle_py.std_sort_by_value(v.astype(np.float32))):
+            bad.append((j, len(v)))
+    assert not bad, f"cases {bad} differ from std::sort"
