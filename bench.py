@@ -999,11 +999,8 @@ def main():
     def traffic_of(kname):
         if kname == "k_project" and fused:
             kname = "k_project_fused"  # the VLP-16 launch's own name in the PMC record
-        recs = [tjson.get("kernels", {}).get(kname)]
-        if kname == "k_vox_pcl":  # the library's k_vox_pcl timer covers both launches (k_vox_pcl_w first)
-            recs.append(tjson.get("kernels", {}).get("k_vox_pcl_w"))
-        recs = [r for r in recs if r]
-        return sum(r["hbm_bytes"] for r in recs) / tjson["batch"] * B if recs and tjson.get("batch") else None
+        rec = tjson.get("kernels", {}).get(kname)
+        return rec["hbm_bytes"] / tjson["batch"] * B if rec and tjson.get("batch") else None
 
     def roofline(kname, nbytes=None, ms=None, traffic=None, note=None):
         nbytes = per[kname] if nbytes is None else nbytes

@@ -33,9 +33,8 @@ __global__ void k_segment(DevCfg, const float4*, const int64_t*, DevBufs);
 __global__ void k_fa_points(DevCfg, DevBufs);
 __global__ void k_select_ring(DevCfg, DevBufs);
 __global__ void k_vox_pcl(DevCfg, DevBufs);
-__global__ void k_vox_pcl_w(DevCfg, DevBufs);
 __global__ void k_debug_exact_sort(const float*, int, int*, long long*);
-__global__ void k_debug_exact_sort32(const uint32_t*, int, int, int*);
+__global__ void k_debug_exact_sort32(const uint32_t*, int, int*);
 __global__ void k_fa_concat(DevCfg, DevBufs);
 __global__ void k_dbscan_adj(DevCfg, DevBufs);
 __global__ void k_vis_clouds(DevCfg, DevBufs, int, float4*, int*);
@@ -176,10 +175,8 @@ static int label_lds(const DevCfg& c) { return c.HW * (int)(sizeof(int) + 1); }
 static int label_band_lds(const DevCfg& c) { return c.lbl_band * c.W * (int)sizeof(int); }
 static bool use_fused(const llsr_handle* h) { return h->dc.ccl_lds != 0; }
 
-// the PCL-order less-flat VoxelGrid of every pending ring: one wave per small ring, then a
-// workgroup per large one (each kernel skips the other's rings)
+// the PCL-order less-flat VoxelGrid of every pending ring
 static void launch_vox_pcl(const DevCfg& c, const DevBufs& d, int B, hipStream_t s) {
-  k_vox_pcl_w<<<dim3((c.H + kVoxRings - 1) / kVoxRings, B), 64 * kVoxRings, 0, s>>>(c, d);
   k_vox_pcl<<<dim3(c.H, B), 256, 0, s>>>(c, d);
 }
 
@@ -630,11 +627,11 @@ extern "C" int32_t llsr_debug_exact_sort(const float* vals, int32_t n, int32_t* 
 }
 
 // Diagnostics (not part of the ABI header): the PCL-order VoxelGrid's exact sort of 32-bit keys
-// (VoxLess32: voxel rank << 11 | position) on n <= 2048 host ranks < 2^21, by the workgroup
-// (mode 0, k_vox_pcl's block_introsort) or one wave (mode 1, k_vox_pcl_w's wave_introsort); out[k] =
-// the input position at sorted position k. For tests/test_gpu_features_ties.py.
-extern "C" int32_t llsr_debug_exact_sort32(const uint32_t* ranks, int32_t n, int32_t mode, int32_t* out) {
-  if (!ranks || !out || n < 0 || n > 2048 || mode < 0 || mode > 1) return LLSR_EINVAL;
+// (VoxLess32: voxel rank << 11 | position) on n <= 2048 host ranks < 2^21, as k_vox_pcl runs it
+// (block_introsort); out[k] = the input position at sorted position k. For
+// tests/test_gpu_features_ties.py.
+extern "C" int32_t llsr_debug_exact_sort32(const uint32_t* ranks, int32_t n, int32_t* out) {
+  if (!ranks || !out || n < 0 || n > 2048) return LLSR_EINVAL;
   for (int32_t t = 0; t < n; ++t)
     if (ranks[t] >= (1u << 21)) return LLSR_EINVAL;
   if (n == 0) return LLSR_OK;
@@ -645,7 +642,7 @@ extern "C" int32_t llsr_debug_exact_sort32(const uint32_t* ranks, int32_t n, int
   int32_t rc = LLSR_OK;
   if (hipMemcpy(dv, ranks, sizeof(uint32_t) * n, hipMemcpyHostToDevice) != hipSuccess) rc = LLSR_EIO;
   if (rc == LLSR_OK) {
-    k_debug_exact_sort32<<<1, 256>>>(dv, n, mode, di);
+    k_debug_exact_sort32<<<1, 256>>>(dv, n, di);
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
         hipMemcpy(out, di, sizeof(int) * n, hipMemcpyDeviceToHost) != hipSuccess)
       rc = LLSR_EIO;

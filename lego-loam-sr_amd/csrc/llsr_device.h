@@ -87,10 +87,6 @@ struct DevBufs {
 
 // DBSCAN adjacency capacity per scan (edge candidates); larger M falls back to on-the-fly rows.
 constexpr int kAdjCap = 2048;
-// the PCL-order less-flat VoxelGrid: rings of at most kVoxWave candidates are sorted by one wave
-// each (k_vox_pcl_w, kVoxRings rings per workgroup), larger ones by a 256-thread workgroup (k_vox_pcl)
-constexpr int kVoxWave = 512;
-constexpr int kVoxRings = 1;
 constexpr int kAdjWords = kAdjCap / 32;
 
 // fullCloud's intensity of cell (row i, col j): (float)(i + j / 10000.0) (IP:341); the double

@@ -334,22 +334,15 @@ __global__ __launch_bounds__(256) void k_debug_exact_sort(const float* vals, int
   for (int t = threadIdx.x; t < n; t += 256) out[t] = (int)(uint32_t)key[t];
 }
 
-// Diagnostics (llsr_debug_exact_sort32): the PCL-order VoxelGrid's sorts on 32-bit keys
-// (rank << 11 | position, VoxLess32) of n <= kRingMax ranks < 2^21: mode 0 block_introsort (256
-// threads, k_vox_pcl), mode 1 wave_introsort (one wave, k_vox_pcl_w); out receives the original
-// positions in sorted order.
-__global__ __launch_bounds__(256) void k_debug_exact_sort32(const uint32_t* ranks, int n, int mode, int* out) {
+// Diagnostics (llsr_debug_exact_sort32): the PCL-order VoxelGrid's sort on 32-bit keys (rank << 11 |
+// position, VoxLess32) of n <= kRingMax ranks < 2^21, as k_vox_pcl runs it (block_introsort, 256
+// threads); out receives the original positions in sorted order.
+__global__ __launch_bounds__(256) void k_debug_exact_sort32(const uint32_t* ranks, int n, int* out) {
   __shared__ uint32_t key[kRingMax];
   __shared__ uint16_t Lp[kRingMax], Rp[kRingMax];
   __shared__ BlockSortLds bsl;
-  __shared__ int stk[48];
   for (int t = threadIdx.x; t < n; t += 256) key[t] = (ranks[t] << 11) | (uint32_t)t;
-  __syncthreads();
-  if (mode == 0) {
-    block_introsort<256>(key, n, Lp, Rp, bsl, VoxLess32{});
-  } else if (threadIdx.x < 64) {
-    wave_introsort<uint32_t, VoxLess32, 48>(key, n, Lp, Rp, stk, VoxLess32{});
-  }
+  block_introsort<256>(key, n, Lp, Rp, bsl, VoxLess32{});
   __syncthreads();
   for (int t = threadIdx.x; t < n; t += 256) out[t] = (int)(key[t] & 0x7ffu);
 }
@@ -875,7 +868,6 @@ __global__ __launch_bounds__(256, 8) void k_vox_pcl(DevCfg c, DevBufs d) {
   const int r = rc[2 * H + i];
   if (r >= 0) return;  // no candidates, or written by k_select_ring (input order / oversized grid)
   const int L = -1 - r;
-  if (L <= kVoxWave) return;  // k_vox_pcl_w's ring
   const int tid = threadIdx.x, nt = blockDim.x;
   const int sp = d.start_ring[b * H + i];
   const size_t base = (size_t)b * c.HW;
@@ -928,67 +920,6 @@ __global__ __launch_bounds__(256, 8) void k_vox_pcl(DevCfg c, DevBufs d) {
     out[vo] = make_float4(sx / nn, sy / nn, sz / nn, si / nn);
   }
   if (tid == 0) rc[2 * H + i] = V;
-}
-
-// ---------------------------------------------------------------------------------------------
-// K8c the same PCL-order VoxelGrid for the rings of at most kVoxWave candidates (nearly every VLP-16
-// ring once FA's never-cleared cloudLabel state has built up, FA:167-198): one wave per ring with
-// its own 4.3 KB of LDS (wave_introsort). In k_vox_pcl such a ring is a single range below the
-// block-wide threshold, so one of its four waves sorted it while the other three waited; here
-// every wave slot of the CU holds a ring. The result is the same std::sort order (sub-ranges are
-// independent, and each range is partitioned exactly as libstdc++ does). grid (H / kVoxRings, B),
-// block 64 * kVoxRings; launched before k_vox_pcl, which skips these rings.
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64 * kVoxRings, 8) void k_vox_pcl_w(DevCfg c, DevBufs d) {
-  constexpr int kStk = 24;  // >= 2 lg(kVoxWave) + 1
-  __shared__ uint32_t keyS[kVoxRings][kVoxWave];
-  __shared__ uint16_t LpS[kVoxRings][kVoxWave], RpS[kVoxRings][kVoxWave];
-  __shared__ int stkS[kVoxRings][kStk];
-  const int w = threadIdx.x >> 6, ln = lane_id();
-  const int i = blockIdx.x * kVoxRings + w, b = blockIdx.y, H = c.H;
-  if (i >= H) return;  // no workgroup barrier below: each wave is independent
-  int* rc = d.ring_cnt + (size_t)b * 3 * H;
-  const int r = rc[2 * H + i];
-  if (r >= 0) return;
-  const int L = -1 - r;
-  if (L > kVoxWave) return;  // k_vox_pcl's ring
-  uint32_t* key = keyS[w];
-  uint16_t* Lp = LpS[w];
-  uint16_t* Rp = RpS[w];
-  const int sp = d.start_ring[b * H + i];
-  const size_t base = (size_t)b * c.HW;
-  const uint32_t* gk = reinterpret_cast<const uint32_t*>(d.ccl_a + base) + sp;
-  const uint16_t* gc = reinterpret_cast<const uint16_t*>(d.ccl_b + base) + sp;
-  for (int t = ln; t < L; t += 64) key[t] = gk[t];
-  wave_introsort<uint32_t, VoxLess32, kStk>(key, L, Lp, Rp, stkS[w], VoxLess32{});
-  uint16_t* cpos = Lp;  // the sort's scratch is free again
-  for (int t = ln; t < L; t += 64) cpos[t] = gc[t];
-  wave_sync_lds();
-  const float4* lp = d.loam + base + sp;
-  float4* out = d.lflat_tmp + base + sp;
-  const unsigned long long ltm = (1ull << ln) - 1ull;
-  // voxel heads in sorted order, 64 positions per step; a head's centroid sums its voxel's points
-  // in sorted order and goes to the voxel's rank among the heads (as k_vox_pcl)
-  int V = 0;
-  for (int t0 = 0; t0 < L; t0 += 64) {
-    const int t = t0 + ln;
-    const uint32_t kt = t < L ? key[t] : 0u;
-    const bool head = t < L && (t == 0 || (kt >> 11) != (key[t - 1] >> 11));
-    const unsigned long long mH = __ballot(head);
-    if (head) {
-      const uint32_t vr = kt >> 11;
-      float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
-      int e = t;
-      for (; e < L && (key[e] >> 11) == vr; ++e) {
-        const float4 p = lp[cpos[key[e] & 0x7ffu]];
-        sx += p.x; sy += p.y; sz += p.z; si += p.w;
-      }
-      const float nn = (float)(e - t);
-      out[V + (int)__popcll(mH & ltm)] = make_float4(sx / nn, sy / nn, sz / nn, si / nn);
-    }
-    V += (int)__popcll(mH);
-  }
-  if (ln == 0) rc[2 * H + i] = V;
 }
 
 // ---------------------------------------------------------------------------------------------

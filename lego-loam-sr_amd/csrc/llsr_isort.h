@@ -180,8 +180,8 @@ __device__ void reg_heap_sort(K& v, int f, int e, Lt lt) {
 // reads. A segment of at most 16 elements is a leaf; one above 16 whose depth limit is spent is
 // heap-sorted in registers (rare), one segment at a time.
 template <class K, class Lt>
-__device__ __forceinline__ void seg_small_sort_body(K* key, uint16_t* Lp, uint16_t* Rp, int f, int n,
-                                                    unsigned long long bnd, int dep, Lt lt) {
+__device__ void seg_small_sort(K* key, uint16_t* Lp, uint16_t* Rp, int f, int n, unsigned long long bnd,
+                               int dep, Lt lt) {
   const int l = lane_id();
   const unsigned long long ltm = (1ull << l) - 1ull;
   const unsigned long long lem = l == 63 ? ~0ull : (2ull << l) - 1ull;  // bits <= l
@@ -291,12 +291,6 @@ __device__ __forceinline__ void seg_small_sort_body(K* key, uint16_t* Lp, uint16
   wave_sync_lds();
   if (l < n) key[f + s0 + rank] = v;
   wave_sync_lds();
-}
-// the same as an out-of-line function (the block sorts call it from several places)
-template <class K, class Lt>
-__device__ void seg_small_sort(K* key, uint16_t* Lp, uint16_t* Rp, int f, int n, unsigned long long bnd,
-                               int dep, Lt lt) {
-  seg_small_sort_body(key, Lp, Rp, f, n, bnd, dep, lt);
 }
 // one range key[f, f + n), n <= 64, with depth limit d
 template <class K, class Lt>
@@ -765,74 +759,6 @@ __device__ __forceinline__ void block_introsort(K* key, int n, uint16_t* Lp, uin
   if (prof && l == 0) {
     prof[1 + 4 * w] = tpw; prof[2 + 4 * w] = tsm; prof[3 + 4 * w] = thp; prof[4 + 4 * w] = clock64() - tend;
   }
-}
-
-// ---- one wave on one array, with the windows of small ranges ---------------------------------
-// The same std::sort as exact_introsort for key[0, n), n <= 4095, by one wave that owns its LDS
-// (k_vox_pcl_w: one ring per wave, so no wave of a workgroup waits on another's chain): left part
-// first, the right part on the wave's stack `stk` (kStack entries: >= the depth limit 2 lg n + 1),
-// every range of at most 64 elements collected with the consecutive ones into a window of <= 64
-// lanes finished by seg_small_sort (as block_introsort's waves do), a range above 64 with no depth
-// left by wave_heap_sort.
-template <class K, class Lt, int kStack>
-__device__ void wave_introsort(K* key, int n, uint16_t* Lp, uint16_t* Rp, int* stk, Lt lt) {
-  const int l = lane_id();
-  wave_sync_lds();  // key[0, n) written by the wave
-  if (n <= 1) return;
-  const int lg = 31 - __clz(n);
-  // the small sorts inlined: the whole sort then addresses LDS directly (no generic pointers
-  // crossing a call)
-  if (n <= 64) {
-    seg_small_sort_body(key, Lp, Rp, 0, n, 1ull, 2 * lg, lt);
-    return;
-  }
-  auto enc = [](int f, int e, int d) { return f | (e << 12) | (d << 24); };
-  int wf = 0, wn = 0, wdep = 0;
-  unsigned long long wb = 0ull;
-  auto flush = [&]() {
-    if (wn > 1) seg_small_sort_body(key, Lp, Rp, wf, wn, wb, wdep, lt);
-    wn = 0;
-  };
-  auto emit = [&](int rf, int rl, int rd) {
-    const int len = rl - rf;
-    if (len <= 0) return;
-    if (wn > 0 && rf == wf + wn && wn + len <= 64) {
-      wb |= 1ull << wn;
-      if (l == wn) wdep = rd;
-      wn += len;
-    } else {
-      flush();
-      wf = rf;
-      wn = len;
-      wb = 1ull;
-      if (l == 0) wdep = rd;
-    }
-  };
-  int rf = 0, rl = n, rd = 2 * lg, sp = 0;
-  while (true) {
-    while (rl - rf > 64 && rd > 0) {
-      rd--;
-      const int cut = wave_partition(key, Lp, Rp, rf, rl, lt);
-      if (sp >= kStack) __builtin_trap();  // cannot: <= one entry per level of the path
-      if (l == 0) stk[sp] = enc(cut, rl, rd);
-      ++sp;
-      rl = cut;
-    }
-    if (rl - rf > 64) {
-      flush();
-      wave_heap_sort(key, rf, rl, lt);  // depth limit spent: __partial_sort
-    } else {
-      emit(rf, rl, rd);
-    }
-    wave_sync_lds();
-    if (sp == 0) break;
-    --sp;
-    const int nx = stk[sp];
-    rf = nx & 0xfff;
-    rl = (nx >> 12) & 0xfff;
-    rd = (nx >> 24) & 0x3f;
-  }
-  flush();
 }
 
 }  // namespace llsr

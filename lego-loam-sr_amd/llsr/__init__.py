@@ -237,6 +237,16 @@ class Pipeline:
         f.restype, f.argtypes = C.c_float, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]
         return float(f(self._h, kernel, phase, reps))
 
+    def debug_s2s_prof(self, out: np.ndarray) -> int:
+        """Diagnostics build (libllsr_prof.so): the last scan-to-scan launch's per-problem phase ticks
+        into out (float32 [P, 8]); returns the number of problems copied."""
+        f = lib().llsr_debug_s2s_prof
+        f.restype, f.argtypes = C.c_int32, [C.c_void_p, C.c_void_p, C.c_int32]
+        n = f(self._h, out.ctypes.data, out.shape[0])
+        if n < 0:
+            raise LlsrError(f"llsr_debug_s2s_prof: {n}")
+        return n
+
     def kernel_times(self) -> dict:
         buf = np.zeros(32, dtype=np.float32)
         n = lib().llsr_kernel_times_ms(self._h, buf.ctypes.data, 32)

@@ -13,7 +13,7 @@ from collections import defaultdict
 
 path, W, K, P = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
 KERNELS = ("k_project_fused", "k_ground_add", "k_ground_elev_ransac", "k_label", "k_segment", "k_fa_points",
-           "k_select_ring", "k_vox_pcl_w", "k_vox_pcl", "k_fa_concat", "k_dbscan_adj", "k_dbscan_merge")
+           "k_select_ring", "k_vox_pcl", "k_fa_concat", "k_dbscan_adj", "k_dbscan_merge")
 runs = defaultdict(list)
 for row in csv.DictReader(open(path)):
     name = row["Kernel_Name"].split("(")[0].replace("void ", "").replace("llsr::", "").split("<")[0]
@@ -26,9 +26,4 @@ for name in KERNELS:
     out[name] = {"dispatches": len(d),
                  "avg_ms_all": round(sum(e - s for s, e in d) / max(1, len(d)) / 1e6, 4),
                  "avg_ms_profiling_pass": round(sum(e - s for s, e in sel) / max(1, len(sel)) / 1e6, 4)}
-# the library's k_vox_pcl timer spans both PCL-order VoxelGrid launches (one wave per small ring,
-# then a workgroup per large one)
-if "k_vox_pcl_w" in out:
-    out["k_vox_pcl_w+k_vox_pcl"] = {k: round(out["k_vox_pcl_w"][k] + out["k_vox_pcl"][k], 4)
-                                     for k in ("avg_ms_all", "avg_ms_profiling_pass")}
 print(json.dumps(out, indent=1))

@@ -100,17 +100,16 @@ def _voxel_rank_cases(rng):
     return cases
 
 
-@pytest.mark.parametrize("mode", [0, 1], ids=["block", "wave"])
-def test_device_exact_sort32_matches_std_sort(require_gpu, mode):
-    """The PCL-order VoxelGrid's 32-bit-key sorts (VoxLess32: rank << 11 | position) against
-    libstdc++'s std::sort: k_vox_pcl's block_introsort (mode 0) and k_vox_pcl_w's wave_introsort
-    (mode 1), including the heap-sort fallback and chains of lopsided partitions."""
+def test_device_exact_sort32_matches_std_sort(require_gpu):
+    """The PCL-order VoxelGrid's 32-bit-key sort (VoxLess32: rank << 11 | position) as k_vox_pcl runs
+    it (block_introsort) against libstdc++'s std::sort, including the heap-sort fallback and chains
+    of lopsided partitions."""
     f = lib().llsr_debug_exact_sort32
-    f.restype, f.argtypes = C.c_int32, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]
+    f.restype, f.argtypes = C.c_int32, [C.c_void_p, C.c_int32, C.c_void_p]
     bad = []
     for j, v in enumerate(_voxel_rank_cases(np.random.default_rng(12))):
         out = np.zeros(len(v), np.int32)
-        assert f(v.ctypes.data, len(v), mode, out.ctypes.data) == 0
+        assert f(v.ctypes.data, len(v), out.ctypes.data) == 0
         if not np.array_equal(out, oracle_py.std_sort_by_value(v.astype(np.float32))):
             bad.append((j, len(v)))
     assert not bad, f"cases {bad} differ from std::sort"
