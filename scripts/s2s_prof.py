@@ -54,6 +54,10 @@ print(json.dumps({"lidar": lidar, "B": B,
                   "us_per_problem": dict(zip(["knn_surf", "knn_corner", "A_rows", "B_sums", "C_solve",
                                               "walks_corner", "walks_surf"], r[:, :7].mean(0).round(1).tolist())),
                   "iterations": dict(zip(["surf", "corner"], r[:, 7:9].mean(0).round(1).tolist())),
+                  "slowest_problem": {"us": dict(zip(["knn_surf", "knn_corner", "A_rows", "B_sums", "C_solve",
+                                                      "walks_corner", "walks_surf"],
+                                                     r[r[:, :7].sum(1).argmax(), :7].round(1).tolist())),
+                                      "iterations": r[r[:, :7].sum(1).argmax(), 7:9].tolist()},
                   "correspondences": dict(zip(["surf", "corner"], r[:, 9:11].mean(0).round(1).tolist())),
                   "per_frame_sequence": {f"frame {k[0]} seq {k[1]}": {
                       "us": dict(zip(["knn_surf", "knn_corner", "A_rows", "B_sums", "C_solve", "walks_corner", "walks_surf"],
