@@ -851,7 +851,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=1024, help="scans per GPU per step")
+    ap.add_argument("--batch", type=int, default=2048, help="scans per GPU per step")
     ap.add_argument("--distinct", type=int, default=16, help="distinct synthetic scans per rank")
     ap.add_argument("--streams", type=int, default=3,
                     help="handles/HIP streams used round-robin, so consecutive batches overlap")
