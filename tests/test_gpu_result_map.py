@@ -54,6 +54,27 @@ def test_scan2map_on_recorded_map(require_gpu, z, probs, mode):
     assert not errs, "\n".join(errs)
 
 
+@pytest.mark.parametrize("mode", [_abi.LLSR_MODE_LM_APPLIED, _abi.LLSR_MODE_FAITHFUL])
+def test_scan2map_on_recorded_map_vs_reference_kdtree(require_gpu, probs, mode):
+    """The HIP scan-to-map against the MO restatement running over the REFERENCE's own nanoflann
+    kd-tree (oracle/_ref, compiled from the reference's nanoflann.hpp; it travels to the GPU box
+    prebuilt) on the recorded real-sensor map: every recorded problem bit-exact, so on this geometry
+    the device's cell-grid kNN-5 (ties by index) and nanoflann's (ties in tree order) agree."""
+    if oracle_py.ref_lib() is None:
+        pytest.skip("oracle/_ref/libref_mo.so not built")
+    cfg = _cfg(mode)
+    pipe = Pipeline(cfg)
+    errs = []
+    use = probs if mode == _abi.LLSR_MODE_LM_APPLIED else probs[:2]
+    for k, (cq, sq, cm, sm, p0, _) in enumerate(use):
+        g = pipe.scan2map(cq, sq, cm, sm, p0)
+        o = oracle_py.scan2map(cfg, cq, sq, cm, sm, p0, knn="kdtree")
+        errs += [f"problem {k}: {key} {g[key]} vs {o[key]}" for key in KEYS
+                 if not np.array_equal(np.asarray(g[key]), np.asarray(o[key]))]
+    pipe.close()
+    assert not errs, "\n".join(errs)
+
+
 def test_scan2map_batch_on_recorded_map(require_gpu, probs):
     """The five recorded-map problems as one device batch (llsr_scan2map_batch), lm_applied."""
     import torch
