@@ -44,6 +44,7 @@ namespace {
 constexpr int kMaxShell = 2;  // grid shells searched before the exact block-wide scan (queries in sparse regions)
 constexpr int kFbMax = 256;       // queries per kNN iteration whose shells did not settle (block scan)
 constexpr int kIx = 5;            // ints per query in S2SArgs::idx
+constexpr int kWalkBudget = 200;  // per-lane surf walk steps before the whole-wave walk takes over
 
 // TransformToStart (FA:1389-1412)
 __device__ __forceinline__ float4 to_start(const float* t, float4 pi) {
@@ -269,12 +270,17 @@ __device__ __forceinline__ float box_lb(const float4& lo, const float4& hi, floa
 // same-ring / other-ring choice, when the nearest neighbour and hence the walk's range and classes
 // are unchanged; INFINITY otherwise): a block whose box is farther holds only points farther than a
 // point of the same class and range, so it cannot hold the argmin.
-__device__ void surf_finish(const float4* sl, const float4* box, const float4* box2, int Ns, int fwd, float4 sel,
-                            float dist_sqr, int nn, float nd, float w2, float w3, int& i1, int& i2, int& i3) {
+// budget: the most 8-point steps (a block visited or skipped, a superblock skipped) the two walks
+// may take; false when it ran out (i2 / i3 then meaningless: the caller walks that query again
+// another way), true with the result otherwise.
+__device__ bool surf_finish(const float4* sl, const float4* box, const float4* box2, int Ns, int fwd, float4 sel,
+                            float dist_sqr, int nn, float nd, float w2, float w3, int& i1, int& i2, int& i3,
+                            int budget = INT_MAX) {
   i1 = -1;
   i2 = -1;
   i3 = -1;
-  if (!(nd < dist_sqr)) return;
+  if (!(nd < dist_sqr)) return true;
+  int spent = 0;
   i1 = nn;
   const int cs = trunc_i32(sl[nn].w);
   float m2 = dist_sqr, m3 = dist_sqr;
@@ -305,6 +311,7 @@ __device__ void surf_finish(const float4* sl, const float4* box, const float4* b
   };
   for (; j < end && (j & 7) && !stop; ++j) up_visit(j, sl[j]);
   for (; j < end && !stop; j += kScan) {
+    if (++spent > budget) return false;
     if ((j & 63) == 0 && j + 64 <= end) {  // a whole superblock
       const float4 lo = box2[2 * (j >> 6)], hi = box2[2 * (j >> 6) + 1];
       if ((double)(int)hi.w <= (double)cs + 2.5 && box_lb(lo, hi, sel) >= bound_up(lo.w, hi.w)) {
@@ -338,6 +345,7 @@ __device__ void surf_finish(const float4* sl, const float4* box, const float4* b
   };
   for (; j >= 0 && (j & 7) != 7 && !stop; --j) down_visit(j, sl[j]);
   for (; j >= 0 && !stop; j -= kScan) {
+    if (++spent > budget) return false;
     if ((j & 63) == 63) {  // superblock [j - 63, j]
       const float4 lo = box2[2 * (j >> 6)], hi = box2[2 * (j >> 6) + 1];
       if ((double)(int)lo.w >= (double)cs - 2.5 && box_lb(lo, hi, sel) >= bound_dn(lo.w, hi.w)) {
@@ -356,6 +364,7 @@ __device__ void surf_finish(const float4* sl, const float4* box, const float4* b
   }
   i2 = b2;
   i3 = b3;
+  return true;
 }
 
 __device__ __forceinline__ float readlane_f(float v, int l) {
@@ -855,8 +864,9 @@ __global__ __launch_bounds__(kNT, 4) void k_s2s_lm(S2SArgs a) {
           if (surf) LLSR_STAMP(tAks);
           else LLSR_STAMP(tAkc);
           if constexpr (surf && kBig) {
-            // the whole wave walks each of its lanes' queries in turn (uniform trip count): for the
-            // long HDL-64E surf clouds, whose walks leave most lanes of a per-lane walk idle
+            // each lane walks its own query up to kWalkBudget 8-point steps; the whole wave then walks
+            // the queries that ran out, one at a time (HDL-64E: the shadow points' queries, whose
+            // ring band holds most of the cloud, would keep a per-lane walk's wave busy alone)
             for (int q0 = 0; q0 < Q; q0 += kThreads) {
               const int q = q0 + tid;
               const bool act = q < Q;
@@ -870,8 +880,14 @@ __global__ __launch_bounds__(kNT, 4) void k_s2s_lm(S2SArgs a) {
                 sel = to_start(tl, qry[q]);
                 walk_bounds(ix, sel, nn, w2, w3);
               }
-              int i1, i2, i3;
-              surf_finish_wave(sl, sbox2, F < Ns ? F : Ns, sel, a.dist_sqr, act, nn, nd, w2, w3, i1, i2, i3);
+              int i1 = -1, i2 = -1, i3 = -1;
+              bool done = true;
+              if (act) done = surf_finish(sl, sbox, sbox2, Ns, F, sel, a.dist_sqr, nn, nd, w2, w3, i1, i2, i3, kWalkBudget);
+              if (__ballot(!done)) {
+                int j1, j2, j3;
+                surf_finish_wave(sl, sbox2, F < Ns ? F : Ns, sel, a.dist_sqr, !done, nn, nd, w2, w3, j1, j2, j3);
+                if (!done) { i1 = j1; i2 = j2; i3 = j3; }
+              }
               if (act) { ix[0] = i1; ix[1] = i2; ix[2] = i3; }
             }
           } else {
