@@ -98,6 +98,21 @@ __device__ __forceinline__ float cell_intensity(int H, int W, int i, int j) {
 // ---- wave / block primitives (wave64) ------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// __ballot of a bool: HIP's __ballot takes an int, which the backend materialises per lane and
+// compares against zero again (two VALU instructions per ballot in the sort's partition loops)
+__device__ __forceinline__ unsigned long long ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
+// lanes 0 .. n-1 as a wave mask (n clamped to [0, 64]; uniform n: scalar instructions only)
+__device__ __forceinline__ unsigned long long lanes_below(int n) {
+  return n >= 64 ? ~0ull : n <= 0 ? 0ull : (1ull << n) - 1ull;
+}
+
+// set bits of m below this lane, __popcll(m & ((1ull << lane) - 1)), as two mbcnt instructions
+// (the and / popcount form costs four and keeps the lane mask in two registers)
+__device__ __forceinline__ int lane_rank(unsigned long long m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // Lane exchanges as VALU ops (ds_bpermute, what __shfl_* compile to, queues in the LDS pipe):
 // DPP row / quad permutations and gfx950's v_permlane16/32_swap.
 template <int J>

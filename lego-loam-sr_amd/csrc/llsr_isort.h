@@ -42,6 +42,24 @@ struct VoxLess {
 struct VoxLess32 {
   __device__ bool operator()(uint32_t a, uint32_t b) const { return (a >> 11) < (b >> 11); }
 };
+// `a < P` and `P < a` against one pivot P, as the partitions test every element of a range
+template <class K, class Lt>
+struct PivotTest {
+  K P;
+  Lt lt;
+  __device__ PivotTest(K p, Lt l) : P(p), lt(l) {}
+  __device__ bool below(K a) const { return lt(a, P); }
+  __device__ bool above(K a) const { return lt(P, a); }
+};
+// VoxLess32 reads the rank bits (>> 11) only: a < P iff a < (P & ~0x7ff), P < a iff a > (P | 0x7ff),
+// one compare of the whole key each
+template <>
+struct PivotTest<uint32_t, VoxLess32> {
+  uint32_t lo, hi;
+  __device__ PivotTest(uint32_t p, VoxLess32) : lo(p & ~0x7ffu), hi(p | 0x7ffu) {}
+  __device__ bool below(uint32_t a) const { return a < lo; }
+  __device__ bool above(uint32_t a) const { return a > hi; }
+};
 __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -183,7 +201,6 @@ template <class K, class Lt>
 __device__ void seg_small_sort(K* key, uint16_t* Lp, uint16_t* Rp, int f, int n, unsigned long long bnd,
                                int dep, Lt lt) {
   const int l = lane_id();
-  const unsigned long long ltm = (1ull << l) - 1ull;
   const unsigned long long lem = l == 63 ? ~0ull : (2ull << l) - 1ull;  // bits <= l
   K v = l < n ? key[f + l] : K(0);
   auto seg_of = [&](int& s, int& e) {  // the segment [s, e) holding this lane
@@ -201,7 +218,7 @@ __device__ void seg_small_sort(K* key, uint16_t* Lp, uint16_t* Rp, int f, int n,
     seg_of(s, e);
     const int dd = dep;
     const bool work = l < n && e - s > 16 && dd > 0;
-    if (!__ballot(work)) break;
+    if (!ballot(work)) break;
     const unsigned long long segm = (e >= 64 ? ~0ull : ((1ull << e) - 1ull)) & ~((1ull << s) - 1ull);
     // __move_median_to_first(first, first + 1, mid, last - 1) of this lane's segment
     const int a = s + 1, b = s + (e - s) / 2, c = e - 1;
@@ -219,13 +236,13 @@ __device__ void seg_small_sort(K* key, uint16_t* Lp, uint16_t* Rp, int f, int n,
       if (l == s) v = vm;
       else if (l == mi) v = v0;
     }
-    const K P = vm;
+    const PivotTest<K, Lt> P(vm, lt);
     // __unguarded_partition: stop lists L ((s, e)) and R ([s, e)), ascending, in LDS; one round of
     // reads gives every lane its pair (k = l - s) and, for a stop, the partner it would swap with
-    const bool isL = work && l > s && !lt(v, P), isR = work && !lt(P, v);
-    const unsigned long long mL = __ballot(isL), mR = __ballot(isR);
+    const bool isL = work && l > s && !P.below(v), isR = work && !P.above(v);
+    const unsigned long long mL = ballot(isL), mR = ballot(isR);
     const int nL = __popcll(mL & segm), nR = __popcll(mR & segm), nm = nL < nR ? nL : nR;
-    const int kL = __popcll(mL & segm & ltm), kRa = __popcll(mR & segm & ltm), kR = nR - 1 - kRa;
+    const int kL = lane_rank(mL & segm), kRa = lane_rank(mR & segm), kR = nR - 1 - kRa;
     uint16_t* L = Lp + f + s;
     uint16_t* R = Rp + f + s;
     if (isL) L[kL] = (uint16_t)l;
@@ -237,9 +254,9 @@ __device__ void seg_small_sort(K* key, uint16_t* Lp, uint16_t* Rp, int f, int n,
     const int pl = isL && kL < nm ? R[nR - 1 - kL] : l;  // L[kL]'s pair R_kL
     const int pr = isR && kR < nm ? L[kR] : l;           // R_kR's pair L[kR]
     wave_sync_lds();
-    const int ks = __popcll(__ballot(kin && Lk < Rk) & segm);  // monotone: the segment's first ks
+    const int ks = __popcll(ballot(kin && Lk < Rk) & segm);  // monotone: the segment's first ks
     // L[ks] and R_{ks-1} (the k-th R stop from the right) are the lanes holding those ranks
-    const unsigned long long bL = __ballot(isL && kL == ks) & segm, bR = __ballot(isR && kR == ks - 1) & segm;
+    const unsigned long long bL = ballot(isL && kL == ks) & segm, bR = ballot(isR && kR == ks - 1) & segm;
     const int Lks = bL ? __ffsll((long long)bL) - 1 : 0;
     const int Rks = bR ? __ffsll((long long)bR) - 1 : 0;
     const int cut = (ks > 0 && (ks >= nL || Lks >= Rks)) ? Rks : Lks;
@@ -247,7 +264,7 @@ __device__ void seg_small_sort(K* key, uint16_t* Lp, uint16_t* Rp, int f, int n,
     const int src = isL && kL < ks ? pl : (isR && kR < ks ? pr : l);
     v = shfl_k(v, src);
     // both parts one level deeper; the cut starts the right part (none when cut == e)
-    bnd |= __ballot(work && l == cut);
+    bnd |= ballot(work && l == cut);
     if (work) dep = dd - 1;
   }
   // segments above 16 with no depth left: libstdc++'s heap sort, in registers
@@ -255,7 +272,7 @@ __device__ void seg_small_sort(K* key, uint16_t* Lp, uint16_t* Rp, int f, int n,
   {
     int s, e;
     seg_of(s, e);
-    unsigned long long hs = __ballot(l < n && l == s && e - s > 16 && dep == 0);
+    unsigned long long hs = ballot(l < n && l == s && e - s > 16 && dep == 0);
     heapm = hs;
     while (hs) {
       const int hs0 = __ffsll((long long)hs) - 1;
@@ -340,7 +357,7 @@ __device__ void wave_heap_sort(K* key, int f, int e, Lt lt) {
         right = !lt(cr, cl);  // __adjust_heap: second = right child, then -- if right < left
         chosen = right ? cr : cl;
       }
-      const unsigned long long rm = __ballot(right);
+      const unsigned long long rm = ballot(right);
       int i = 0, ai = hole;
       for (int k = 0; k < 6; ++k) {
         if (!(ai < lim)) break;
@@ -363,7 +380,7 @@ __device__ void wave_heap_sort(K* key, int f, int e, Lt lt) {
     }
     // __push_heap from the hole: path position t + 1 moves up while its new parent value (the old
     // value of p_{t+1}) is less than `value`; it stops at j = 1 + the deepest t < L where it is not
-    const unsigned long long stay = __ballot(l < L && !lt(pchild, value));
+    const unsigned long long stay = ballot(l < L && !lt(pchild, value));
     const int j = stay ? 64 - __clzll((long long)stay) : 0;
     const int pj = __builtin_amdgcn_readlane(pnode, j < L ? j : 0);
     wave_sync_lds();
@@ -387,7 +404,6 @@ template <class K, class Lt, int kStack = kSortStack>
 __device__ void exact_introsort(K* key, int n, uint16_t* Lp, uint16_t* Rp, int* stk, Lt lt,
                                 int depth0 = -1) {
   const int l = lane_id();
-  const unsigned long long ltm = (1ull << l) - 1ull;
   wave_sync_lds();
   if (n <= 1) return;
   const int lg = 31 - __clz(n);
@@ -413,14 +429,16 @@ __device__ void exact_introsort(K* key, int n, uint16_t* Lp, uint16_t* Rp, int* 
       if (l == 0) { key[m] = vf; key[rf] = P; }
       wave_sync_lds();
       int nL = 0, nR = 0;
+      const PivotTest<K, Lt> pt(P, lt);
       for (int c0 = rf; c0 < rl; c0 += 64) {
         const int i = c0 + l;
         const K v = i < rl ? key[i] : K(0);
-        const bool fl = i < rl && i > rf && !lt(v, P);
-        const bool fr = i < rl && !lt(P, v);
-        const unsigned long long mL = __ballot(fl), mR = __ballot(fr);
-        if (fl) Lp[nL + __popcll(mL & ltm)] = (uint16_t)i;
-        if (fr) Rp[nR + __popcll(mR & ltm)] = (uint16_t)i;
+        const bool fl = i < rl && i > rf && !pt.below(v);
+        const bool fr = i < rl && !pt.above(v);
+        const unsigned long long in = lanes_below(rl - c0);
+        const unsigned long long mL = in & (c0 == rf ? ~1ull : ~0ull) & ~ballot(pt.below(v)), mR = in & ~ballot(pt.above(v));
+        if (fl) Lp[nL + lane_rank(mL)] = (uint16_t)i;
+        if (fr) Rp[nR + lane_rank(mR)] = (uint16_t)i;
         nL += __popcll(mL);
         nR += __popcll(mR);
       }
@@ -429,7 +447,7 @@ __device__ void exact_introsort(K* key, int n, uint16_t* Lp, uint16_t* Rp, int* 
       int ks = nm;  // first k with !(L[k] < R[k]) (monotone)
       for (int c0 = 0; c0 < nm; c0 += 64) {
         const int k = c0 + l;
-        const unsigned long long m = __ballot(k < nm && !(Lp[k] < Rp[nR - 1 - k]));
+        const unsigned long long m = ballot(k < nm && !(Lp[k] < Rp[nR - 1 - k]));
         if (m) { ks = c0 + __ffsll((long long)m) - 1; break; }
       }
       const int cut = (ks > 0 && (ks >= nL || Lp[ks] >= Rp[nR - ks])) ? Rp[nR - ks] : Lp[ks];
@@ -484,7 +502,6 @@ struct BlockSortLds {
 template <class K, class Lt>
 __device__ __forceinline__ int wave_partition(K* key, uint16_t* Lp, uint16_t* Rp, int rf, int rl, Lt lt) {
   const int l = lane_id();
-  const unsigned long long ltm = (1ull << l) - 1ull;
   // __move_median_to_first(first, first+1, mid, last-1)
   const int a = rf + 1, b = rf + (rl - rf) / 2, c = rl - 1;
   const K va = key[a], vb = key[b], vc = key[c], vf = key[rf];
@@ -498,17 +515,22 @@ __device__ __forceinline__ int wave_partition(K* key, uint16_t* Lp, uint16_t* Rp
   // __unguarded_partition: L stops (!(a < P), (rf, rl)) and R stops (!(P < a), [rf, rl)), both
   // listed ascending (R[k], the k-th from the right, is Rp[nR - 1 - k]); two chunks of 64 per step
   int nL = 0, nR = 0;
+  const PivotTest<K, Lt> pt(P, lt);
   for (int c0 = rf; c0 < rl; c0 += 128) {
     const int i0 = c0 + l, i1 = c0 + 64 + l;
     const K v0 = i0 < rl ? key[i0] : K(0), v1 = i1 < rl ? key[i1] : K(0);
-    const bool fl0 = i0 < rl && i0 > rf && !lt(v0, P), fr0 = i0 < rl && !lt(P, v0);
-    const bool fl1 = i1 < rl && !lt(v1, P), fr1 = i1 < rl && !lt(P, v1);
-    const unsigned long long mL0 = __ballot(fl0), mR0 = __ballot(fr0), mL1 = __ballot(fl1), mR1 = __ballot(fr1);
+    const bool fl0 = i0 < rl && i0 > rf && !pt.below(v0), fr0 = i0 < rl && !pt.above(v0);
+    const bool fl1 = i1 < rl && !pt.below(v1), fr1 = i1 < rl && !pt.above(v1);
+    // the masks from one ballot per key compare, the index bounds as scalar masks (a ballot of a
+    // combined predicate is materialised per lane and compared again)
+    const unsigned long long in0 = lanes_below(rl - c0), in1 = lanes_below(rl - c0 - 64);
+    const unsigned long long mL0 = in0 & (c0 == rf ? ~1ull : ~0ull) & ~ballot(pt.below(v0)), mR0 = in0 & ~ballot(pt.above(v0));
+    const unsigned long long mL1 = in1 & ~ballot(pt.below(v1)), mR1 = in1 & ~ballot(pt.above(v1));
     const int nL1 = nL + __popcll(mL0), nR1 = nR + __popcll(mR0);
-    if (fl0) Lp[rf + nL + __popcll(mL0 & ltm)] = (uint16_t)i0;
-    if (fr0) Rp[rf + nR + __popcll(mR0 & ltm)] = (uint16_t)i0;
-    if (fl1) Lp[rf + nL1 + __popcll(mL1 & ltm)] = (uint16_t)i1;
-    if (fr1) Rp[rf + nR1 + __popcll(mR1 & ltm)] = (uint16_t)i1;
+    if (fl0) Lp[rf + nL + lane_rank(mL0)] = (uint16_t)i0;
+    if (fr0) Rp[rf + nR + lane_rank(mR0)] = (uint16_t)i0;
+    if (fl1) Lp[rf + nL1 + lane_rank(mL1)] = (uint16_t)i1;
+    if (fr1) Rp[rf + nR1 + lane_rank(mR1)] = (uint16_t)i1;
     nL = nL1 + __popcll(mL1);
     nR = nR1 + __popcll(mR1);
   }
@@ -521,7 +543,7 @@ __device__ __forceinline__ int wave_partition(K* key, uint16_t* Lp, uint16_t* Rp
     const int k0 = c0 + l, k1 = c0 + 64 + l;
     const int a0 = k0 < nm ? L[k0] : 0, b0 = k0 < nm ? R[nR - 1 - k0] : 0;
     const int a1 = k1 < nm ? L[k1] : 0, b1 = k1 < nm ? R[nR - 1 - k1] : 0;
-    const unsigned long long m0 = __ballot(k0 < nm && !(a0 < b0)), m1 = __ballot(k1 < nm && !(a1 < b1));
+    const unsigned long long m0 = ballot(k0 < nm && !(a0 < b0)), m1 = ballot(k1 < nm && !(a1 < b1));
     if (m0) { ks = c0 + __ffsll((long long)m0) - 1; break; }
     if (m1) { ks = c0 + 64 + __ffsll((long long)m1) - 1; break; }
   }
@@ -561,7 +583,7 @@ __device__ __forceinline__ int block_partition(K* key, uint16_t* Lp, uint16_t* R
     s.ks = 0x7fffffff;
   }
   __syncthreads();
-  const K P = (K)s.piv;
+  const PivotTest<K, Lt> pt((K)s.piv, lt);
   const int per = (rl - rf + kNT - 1) / kNT;
   const int c0 = min(rf + tid * per, rl), c1 = min(c0 + per, rl);
   uint32_t mL = 0, mR = 0;
@@ -570,8 +592,8 @@ __device__ __forceinline__ int block_partition(K* key, uint16_t* Lp, uint16_t* R
     const int i = c0 + u;
     if (i >= c1) continue;
     const K v = key[i];
-    if (i > rf && !lt(v, P)) mL |= 1u << u;
-    if (!lt(P, v)) mR |= 1u << u;
+    if (i > rf && !pt.below(v)) mL |= 1u << u;
+    if (!pt.above(v)) mR |= 1u << u;
   }
   int tot;
   const int ex = block_excl_scan((int)(__popc(mL) | (__popc(mR) << 16)), s.scan, &tot);
