@@ -30,13 +30,13 @@ __global__ void k_ground_add(DevCfg, DevBufs);
 __global__ void k_ground_elev_ransac(DevCfg, DevBufs);
 template <bool kLds> __global__ void k_label(DevCfg, DevBufs);
 __global__ void k_segment(DevCfg, const float4*, const int64_t*, DevBufs);
-__global__ void k_fa_points(DevCfg, DevBufs);
+void launch_fa_points(const DevCfg&, const DevBufs&, int, hipStream_t);
 __global__ void k_select_ring(DevCfg, DevBufs);
 __global__ void k_vox_pcl(DevCfg, DevBufs);
 __global__ void k_debug_exact_sort(const float*, int, int*, long long*);
 __global__ void k_debug_exact_sort32(const uint32_t*, int, int*);
 __global__ void k_fa_concat(DevCfg, DevBufs);
-__global__ void k_dbscan_adj(DevCfg, DevBufs);
+__global__ void k_dbscan_adj(DevCfg, DevBufs, const float4* __restrict__);
 __global__ void k_vis_clouds(DevCfg, DevBufs, int, float4*, int*);
 template <int kDbL> __global__ void k_dbscan_merge(DevCfg, DevBufs);
 
@@ -559,7 +559,7 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   mark();
   k_segment<<<B, 1024, 0, s>>>(c, pts, d_offsets, h->d);
   mark();
-  k_fa_points<<<B, 512, 0, s>>>(c, h->d);
+  launch_fa_points(c, h->d, B, s);
   mark();
   k_select_ring<<<dim3(c.H, B), 256, 0, s>>>(c, h->d);
   mark();
@@ -567,7 +567,7 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   mark();
   k_fa_concat<<<B, 256, 0, s>>>(c, h->d);
   mark();
-  k_dbscan_adj<<<dim3(32, B), 256, 0, s>>>(c, h->d);
+  k_dbscan_adj<<<dim3(32, B), 256, 0, s>>>(c, h->d, h->d.db_pts);
   mark();
   if (c.HW <= 32768) k_dbscan_merge<1024><<<B, 64, 0, s>>>(c, h->d);
   else k_dbscan_merge<2048><<<B, 64, 0, s>>>(c, h->d);
@@ -707,7 +707,7 @@ extern "C" int32_t llsr_debug_exact_sort_phases(const float* vals, int32_t n, lo
 // builds its ring offsets from these counts).
 static void restore_selection(llsr_handle* h, int B, hipStream_t s) {
   const DevCfg& c = h->dc;
-  k_fa_points<<<B, 512, 0, s>>>(c, h->d);
+  launch_fa_points(c, h->d, B, s);
   k_select_ring<<<dim3(c.H, B), 256, 0, s>>>(c, h->d);
   if (c.exact_vg) launch_vox_pcl(c, h->d, B, s);
   (void)hipStreamSynchronize(s);
@@ -728,7 +728,7 @@ extern "C" float llsr_debug_phase_ms(llsr_handle* h, int32_t k, int32_t phase, i
   if (k == 9) {  // k_vox_pcl needs the keys k_select_ring leaves: both re-run before each launch
     float tot = 0.f;
     for (int r = 0; r < reps; ++r) {
-      k_fa_points<<<B, 512, 0, s>>>(h->dc, h->d);
+      launch_fa_points(h->dc, h->d, B, s);
       k_select_ring<<<dim3(c.H, B), 256, 0, s>>>(h->dc, h->d);
       (void)hipEventRecord(e0, s);
       launch_vox_pcl(c, h->d, B, s);
@@ -745,7 +745,7 @@ extern "C" float llsr_debug_phase_ms(llsr_handle* h, int32_t k, int32_t phase, i
     // k_fa_points restores it before every timed launch, so each phase sees the batch's real work
     float tot = 0.f;
     for (int r = 0; r < reps; ++r) {
-      k_fa_points<<<B, 512, 0, s>>>(h->dc, h->d);
+      launch_fa_points(h->dc, h->d, B, s);
       (void)hipEventRecord(e0, s);
       k_select_ring<<<dim3(c.H, B), 256, 0, s>>>(c, h->d);
       (void)hipEventRecord(e1, s);
@@ -761,12 +761,12 @@ extern "C" float llsr_debug_phase_ms(llsr_handle* h, int32_t k, int32_t phase, i
     switch (k) {
       case 8: k_select_ring<<<dim3(c.H, B), 256, 0, s>>>(c, h->d); break;
       case 10: k_fa_concat<<<B, 256, 0, s>>>(c, h->d); break;
-      case 11: k_dbscan_adj<<<dim3(32, B), 256, 0, s>>>(c, h->d); break;
+      case 11: k_dbscan_adj<<<dim3(32, B), 256, 0, s>>>(c, h->d, h->d.db_pts); break;
       case 12:
         if (c.HW <= 32768) k_dbscan_merge<1024><<<B, 64, 0, s>>>(c, h->d);
         else k_dbscan_merge<2048><<<B, 64, 0, s>>>(c, h->d);
         break;
-      case 7: k_fa_points<<<B, 512, 0, s>>>(c, h->d); break;
+      case 7: launch_fa_points(c, h->d, B, s); break;
       case 6: k_segment<<<B, 1024, 0, s>>>(c, nullptr, nullptr, h->d); break;
       case 5:
         if (c.ccl_lds) k_label<true><<<B, 1024, label_lds(c), s>>>(c, h->d);

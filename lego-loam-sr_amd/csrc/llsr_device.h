@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "llsr_libm.h"
+
 namespace llsr {
 
 // Per-slot counter words (counts[b * kCnt + ...]).
@@ -84,6 +86,53 @@ struct DevBufs {
   uint32_t* mt0;        // [624] RANSAC's mt19937 state after seed(12345) and its first twist
   int* phantom;         // [B] FA carry-over state: cloudSmoothness[4].ind (value is always 0)
 };
+
+// C_HALF before k_fa_points when k_segment's first tile of cells holds no passing point
+constexpr int kHalfUnknown = -2;
+
+// adjustDistortion's first orientation branch (FA:578-583) and its halfPassed test (FA:584-586)
+__device__ __forceinline__ float ori_branch1(float o, float start) {
+  constexpr double kPi_ = 3.14159265358979323846;
+  if ((double)o < (double)start - kPi_ / 2) o = (float)(o + 2 * kPi_);
+  else if ((double)o > (double)start + kPi_ * 3 / 2) o = (float)(o - 2 * kPi_);
+  return o;
+}
+// o = -atan2f(y, x) of a segmented point
+__device__ __forceinline__ bool half_passed(float o, float start) {
+  return (double)(ori_branch1(o, start) - start) > 3.14159265358979323846;
+}
+
+// halfPassed's test (FA:578-586) on o = -atan2f(y, x) from project_cell_fast's atan2 (|err| < 1e-6
+// rad): with d = o - start its outcome changes only at d = -pi, -pi/2, pi and 3 pi / 2 (the branch
+// cuts and the test, o + 2 pi and o - 2 pi folded in), so the approximation decides it exactly when
+// d is 1e-5 away from each; otherwise, and for zero / huge operands, the exact libm path.
+// 1 / 0: passes / fails, 2: undecided (take the exact path)
+__device__ __forceinline__ int half_passed_fast(float y, float x, float start) {
+  const float ax = fabsf(y), bx = fabsf(x);
+  const float mx = fmaxf(ax, bx), mn = fminf(ax, bx);
+  if (!(mn > 0.0f && mx < 1e30f)) return 2;
+  const float t = mn * __builtin_amdgcn_rcpf(mx);
+  const float u = t * t;
+  float pa = __builtin_fmaf(u, -0x1.09b84ap-8f, 0x1.6633d8p-6f);
+  pa = __builtin_fmaf(u, pa, -0x1.ca08a0p-5f);
+  pa = __builtin_fmaf(u, pa, 0x1.8af1c2p-4f);
+  pa = __builtin_fmaf(u, pa, -0x1.1cd946p-3f);
+  pa = __builtin_fmaf(u, pa, 0x1.988174p-3f);
+  pa = __builtin_fmaf(u, pa, -0x1.554c3ap-2f);
+  pa = __builtin_fmaf(u, pa, 0x1.ffffeap-1f);
+  float ha = pa * t;
+  ha = ax > bx ? 1.57079637f - ha : ha;
+  ha = x < 0.0f ? 3.14159274f - ha : ha;
+  ha = y < 0.0f ? -ha : ha;
+  const double dd = (double)-ha - (double)start;
+  constexpr double kPi_ = 3.14159265358979323846, e = 1e-5;
+  if (!(fabs(dd + kPi_) > e && fabs(dd + kPi_ / 2) > e && fabs(dd - kPi_) > e && fabs(dd - 1.5 * kPi_) > e)) return 2;
+  return (dd < -kPi_ / 2 ? dd > -kPi_ : (dd <= 1.5 * kPi_ && dd > kPi_)) ? 1 : 0;
+}
+__device__ __forceinline__ bool half_passed_any(float y, float x, float start) {
+  const int r = half_passed_fast(y, x, start);
+  return r == 2 ? half_passed(-llsr_libm::atan2f_(y, x), start) : r == 1;
+}
 
 // DBSCAN adjacency capacity per scan (edge candidates); larger M falls back to on-the-fly rows.
 constexpr int kAdjCap = 2048;

@@ -16,19 +16,16 @@ constexpr double kPi = 3.14159265358979323846;
 
 // ---------------------------------------------------------------------------------------------
 // K7 per-point stage: adjustDistortion (FA:565-598), calculateSmoothnessOurs (FA:817-848),
-// markOccludedPoints (FA:851-899). One workgroup (1024 threads) per scan.
+// markOccludedPoints (FA:851-899). One workgroup (256 threads) per (tile of kFaTile segmented
+// points, scan): ~17 tiles of a VLP-16 scan in flight at once instead of one workgroup walking them.
 // halfPassed is a one-way latch, so the serial loop equals: points up to the first index whose
-// first-branch orientation passes start + pi use branch 1, later ones branch 2 (block min).
+// first-branch orientation passes start + pi use branch 1, later ones branch 2; k_segment leaves
+// that index in C_HALF (kHalfUnknown when its first tile holds none, then each workgroup finds it).
 // Curvature reads an LDS tile of LOAM points with a +-5 halo. Occlusion writes become a gather
 // over the +-6 window of per-point flags. FA carry-over arrays (picked, cloudLabel) are per slot.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ float ori_branch1(float o, float start) {
-  if ((double)o < (double)start - kPi / 2) o = (float)(o + 2 * kPi);
-  else if ((double)o > (double)start + kPi * 3 / 2) o = (float)(o - 2 * kPi);
-  return o;
-}
-
-constexpr int kTile = 2048;  // points per tile: 4 per lane (512 lanes), so every lane has 4 loads in flight
+constexpr int kFaT = 256;
+constexpr int kFaTile = 4 * kFaT - 12;  // 1012 points: with the +-5 point halo and the +-6 flag halo, 4 slots per lane
 
 // LOAM-frame point of segmented point i (FA:565-598): orientation branch by the halfPassed latch
 // (`first`), relative time, intensity = ring + scan_period * relTime.
@@ -47,145 +44,144 @@ __device__ __forceinline__ float4 loam_point(const DevCfg& c, float4 p, int i, i
   return make_float4(p.y, p.z, p.x, inten);
 }
 
-__global__ __launch_bounds__(512) void k_fa_points(DevCfg c, DevBufs d) {
+__global__ __launch_bounds__(kFaT) void k_fa_points(DevCfg c, DevBufs d) {
+  constexpr int kTile = kFaTile;
   __shared__ float4 tp[kTile + 10];
   __shared__ uint8_t fl[kTile + 12];  // bit0 A_i, bit1 B_i, bit2 C_i for i in [t0-6, t0+T+6)
-  __shared__ int tmp[32];
-  const int b = blockIdx.x;
+  __shared__ int tmp[kFaT / 64];
+  const int b = blockIdx.y;
+  const int t0 = blockIdx.x * kTile;
   const size_t base = (size_t)b * c.HW;
-  const int tid = threadIdx.x, nt = blockDim.x;
-  int* cnt = d.counts + b * kCnt;
+  const int tid = threadIdx.x;
+  constexpr int nt = kFaT;
+  const int* cnt = d.counts + b * kCnt;
   const int S = cnt[C_S];
+  if (t0 >= S) return;
   const float start = d.orient[b * 4 + 0], endo = d.orient[b * 4 + 1], diff = d.orient[b * 4 + 2];
   const float4* seg = d.seg + base;
   float4* loam = d.loam + base;
 
-  // The latch index is the smallest i whose test passes, so the scan stops after the first chunk
-  // of kP * nt points that holds one (normally inside ring 0, half a turn in): later chunks only
-  // hold larger indices. Typical cost: one chunk of orientations instead of all S.
-  int first = INT_MAX;
-  constexpr int kP = 4;
-  for (int c0 = 0; c0 < S; c0 += kP * nt) {
-    const int i0 = c0 + tid;
-    float4 pp[kP];
+  int first = cnt[C_HALF];  // nothing writes it during this launch: uniform over the workgroup
+  if (first == kHalfUnknown) {
+    // the latch lies past k_segment's first tile (or nowhere): the smallest passing index, chunk
+    // by chunk (later chunks only hold larger indices)
+    first = INT_MAX;
+    for (int c0 = 0; c0 < S; c0 += 4 * nt) {
+      const int i0 = c0 + tid;
+      float4 pp[4];
 #pragma unroll
-    for (int u = 0; u < kP; ++u) pp[u] = i0 + u * nt < S ? seg[i0 + u * nt] : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int u = 0; u < 4; ++u) pp[u] = i0 + u * nt < S ? seg[i0 + u * nt] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int u = 0; u < kP; ++u) {
-      const int i = i0 + u * nt;
-      if (i >= S) continue;
-      const float o = ori_branch1(-atan2f_(pp[u].y, pp[u].x), start);
-      if ((double)(o - start) > kPi && i < first) first = i;
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * nt;
+        if (i >= S) continue;
+        if (i < first && half_passed_any(pp[u].y, pp[u].x, start)) first = i;
+      }
+      first = block_reduce_min(first, tmp);
+      if (first != INT_MAX) break;
     }
-    first = block_reduce_min(first, tmp);
-    if (first != INT_MAX) break;
   }
-  if (tid == 0) cnt[C_HALF] = first;
 
-  // Tiles of kTile points: the LOAM points (and the +-5 halo) are computed straight into LDS from
-  // the segmented cloud, written out once, and the curvature / occlusion pass reads them there.
   const float* rng = d.seg_range + base;
   const uint32_t* col = d.seg_col + base;
   uint8_t* picked = d.picked + base;
   int8_t* clabel = d.clabel + base;
   float* curv = d.curv + base;
-  // per tile ONE round of loads: the tile's points with their +-5 halo (kP5 per lane) and the
-  // occlusion inputs (range, column of i; the neighbours' from the adjacent lanes, the wave's edge
-  // lanes loading their one outside value), all in flight together
-  constexpr int kP5 = (kTile + 10 + 511) / 512;
-  constexpr int kQ = (kTile + 12 + 511) / 512;
+  // ONE round of loads: the tile's points with their +-5 halo and the occlusion inputs (range,
+  // column of i; the neighbours' from the adjacent lanes, the wave's edge lanes loading their one
+  // outside value), all in flight together. Slot q = tid + u * nt of both covers [0, 4 nt).
   const int ln = lane_id();
-  for (int t0 = 0; t0 < S; t0 += kTile) {
-    float4 pp[kP5];
-    float r1[kQ], rx[kQ];
-    uint32_t c1[kQ], cx[kQ];
+  float4 pp[4];
+  float r1[4], rx[4];
+  uint32_t c1[4], cx[4];
 #pragma unroll
-    for (int u = 0; u < kP5; ++u) {
-      const int q = tid + u * nt, k = t0 - 5 + q;
-      pp[u] = (q < kTile + 10 && k >= 0 && k < S) ? seg[k] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int u = 0; u < kQ; ++u) {
-      const int q = tid + u * nt, i = t0 - 6 + q;
-      const bool in = q <= kTile + 12 && i >= 0 && i < S;  // (q = kTile + 12: the last flag's i + 1)
-      r1[u] = in ? rng[i] : 0.0f;
-      c1[u] = in ? col[i] : 0u;
-      const int ie = ln == 0 ? i - 1 : i + 1;  // lane 0: i - 1; lane 63: i + 1 (the others unused)
-      const bool ine = (ln == 0 || ln == 63) && q < kTile + 12 && ie >= 0 && ie < S;
-      rx[u] = ine ? rng[ie] : 0.0f;
-      cx[u] = ine ? col[ie] : 0u;
-    }
-#pragma unroll
-    for (int u = 0; u < kP5; ++u) {
-      const int q = tid + u * nt, k = t0 - 5 + q;
-      if (q >= kTile + 10) continue;
-      if (k >= 0 && k < S) {
-        const float4 lp = loam_point(c, pp[u], k, first, start, endo, diff);
-        tp[q] = lp;
-        if (q >= 5 && q < kTile + 5) loam[k] = lp;
-      } else {
-        tp[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-    }
-    // occlusion flags of the tile (+ halo)
-#pragma unroll
-    for (int u = 0; u < kQ; ++u) {
-      const int q = tid + u * nt, i = t0 - 6 + q;
-      const float up = __shfl_up(r1[u], 1, 64), dn = __shfl_down(r1[u], 1, 64);
-      const uint32_t cdn = (uint32_t)__shfl_down((int)c1[u], 1, 64);
-      if (q >= kTile + 12) continue;
-      uint8_t f = 0;
-      if (i >= 5 && i < S - 6) {
-        const float r0 = ln == 0 ? rx[u] : up, r2 = ln == 63 ? rx[u] : dn;
-        const uint32_t c2 = ln == 63 ? cx[u] : cdn;
-        const float d1 = r1[u], d2 = r2;
-        const int colDiff = abs((int)(c2 - c1[u]));
-        if (colDiff < 10) {
-          if ((double)(d1 - d2) > 0.3) f |= 1;
-          else if ((double)(d2 - d1) > 0.3) f |= 2;
-        }
-        const float diff1 = fabs_((float)(r0 - r1[u]));
-        const float diff2 = fabs_((float)(r2 - r1[u]));
-        if ((double)diff1 > 0.02 * (double)r1[u] && (double)diff2 > 0.02 * (double)r1[u]) f |= 4;
-      }
-      fl[q] = f;
-    }
-    __syncthreads();
-    for (int q0 = tid; q0 < kTile; q0 += nt) {
-      const int k = t0 + q0;
-      if (k >= S) break;
-      const bool inner = k >= 5 && k < S - 5;
-      float cv = 0.0f;
-      if (inner) {
-        const int q = q0 + 5;
-        float dx = 0.f, dy = 0.f, dz = 0.f;
-#pragma unroll
-        for (int m = -5; m < 6; ++m) dx += tp[q + m].x;
-        dx -= 11 * tp[q].x;
-#pragma unroll
-        for (int m = -5; m < 6; ++m) dy += tp[q + m].y;
-        dy -= 11 * tp[q].y;
-#pragma unroll
-        for (int m = -5; m < 6; ++m) dz += tp[q + m].z;
-        dz -= 11 * tp[q].z;
-        const float4 p = tp[q];
-        cv = sqrt_(dx * dx + dy * dy + dz * dz) / sqrt_(p.x * p.x + p.y * p.y + p.z * p.z) / 10;
-      }
-      curv[k] = cv;
-      // picked[k]: reset on [5, S-5) by the smoothness loop, then any occlusion write
-      bool occ = false;
-      const int fq = q0 + 6;  // fl index of i = k
-      if (fl[fq] & 4) occ = true;
-#pragma unroll
-      for (int m = 0; m <= 5; ++m) occ |= (fl[fq + m] & 1) != 0;   // A_i, i in [k, k+5]
-#pragma unroll
-      for (int m = 1; m <= 6; ++m) occ |= (fl[fq - m] & 2) != 0;   // B_i, i in [k-6, k-1]
-      const uint8_t old = inner ? (uint8_t)0 : picked[k];  // only the 10 edge points keep theirs
-      picked[k] = old | (occ ? (uint8_t)1 : (uint8_t)0);
-      if (inner) clabel[k] = 0;
-    }
-    __syncthreads();
+  for (int u = 0; u < 4; ++u) {
+    const int q = tid + u * nt, k = t0 - 5 + q;
+    pp[u] = (q < kTile + 10 && k >= 0 && k < S) ? seg[k] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int q = tid + u * nt, i = t0 - 6 + q;
+    const bool in = i >= 0 && i < S;
+    r1[u] = in ? rng[i] : 0.0f;
+    c1[u] = in ? col[i] : 0u;
+    const int ie = ln == 0 ? i - 1 : i + 1;  // lane 0: i - 1; lane 63: i + 1 (the others unused)
+    const bool ine = (ln == 0 || ln == 63) && ie >= 0 && ie < S;
+    rx[u] = ine ? rng[ie] : 0.0f;
+    cx[u] = ine ? col[ie] : 0u;
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int q = tid + u * nt, k = t0 - 5 + q;
+    if (q >= kTile + 10) continue;
+    if (k >= 0 && k < S) {
+      const float4 lp = loam_point(c, pp[u], k, first, start, endo, diff);
+      tp[q] = lp;
+      if (q >= 5 && q < kTile + 5) loam[k] = lp;
+    } else {
+      tp[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  // occlusion flags of the tile (+ halo)
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int q = tid + u * nt, i = t0 - 6 + q;
+    const float up = __shfl_up(r1[u], 1, 64), dn = __shfl_down(r1[u], 1, 64);
+    const uint32_t cdn = (uint32_t)__shfl_down((int)c1[u], 1, 64);
+    uint8_t f = 0;
+    if (i >= 5 && i < S - 6) {
+      const float r0 = ln == 0 ? rx[u] : up, r2 = ln == 63 ? rx[u] : dn;
+      const uint32_t c2 = ln == 63 ? cx[u] : cdn;
+      const float d1 = r1[u], d2 = r2;
+      const int colDiff = abs((int)(c2 - c1[u]));
+      if (colDiff < 10) {
+        if ((double)(d1 - d2) > 0.3) f |= 1;
+        else if ((double)(d2 - d1) > 0.3) f |= 2;
+      }
+      const float diff1 = fabs_((float)(r0 - r1[u]));
+      const float diff2 = fabs_((float)(r2 - r1[u]));
+      if ((double)diff1 > 0.02 * (double)r1[u] && (double)diff2 > 0.02 * (double)r1[u]) f |= 4;
+    }
+    fl[q] = f;
+  }
+  __syncthreads();
+  for (int q0 = tid; q0 < kTile; q0 += nt) {
+    const int k = t0 + q0;
+    if (k >= S) break;
+    const bool inner = k >= 5 && k < S - 5;
+    float cv = 0.0f;
+    if (inner) {
+      const int q = q0 + 5;
+      float dx = 0.f, dy = 0.f, dz = 0.f;
+#pragma unroll
+      for (int m = -5; m < 6; ++m) dx += tp[q + m].x;
+      dx -= 11 * tp[q].x;
+#pragma unroll
+      for (int m = -5; m < 6; ++m) dy += tp[q + m].y;
+      dy -= 11 * tp[q].y;
+#pragma unroll
+      for (int m = -5; m < 6; ++m) dz += tp[q + m].z;
+      dz -= 11 * tp[q].z;
+      const float4 p = tp[q];
+      cv = sqrt_(dx * dx + dy * dy + dz * dz) / sqrt_(p.x * p.x + p.y * p.y + p.z * p.z) / 10;
+    }
+    curv[k] = cv;
+    // picked[k]: reset on [5, S-5) by the smoothness loop, then any occlusion write
+    bool occ = false;
+    const int fq = q0 + 6;  // fl index of i = k
+    if (fl[fq] & 4) occ = true;
+#pragma unroll
+    for (int m = 0; m <= 5; ++m) occ |= (fl[fq + m] & 1) != 0;   // A_i, i in [k, k+5]
+#pragma unroll
+    for (int m = 1; m <= 6; ++m) occ |= (fl[fq - m] & 2) != 0;   // B_i, i in [k-6, k-1]
+    const uint8_t old = inner ? (uint8_t)0 : picked[k];  // only the 10 edge points keep theirs
+    picked[k] = old | (occ ? (uint8_t)1 : (uint8_t)0);
+    if (inner) clabel[k] = 0;
+  }
+}
+
+void launch_fa_points(const DevCfg& c, const DevBufs& d, int B, hipStream_t s) {
+  k_fa_points<<<dim3((c.HW + kFaTile - 1) / kFaTile, B), kFaT, 0, s>>>(c, d);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1016,9 +1012,16 @@ __device__ __forceinline__ bool db_near_fast(const DevCfg& c, float4 pi, float4 
 // exact db_near inside the band). Takes the O(M^2) float work off DBSCAN's serial merge.
 // grid (32, B), block 256.
 // ---------------------------------------------------------------------------------------------
+// A wave's LDS instructions execute in issue order, so lanes of one wave only need the compiler
+// not to move memory operations across these points (no s_waitcnt, no cache maintenance).
+__device__ __forceinline__ void wave_order() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
 constexpr int kAdjRows = 16;
 
-__global__ __launch_bounds__(256) void k_dbscan_adj(DevCfg c, DevBufs d) {
+__global__ __launch_bounds__(256) void k_dbscan_adj(DevCfg c, DevBufs d, const float4* __restrict__ db_pts) {
   const int b = blockIdx.y;
   const size_t base = (size_t)b * c.HW;
   const int M = d.counts[b * kCnt + C_M];
@@ -1028,8 +1031,10 @@ __global__ __launch_bounds__(256) void k_dbscan_adj(DevCfg c, DevBufs d) {
   const int nwv = (gridDim.x * blockDim.x) >> 6;
   const int l = lane_id();
   uint32_t* adj = d.db_adj + (size_t)b * kAdjCap * kAdjWords;
-  const float4* pts = d.db_pts + base;
+  const float4* __restrict__ pts = db_pts + base;  // d.db_pts as a restrict argument: scalar loads
   const float r2 = c.DBFr * c.DBFr, lo = r2 * (1.0f - 2e-5f), hi = r2 * (1.0f + 2e-5f);
+  __shared__ unsigned long long sb[4][kAdjRows];  // each wave's row ballots, read back as words
+  const int wl = threadIdx.x >> 6;
   for (int task = wv; task < nch * ngr; task += nwv) {
     const int ch = task % nch, i0 = (task / nch) * kAdjRows;
     const int j = ch * 64 + l;
@@ -1039,26 +1044,34 @@ __global__ __launch_bounds__(256) void k_dbscan_adj(DevCfg c, DevBufs d) {
     const float k2 = pj.w * pj.w, z2 = kz * kz;
     const bool fast = c.DBFr > 0.0f && k2 > 1e-30f && k2 < 1e30f && z2 > 1e-30f && z2 < 1e30f;
     const float rk = __builtin_amdgcn_rcpf(k2), rz = __builtin_amdgcn_rcpf(z2);
-    // the task's row points: one load by lanes 0 .. kAdjRows-1, broadcast per row by readlane;
+    // the task's row points: wave-uniform addresses of a read-only array, so scalar loads, all in
+    // flight before the first row (rows past M repeat row M - 1; their bits are never stored);
     // the rows' ballots gather in lanes 2r (low word) / 2r+1 (high word) and leave in ONE store
-    // (vector-memory instructions, not arithmetic, set this kernel's pace)
-    const float4 prow = l < kAdjRows && i0 + l < M ? pts[i0 + l] : make_float4(0.f, 0.f, 0.f, 0.f);
     uint32_t out = 0u;
+    constexpr int kHalf = kAdjRows / 2;  // 8 rows' points at a time in SGPRs (16 would spill)
+#pragma unroll
     for (int r = 0; r < kAdjRows; ++r) {
-      if (i0 + r >= M) break;
-      float4 pi;
-      pi.x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(prow.x), r));
-      pi.y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(prow.y), r));
-      pi.z = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(prow.z), r));
-      pi.w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(prow.w), r));
+      float3 prw[kHalf];
+      if (r % kHalf == 0) {
+#pragma unroll
+        for (int e = 0; e < kHalf; ++e) {
+          const float4 q = pts[min(i0 + r + e, M - 1)];
+          prw[e] = make_float3(q.x, q.y, q.z);
+        }
+      }
+      const float3 pr = prw[r % kHalf];
+      const float4 pi = make_float4(pr.x, pr.y, pr.z, 0.0f);  // (db_near reads no pi.w)
       const float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
       const float s = (dx * dx + dy * dy) * rk + dz * dz * rz;
       bool nb = fast && s < lo;
       if (inj && !(fast && (s < lo || s > hi))) nb = db_near(c, pi, pj, kz);
       nb = nb && inj;
       const unsigned long long m = __ballot(nb);
-      out = l == 2 * r ? (uint32_t)m : l == 2 * r + 1 ? (uint32_t)(m >> 32) : out;
+      if (l == 0) sb[wl][r] = m;
     }
+    wave_order();
+    if (l < 2 * kAdjRows) out = reinterpret_cast<const uint32_t*>(sb[wl])[l];
+    wave_order();  // the next task's writes after these reads
     const int w = 2 * ch + (l & 1);
     if (l < 2 * kAdjRows && i0 + (l >> 1) < M && w < kAdjWords) adj[(size_t)(i0 + (l >> 1)) * kAdjWords + w] = out;
   }
@@ -1106,12 +1119,6 @@ __device__ __forceinline__ int wave_min_ballot(int v, bool valid, int nbits) {
   return res;
 }
 
-// A wave's LDS instructions execute in issue order, so lanes of one wave only need the compiler
-// not to move memory operations across these points (no s_waitcnt, no cache maintenance).
-__device__ __forceinline__ void wave_order() {
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("" ::: "memory");
-}
 
 // kRowBlk adjacency rows are staged into LDS per block (one load latency per block instead of one
 // per point: the rows of a 300-point scan come from L2 / the Infinity Cache, ~1 us away), the next

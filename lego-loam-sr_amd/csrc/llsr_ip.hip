@@ -1149,6 +1149,12 @@ __global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
 template __global__ void k_label<true>(DevCfg, DevBufs);
 template __global__ void k_label<false>(DevCfg, DevBufs);
 
+// halfPassed's exact test, out of line: the rare undecided points of k_segment's first tile (inlined,
+// the libm code's registers would spill k_segment's SGPRs)
+__device__ __attribute__((noinline)) bool half_passed_exact(float y, float x, float start) {
+  return half_passed(-atan2f_(y, x), start);
+}
+
 // ---------------------------------------------------------------------------------------------
 // K6 segmented / outlier extraction (IP:791-832) + findStartEndAngle (IP:430-445).
 // Row-major block compaction; ring start/end indices fall out of the running count at each
@@ -1163,7 +1169,14 @@ __global__ __launch_bounds__(1024) void k_segment(DevCfg c, const float4* __rest
   const int8_t* g = d.ground + base;
   const int* lab = d.label + base;
   int* cnt = d.counts + b * kCnt;
+  __shared__ float s_start;
+  __shared__ int s_half;  // adjustDistortion's halfPassed latch among the first tile's segmented points
+  constexpr int kUnd = 64;
+  __shared__ float4 s_und[kUnd];  // points the fast halfPassed test left undecided: x, y, -, index
+  __shared__ int s_nund;
   if (tid == 0) {
+    s_half = INT_MAX;
+    s_nund = 0;
     float o0 = 0.f, o1 = 0.f, o2 = 0.f;
     if (cnt[C_NPTS] > 0) {
       const float4 a = pts[off[b] + cnt[C_FIRST]], e = pts[off[b] + cnt[C_LAST]];
@@ -1176,6 +1189,7 @@ __global__ __launch_bounds__(1024) void k_segment(DevCfg c, const float4* __rest
     d.orient[b * 4 + 0] = o0;
     d.orient[b * 4 + 1] = o1;
     d.orient[b * 4 + 2] = o2;
+    s_start = o0;
   }
   // 0 = skip, 1 = segmented, 2 = outlier
   auto kind = [&](int cell, int L, int8_t gv) -> int {
@@ -1258,6 +1272,19 @@ __global__ __launch_bounds__(1024) void k_segment(DevCfg c, const float4* __rest
         if (i > 0) d.end_ring[b * H + i - 1] = ps - 1 - 5;
       }
       if (kk[u] == 1) {
+        // halfPassed (FA:584): the latch is the smallest passing index, and the first tile holds
+        // the smallest indices (row 0: half a turn in, normally); k_fa_points searches otherwise
+        // (ps grows with the lane within a slot: the wave's first passing lane holds its minimum)
+        // (undecided lanes, rare, queue for the exact test after the loop)
+        if (t0 == 0) {
+          const int hp = half_passed_fast(f[u].y, f[u].x, s_start);
+          const unsigned long long mp = ballot(hp == 1);
+          if (mp && l == __builtin_ctzll(mp)) atomicMin(&s_half, ps);
+          if (hp == 2) {
+            const int k = atomicAdd(&s_nund, 1);
+            if (k < kUnd) s_und[k] = make_float4(f[u].x, f[u].y, 0.0f, __int_as_float(ps));
+          }
+        }
         d.seg[base + ps] = f[u];
         d.seg_ground[base + ps] = gc[u] == 1;
         d.seg_col[base + ps] = (uint32_t)j;
@@ -1273,7 +1300,15 @@ __global__ __launch_bounds__(1024) void k_segment(DevCfg c, const float4* __rest
     baseO += tot >> 16;
   }
   const int S = baseS, O = baseO;
-  if (tid == 0) {
+  __syncthreads();
+  const int nund = s_nund;
+  if (nund > 0 && nund <= kUnd && tid < nund) {
+    const float4 q = s_und[tid];
+    if (half_passed_exact(q.y, q.x, s_start)) atomicMin(&s_half, __float_as_int(q.w));
+  }
+  __syncthreads();  // s_half final
+  if (tid == 0) {  // (more undecided points than the queue holds: k_fa_points searches)
+    cnt[C_HALF] = (s_half == INT_MAX || nund > kUnd) ? kHalfUnknown : s_half;
     d.end_ring[b * H + H - 1] = S - 1 - 5;
     cnt[C_S] = S;
     cnt[C_O] = O;

@@ -234,3 +234,27 @@ def test_batches_queued_on_two_streams_before_fetch(require_gpu):
         errs = compare(pipe.fetch(b), last[b])
         assert not errs, f"slot {b}:\n  " + "\n  ".join(errs)
     pipe.close()
+
+
+def test_half_passed_latch_outside_first_tile(require_gpu):
+    """adjustDistortion's halfPassed latch (FA:584) when k_segment's first tile of cells (rows 0-2 of
+    VLP-16) holds no passing point: the bottom rings removed, or kept only over the first eighth of
+    the turn (their points sit within 45 deg of the start). k_fa_points then finds the latch itself."""
+    cfg = default_config("vlp16")
+    pipe = Pipeline(cfg, max_points=2 * cfg.num_vertical_scans * cfg.num_horizontal_scans)
+    ora = oracle_py.Oracle(cfg)
+    elev, W = synth.beam_layout("vlp16")
+    failures = []
+    for s, mode in ((1, "empty"), (2, "sector"), (3, "normal"), (4, "sector")):
+        pts = synth.make_scan(s, "vlp16").copy()
+        idx = np.arange(len(pts))
+        low = elev[idx % len(elev)] < -10.0  # rows 0-2
+        if mode == "empty":
+            pts[low, :3] = np.nan
+        elif mode == "sector":
+            pts[low & (idx // len(elev) > W // 8), :3] = np.nan
+        errs = compare(pipe.process_scan(pts), ora.process(pts))
+        if errs:
+            failures.append((s, mode, errs))
+    pipe.close()
+    assert not failures, "\n".join(f"seed {s} ({m}):\n  " + "\n  ".join(e) for s, m, e in failures)
