@@ -175,6 +175,11 @@ static int label_lds(const DevCfg& c) { return c.HW * (int)(sizeof(int) + 1); }
 static int label_band_lds(const DevCfg& c) { return c.lbl_band * c.W * (int)sizeof(int); }
 static bool use_fused(const llsr_handle* h) { return h->dc.ccl_lds != 0; }
 
+// k_segment / k_ground_elev_ransac (any multiple of 64 up to 1024 threads): 512 for range images
+// that fit LDS (VLP-16: three / two scans per CU instead of one; r06_v40, 0.289 -> 0.282 and
+// 0.180 -> 0.167 ms per 1024 scans), 1024 for the larger ones (HDL-64E: 512 was slower)
+static int per_scan_threads(const DevCfg& c) { return c.ccl_lds ? 512 : 1024; }
+
 // the PCL-order less-flat VoxelGrid of every pending ring
 static void launch_vox_pcl(const DevCfg& c, const DevBufs& d, int B, hipStream_t s) {
   k_vox_pcl<<<dim3(c.H, B), 256, 0, s>>>(c, d);
@@ -550,14 +555,14 @@ extern "C" int32_t llsr_process_batch(llsr_handle* h, const float* d_xyzi, const
   }
   k_ground_add<<<dim3((c.H + 3) / 4, B), 256, 0, s>>>(c, h->d);
   mark();
-  k_ground_elev_ransac<<<B, 1024, 0, s>>>(c, h->d);
+  k_ground_elev_ransac<<<B, per_scan_threads(c), 0, s>>>(c, h->d);
   mark();
   if (c.ccl_lds)
     k_label<true><<<B, 1024, label_lds(c), s>>>(c, h->d);
   else
     k_label<false><<<B, 1024, label_band_lds(c), s>>>(c, h->d);
   mark();
-  k_segment<<<B, 1024, 0, s>>>(c, pts, d_offsets, h->d);
+  k_segment<<<B, per_scan_threads(c), 0, s>>>(c, pts, d_offsets, h->d);
   mark();
   launch_fa_points(c, h->d, B, s);
   mark();
@@ -767,12 +772,12 @@ extern "C" float llsr_debug_phase_ms(llsr_handle* h, int32_t k, int32_t phase, i
         else k_dbscan_merge<2048><<<B, 64, 0, s>>>(c, h->d);
         break;
       case 7: launch_fa_points(c, h->d, B, s); break;
-      case 6: k_segment<<<B, 1024, 0, s>>>(c, nullptr, nullptr, h->d); break;
+      case 6: k_segment<<<B, per_scan_threads(c), 0, s>>>(c, nullptr, nullptr, h->d); break;
       case 5:
         if (c.ccl_lds) k_label<true><<<B, 1024, label_lds(c), s>>>(c, h->d);
         else k_label<false><<<B, 1024, label_band_lds(c), s>>>(c, h->d);
         break;
-      case 4: k_ground_elev_ransac<<<B, 1024, 0, s>>>(c, h->d); break;
+      case 4: k_ground_elev_ransac<<<B, per_scan_threads(c), 0, s>>>(c, h->d); break;
       case 3: k_ground_add<<<dim3((c.H + 3) / 4, B), 256, 0, s>>>(c, h->d); break;
       case 1:
         if (!use_fused(h)) return -2.f;

@@ -600,7 +600,7 @@ __device__ __forceinline__ float ransac_dist(const float cf[4], float4 q) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// K4 ELEVATION + NEAR + RANSAC + final ground (IP:673-735). One workgroup (1024 threads) per
+// K4 ELEVATION + NEAR + RANSAC + final ground (IP:673-735). One workgroup (512 or 1024 threads) per
 // scan: a last-valid carry scan over columns, a row-major compaction of near-ground cells, and
 // PCL 1.10's RandomSampleConsensus driven by lane 0 with inlier counting spread over the block.
 // ---------------------------------------------------------------------------------------------
