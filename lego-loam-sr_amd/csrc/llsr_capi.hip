@@ -330,6 +330,7 @@ static size_t layout(DevBufs& d, char* p0, int B, int H, int HW) {
   d.db_adj = carve<uint32_t>(p, (size_t)B * kAdjCap * kAdjWords);
   d.mt0 = carve<uint32_t>(p, 624);
   d.phantom = carve<int>(p, (size_t)B);
+  d.seg_zero = carve<int>(p, (size_t)B);
   return (size_t)(p - p0);
 }
 
@@ -487,6 +488,7 @@ extern "C" int32_t llsr_reset_state(llsr_handle* h) {
   HIP_OK(h, hipMemsetAsync(h->d.picked, 0, n, h->stream));
   HIP_OK(h, hipMemsetAsync(h->d.clabel, 0, n, h->stream));
   HIP_OK(h, hipMemsetAsync(h->d.phantom, 0, sizeof(int) * (size_t)h->max_batch, h->stream));
+  HIP_OK(h, hipMemsetD32Async(h->d.seg_zero, h->dc.HW, (size_t)h->max_batch, h->stream));
   HIP_OK(h, hipStreamSynchronize(h->stream));
   return LLSR_OK;
 }

@@ -85,6 +85,8 @@ struct DevBufs {
   uint32_t* db_adj;     // [B][kAdjCap][kAdjWords] eps-neighbourhood bitmask rows
   uint32_t* mt0;        // [624] RANSAC's mt19937 state after seed(12345) and its first twist
   int* phantom;         // [B] FA carry-over state: cloudSmoothness[4].ind (value is always 0)
+  int* seg_zero;        // [B] seg_ground / seg_col / seg_range are zero on [seg_zero, HW) (k_segment's
+                        // last S; HW after llsr_reset_state), so a batch clears only [S, seg_zero)
 };
 
 // C_HALF before k_fa_points when k_segment's first tile of cells holds no passing point

@@ -1313,8 +1313,12 @@ __global__ __launch_bounds__(1024) void k_segment(DevCfg c, const float4* __rest
     cnt[C_S] = S;
     cnt[C_O] = O;
   }
-  // CloudInfo arrays are H*W long and zero past S (IP:184-186); FA reads a few past S.
-  for (int k = S + tid; k < HW; k += nt) {
+  // CloudInfo arrays are H*W long and zero past S (IP:184-186); FA reads a few past S. They are
+  // zero past the slot's previous S already (d.seg_zero), so only [S, previous S) is cleared.
+  const int zend = min(d.seg_zero[b], HW);
+  __syncthreads();  // every thread read the old bound
+  if (tid == 0) d.seg_zero[b] = S;
+  for (int k = S + tid; k < zend; k += nt) {
     d.seg_ground[base + k] = 0;
     d.seg_col[base + k] = 0u;
     d.seg_range[base + k] = 0.0f;
