@@ -35,6 +35,7 @@ __global__ void k_select_ring(DevCfg, DevBufs);
 __global__ void k_vox_pcl(DevCfg, DevBufs);
 __global__ void k_debug_exact_sort(const float*, int, int*, long long*);
 __global__ void k_debug_exact_sort32(const uint32_t*, int, int*);
+__global__ void k_debug_half_passed(const float*, int, uint8_t*);
 __global__ void k_fa_concat(DevCfg, DevBufs);
 __global__ void k_dbscan_adj(DevCfg, DevBufs, const float4* __restrict__);
 __global__ void k_vis_clouds(DevCfg, DevBufs, int, float4*, int*);
@@ -659,6 +660,30 @@ extern "C" int32_t llsr_debug_exact_sort32(const uint32_t* ranks, int32_t n, int
   return rc;
 }
 
+// Diagnostics (not part of the ABI header): adjustDistortion's halfPassed test (FA:578-586) as
+// k_segment evaluates it, for n (y, x, start) triples: out[3 i] = the certified fast test's code
+// (0 fails, 1 passes, 2 undecided), out[3 i + 1] = its decision with the exact fallback, out[3 i + 2] =
+// the exact libm test.
+extern "C" int32_t llsr_debug_half_passed(const float* yxs, int32_t n, uint8_t* out) {
+  if (!yxs || !out || n < 0 || n > (1 << 24)) return LLSR_EINVAL;
+  if (n == 0) return LLSR_OK;
+  float* dv = nullptr;
+  uint8_t* dout = nullptr;
+  if (hipMalloc(&dv, sizeof(float) * 3 * (size_t)n) != hipSuccess) return LLSR_ENODEV;
+  if (hipMalloc(&dout, 3 * (size_t)n) != hipSuccess) { (void)hipFree(dv); return LLSR_ENODEV; }
+  int32_t rc = LLSR_OK;
+  if (hipMemcpy(dv, yxs, sizeof(float) * 3 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess) rc = LLSR_EIO;
+  if (rc == LLSR_OK) {
+    k_debug_half_passed<<<(n + 255) / 256, 256>>>(dv, n, dout);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(out, dout, 3 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = LLSR_EIO;
+  }
+  (void)hipFree(dv);
+  (void)hipFree(dout);
+  return rc;
+}
+
 // Diagnostics (not part of the ABI header): mean device ms of one block_introsort of vals[0, n)
 // by one 256-thread workgroup (k_debug_exact_sort), over `reps` launches.
 extern "C" float llsr_debug_exact_sort_ms(const float* vals, int32_t n, int32_t reps) {
@@ -774,7 +799,7 @@ extern "C" float llsr_debug_phase_ms(llsr_handle* h, int32_t k, int32_t phase, i
         else k_dbscan_merge<2048><<<B, 64, 0, s>>>(c, h->d);
         break;
       case 7: launch_fa_points(c, h->d, B, s); break;
-      case 6: k_segment<<<B, per_scan_threads(c), 0, s>>>(c, nullptr, nullptr, h->d); break;
+      case 6: k_segment<<<B, per_scan_threads(c), 0, s>>>(c, h->last_pts, h->last_off, h->d); break;
       case 5:
         if (c.ccl_lds) k_label<true><<<B, 1024, label_lds(c), s>>>(c, h->d);
         else k_label<false><<<B, 1024, label_band_lds(c), s>>>(c, h->d);

@@ -1155,6 +1155,17 @@ __device__ __attribute__((noinline)) bool half_passed_exact(float y, float x, fl
   return half_passed(-atan2f_(y, x), start);
 }
 
+// Diagnostics (llsr_debug_half_passed): per (y, x, start) triple the fast test's code (0 / 1 / 2 =
+// fails / passes / undecided), half_passed_any and the exact test
+__global__ void k_debug_half_passed(const float* yxs, int n, uint8_t* out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const float y = yxs[3 * t], x = yxs[3 * t + 1], st = yxs[3 * t + 2];
+  out[3 * t] = (uint8_t)half_passed_fast(y, x, st);
+  out[3 * t + 1] = half_passed_any(y, x, st) ? 1 : 0;
+  out[3 * t + 2] = half_passed_exact(y, x, st) ? 1 : 0;
+}
+
 // ---------------------------------------------------------------------------------------------
 // K6 segmented / outlier extraction (IP:791-832) + findStartEndAngle (IP:430-445).
 // Row-major block compaction; ring start/end indices fall out of the running count at each

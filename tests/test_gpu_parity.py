@@ -258,3 +258,32 @@ def test_half_passed_latch_outside_first_tile(require_gpu):
             failures.append((s, mode, errs))
     pipe.close()
     assert not failures, "\n".join(f"seed {s} ({m}):\n  " + "\n  ".join(e) for s, m, e in failures)
+
+
+def test_half_passed_fast_test_certified(require_gpu):
+    """k_segment's halfPassed test (FA:578-586): the fast atan2 decision, wherever it decides, equals
+    the exact libm test, on random triples and on points within 1e-4 rad of the four cut points
+    (o - start = -pi, -pi/2, pi, 3 pi / 2) and on the axes; half_passed_any always equals it."""
+    import ctypes as C
+    from llsr import lib
+    f = lib().llsr_debug_half_passed
+    f.restype, f.argtypes = C.c_int32, [C.c_void_p, C.c_int32, C.c_void_p]
+    rng = np.random.default_rng(7)
+    n = 1 << 20
+    start = rng.uniform(-np.pi, np.pi, n)
+    o = rng.uniform(-np.pi, np.pi, n)
+    m = n // 2  # half of them near a cut point, the angle wrapped back into (-pi, pi]
+    cut = rng.choice([-np.pi, -np.pi / 2, np.pi, 1.5 * np.pi], m)
+    o[:m] = start[:m] + cut + rng.uniform(-1e-4, 1e-4, m) * rng.choice([1.0, 1e-3, 1e-6], m)
+    o = np.angle(np.exp(1j * o))
+    r = rng.uniform(0.5, 80.0, n)
+    y, x = r * np.sin(-o), r * np.cos(-o)  # o = -atan2(y, x)
+    x[:64], y[64:128], x[128:136], y[128:136] = 0.0, 0.0, 0.0, 0.0  # axes and the origin
+    yxs = np.stack([y, x, start], axis=1).astype(np.float32)
+    out = np.zeros((n, 3), np.uint8)
+    assert f(yxs.ctypes.data, n, out.ctypes.data) == 0
+    fast, anyd, exact = out[:, 0], out[:, 1], out[:, 2]
+    decided = fast != 2
+    assert np.array_equal(fast[decided], exact[decided])
+    assert np.array_equal(anyd, exact)
+    assert decided[m:].mean() > 0.99  # the random half: the fast test decides nearly all
