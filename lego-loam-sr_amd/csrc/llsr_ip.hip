@@ -691,16 +691,23 @@ __global__ __launch_bounds__(1024) void k_ground_elev_ransac(DevCfg c, DevBufs d
   __shared__ int ncnt[2][kC * 16 + 1];
   const int nw = nt >> 6, wv = tid >> 6, ln = lane_id();
   int par = 0;
+  // the next tile's ground flags are loaded before this tile's barriers (one load latency per tile
+  // instead of two: the points' loads depend on the flags)
+  int8_t gn[kC];
+#pragma unroll
+  for (int u = 0; u < kC; ++u) gn[u] = u * nt + tid < HW ? g[u * nt + tid] : (int8_t)0;
   for (int t0 = 0; t0 < HW; t0 += kC * nt, par ^= 1) {
     int8_t gv[kC];
 #pragma unroll
-    for (int u = 0; u < kC; ++u) {
-      const int cell = t0 + u * nt + tid;
-      gv[u] = cell < HW ? g[cell] : (int8_t)0;
-    }
+    for (int u = 0; u < kC; ++u) gv[u] = gn[u];
     float4 p[kC];
 #pragma unroll
     for (int u = 0; u < kC; ++u) p[u] = gv[u] == 1 ? full[t0 + u * nt + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < kC; ++u) {
+      const int cell = t0 + kC * nt + u * nt + tid;
+      gn[u] = cell < HW ? g[cell] : (int8_t)0;
+    }
     bool nearc[kC];
     float depth[kC];
     unsigned long long mN[kC];
@@ -824,12 +831,20 @@ __global__ __launch_bounds__(1024) void k_ground_elev_ransac(DevCfg c, DevBufs d
   int ninl = 0;
   if (sh_int[5]) {
     const float cf[4] = {best_cf[0], best_cf[1], best_cf[2], best_cf[3]};
-    for (int k = tid; k < K; k += nt) {
-      const float4 q = nearp[k];
-      if ((double)ransac_dist(cf, q) < 0.5) {
+    constexpr int kF = 4;  // points per lane with their loads in flight together
+    for (int k0 = 0; k0 < K; k0 += kF * nt) {
+      float4 q[kF];
+#pragma unroll
+      for (int u = 0; u < kF; ++u) {
+        const int k = k0 + u * nt + tid;
+        q[u] = k < K ? nearp[k] : make_float4(0.f, 0.f, 0.f, -1.f);
+      }
+#pragma unroll
+      for (int u = 0; u < kF; ++u) {
+        if (q[u].w < 0.0f || !((double)ransac_dist(cf, q[u]) < 0.5)) continue;
         ++ninl;
-        const int cell = (int)q.w;
-        const float depth = sqrt_(q.x * q.x + q.y * q.y);  // the near cloud holds the cell's x, y, z
+        const int cell = (int)q[u].w;
+        const float depth = sqrt_(q[u].x * q[u].x + q[u].y * q[u].y);  // the near cloud holds the cell's x, y, z
         if ((double)depth <= 5) g[cell] = 1;
       }
     }
