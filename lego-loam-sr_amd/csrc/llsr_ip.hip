@@ -1106,22 +1106,43 @@ __global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
   // theirs, their own row included, with atomics.
   const int R = c.lbl_band;
   unsigned long long* rowA = d.ccl_b + base;
-  for (int cell = tid; cell < HW; cell += nt) {
-    const int v = lab[cell];
-    if (v >= -1 || uf_find(P, cell) != cell) continue;  // -1, a member, or a joined band root
-    rowA[cell] = (unsigned long long)(v & 0xffff) << ((cell / W) / R * R);
-    lab[cell] = (int)(0x80000000u | (((unsigned)v >> 16) & 0x7fffu));
+  // the cell sweeps below take kU cells per lane with their loads in flight together (one global
+  // load latency per kU cells: nearly every cell only needs its word to be skipped)
+  constexpr int kU = 8;
+  for (int c0 = 0; c0 < HW; c0 += kU * nt) {
+    int v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int cell = c0 + u * nt + tid;
+      v[u] = cell < HW ? lab[cell] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int cell = c0 + u * nt + tid;
+      if (v[u] >= -1 || uf_find(P, cell) != cell) continue;  // -1, a member, or a joined band root
+      rowA[cell] = (unsigned long long)(v[u] & 0xffff) << ((cell / W) / R * R);
+      lab[cell] = (int)(0x80000000u | (((unsigned)v[u] >> 16) & 0x7fffu));
+    }
   }
   __syncthreads();
-  for (int cell = tid; cell < HW; cell += nt) {
-    const int v = lab[cell];
-    if (v >= -1 || P.ld(cell) == cell) continue;  // only band roots joined to another seed
-    const int gr = uf_find(P, cell);
-    const int row = cell / W;
-    __hip_atomic_fetch_add(&lab[gr], (int)(((unsigned)v >> 16) & 0x7fffu), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_fetch_or(&rowA[gr], ((unsigned long long)(v & 0xffff) << (row / R * R)) | (1ull << row),
-                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  for (int c0 = 0; c0 < HW; c0 += kU * nt) {
+    int v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int cell = c0 + u * nt + tid;
+      v[u] = cell < HW ? lab[cell] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int cell = c0 + u * nt + tid;
+      if (v[u] >= -1 || P.ld(cell) == cell) continue;  // only band roots joined to another seed
+      const int gr = uf_find(P, cell);
+      const int row = cell / W;
+      __hip_atomic_fetch_add(&lab[gr], (int)(((unsigned)v[u] >> 16) & 0x7fffu), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_or(&rowA[gr], ((unsigned long long)(v[u] & 0xffff) << (row / R * R)) | (1ull << row),
+                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
   }
   __syncthreads();
   // feasibility and rank of feasible seeds in row-major order: tiles of 4 consecutive cells per
@@ -1153,11 +1174,24 @@ __global__ __launch_bounds__(1024) void k_label(DevCfg c, DevBufs d) {
   __syncthreads();
   // every label-0 cell takes its seed's label (a seed's own word may already hold the final value:
   // both forms read the same through the mask)
-  for (int cell = tid; cell < HW; cell += nt) {
-    const int v = lab[cell];
-    if (v == -1) continue;
-    const int gr = uf_find(P, v >= 0 ? v : cell);
-    lab[cell] = __hip_atomic_load(&lab[gr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & 0x7fffffff;
+  for (int c0 = 0; c0 < HW; c0 += kU * nt) {
+    int v[kU], gr[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int cell = c0 + u * nt + tid;
+      v[u] = cell < HW ? lab[cell] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int cell = c0 + u * nt + tid;
+      gr[u] = v[u] == -1 ? -1 : uf_find(P, v[u] >= 0 ? v[u] : cell);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int cell = c0 + u * nt + tid;
+      if (gr[u] >= 0)
+        lab[cell] = __hip_atomic_load(&lab[gr[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & 0x7fffffff;
+    }
   }
 }
 
